@@ -1,0 +1,164 @@
+/*
+ * ecx.h -- C ABI of the MI355X GF(256) erasure engine (libecx.so).
+ *
+ * This is the drop-in boundary for the reference's coding path
+ * (krishnarb3/repair-pipelining, rs/ + clay/ + lrc/).  Every entry point
+ * names the reference interface it replaces (file:line; file legend in
+ * SURVEY.md section 0.1).  A JVM binding (JNI) maps byte[] / ByteBuffer onto
+ * these plain pointers; see INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every function returns int: 0 (ECX_OK) or a non-negative result on
+ *     success, a negative ECX_E_* code where the Java code throws.
+ *     ecx_last_error() gives the thread-local message.
+ *   - "Host" entry points take caller-owned host buffers (the Java byte[][]
+ *     of the reference) and run the arithmetic on the current HIP device:
+ *     the bytes are staged to HBM, one fused kernel applies the composed
+ *     GF(256) map, and the results are copied back.  There is no CPU
+ *     arithmetic fallback: without a usable device they return ECX_E_DEVICE.
+ *   - "Batch" entry points take DEVICE pointers (HBM-resident stripes) and a
+ *     hipStream_t passed as void*; they only enqueue work.
+ *   - Byte order / layout: a shard or sub-chunk is `byte_count` contiguous
+ *     bytes.  Clay stripes are plane-major as in the reference
+ *     (ClayCodeErasureDecodingStep.java:84-97): input slot z*n + node,
+ *     output slot z*|E| + j.
+ *   - Thread safety: all entry points may be called concurrently; codec
+ *     objects are immutable after creation except for their internal,
+ *     lock-protected map cache.
+ */
+#ifndef ECX_H
+#define ECX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status */
+enum ecx_status {
+    ECX_OK = 0,
+    ECX_E_ILLEGAL_ARGUMENT = -1,  /* IllegalArgumentException (sizes, offsets, counts)  */
+    ECX_E_NOT_ENOUGH_SHARDS = -2, /* "Not enough shards present"  ReedSolomon.java:211-213 */
+    ECX_E_SINGULAR = -3,          /* "Matrix is singular"          Matrix.java:311-313      */
+    ECX_E_TOO_MANY_SHARDS = -4,   /* "too many shards - max is 256" ReedSolomon.java:48-50  */
+    ECX_E_INDEX = -5,             /* ArrayIndexOutOfBoundsException (e.g. Clay (k+m)%m!=0) */
+    ECX_E_NULL = -6,              /* NullPointerException (decodeMissingSingle, bug B3)    */
+    ECX_E_NOMEM = -7,             /* host or device allocation failed                      */
+    ECX_E_DEVICE = -10            /* no HIP device / HIP runtime error                     */
+};
+
+const char *ecx_status_string(int status);
+const char *ecx_last_error(void);
+int ecx_version(void);
+
+/* ---------------------------------------------------------------- device */
+int ecx_device_count(int *count);
+int ecx_set_device(int device);     /* per calling thread */
+int ecx_synchronize(void *stream);  /* hipStreamSynchronize(stream) */
+
+/* ---------------------------------------------------------------- Galois.java (host planner) */
+int ecx_gf_multiply(int a, int b);               /* Galois.multiply  Galois.java:199-209 */
+int ecx_gf_divide(int a, int b);                 /* Galois.divide    Galois.java:214-228 */
+int ecx_gf_exp(int a, int n);                    /* Galois.exp       Galois.java:239-254 */
+int ecx_gf_tables(int16_t *log_table /*256*/, uint8_t *exp_table /*510*/,
+                  uint8_t *mul_table /*65536*/); /* Galois.java:59,103,178 */
+
+/* ---------------------------------------------------------------- Matrix.java (host planner) */
+int ecx_matrix_times(const uint8_t *a, int a_rows, int a_cols, const uint8_t *b, int b_rows, int b_cols,
+                     uint8_t *out);                              /* Matrix.times   Matrix.java:193-210 */
+int ecx_matrix_invert(const uint8_t *m, int n, uint8_t *out);   /* Matrix.invert  Matrix.java:273-346 */
+
+/* ---------------------------------------------------------------- CodingLoop.java (host, GPU-executed) */
+/* CodingLoop.codeSomeShards (CodingLoop.java:79-85; default implementation
+ * InputOutputByteTableCodingLoop.java:12-44): outputs[o][offset..+byte_count) =
+ * sum_i matrix_rows[o*input_count + i] * inputs[i][...].  Outputs are overwritten. */
+int ecx_code_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inputs, int input_count,
+                         uint8_t *const *outputs, int output_count, int offset, int byte_count);
+/* CodingLoop.checkSomeShards (CodingLoop.java:110-117): 1 if to_check equals the
+ * coded outputs, 0 otherwise.  temp_buffer is accepted for signature parity and unused. */
+int ecx_check_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inputs, int input_count,
+                          const uint8_t *const *to_check, int check_count, int offset, int byte_count,
+                          uint8_t *temp_buffer);
+/* InputOutputByteTableCodingLoopSingle.codeSomeShards (…Single.java:4-20):
+ * output (=, or ^= when !is_first_time) matrix_rows[output_index*row_length + index] * input. */
+int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *input, int index,
+                    uint8_t *output, int output_index, int offset, int byte_count, int is_first_time);
+
+/* ---------------------------------------------------------------- ReedSolomon.java */
+typedef struct ecx_rs ecx_rs;
+int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out); /* ReedSolomon.create :34-61 */
+void ecx_rs_destroy(ecx_rs *rs);
+int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out /* total x data */); /* buildMatrix :373-385 */
+int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int offset,
+                         int byte_count);                            /* encodeParity :94-108 */
+int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *output, int input_index,
+                                int output_index, int offset, int byte_count); /* :110-118 */
+int ecx_rs_is_parity_correct(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length,
+                             int first_byte, int byte_count, uint8_t *temp_buffer,
+                             int temp_length);                       /* isParityCorrect :129-178 */
+int ecx_rs_decode_missing(ecx_rs *rs, uint8_t *const *shards, const uint8_t *shard_present, int shard_count,
+                          int shard_length, int offset, int byte_count); /* decodeMissing :189-286 */
+/* decodeMissingSingle :288-333.  outputs[j] are caller arrays written in place
+ * (assigned when is_first, XOR-accumulated otherwise). */
+int ecx_rs_decode_missing_single(ecx_rs *rs, const uint8_t *shard, int shard_index, int index,
+                                 const uint8_t *shard_present, uint8_t *const *outputs, int output_count,
+                                 int offset, int byte_count, int is_first);
+
+/* ---------------------------------------------------------------- compiled GF maps (device batch) */
+/* An ecx_map is one composed GF(256) linear map (a code + erasure pattern),
+ * compiled into the kernel's table format and resident on the device.
+ * Batch layout: input slot j of stripe s is at in + s*in_stripe_stride + in_slot[j]*in_slot_stride;
+ * output row o goes to out + s*out_stripe_stride + out_slot[o]*out_slot_stride. */
+typedef struct ecx_map ecx_map;
+int ecx_map_create(const uint8_t *matrix /* n_out x n_in */, int n_out, int n_in, const int *in_slot,
+                   const int *out_slot, ecx_map **out);
+void ecx_map_destroy(ecx_map *map);
+int ecx_map_info(const ecx_map *map, int *n_out, int *n_in, int *nnz);
+int ecx_map_matrix(const ecx_map *map, uint8_t *matrix /* n_out x n_in */, int *in_slot, int *out_slot);
+int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                        uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                        int64_t byte_count, void *stream);
+
+/* Maps of the codec entry points (owned by the codec; do not destroy). */
+int ecx_rs_encode_map(ecx_rs *rs, const ecx_map **out);              /* encodeParity, slots = shard index */
+int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **out); /* decodeMissing */
+
+/* ---------------------------------------------------------------- ClayCodeErasureDecodingStep.java */
+typedef struct ecx_clay ecx_clay;
+/* new ClayCodeErasureDecodingStep(erasedIndexes, RS(2,2), RS(k,m)) -- ClayCode.java:28-41, :43-51 */
+int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_erased, ecx_clay **out);
+void ecx_clay_destroy(ecx_clay *clay);
+int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha); /* ClayCodeUtil :690-695 */
+int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out /* alpha */); /* :924-941 */
+/* performCoding(ECChunk[],ECChunk[]) -- ClayCodeErasureDecodingStep.java:53-107.
+ * inputs: n*alpha host pointers, NULL = absent; outputs: n_erased*alpha host pointers. */
+int ecx_clay_perform_coding(ecx_clay *clay, const uint8_t *const *inputs, uint8_t *const *outputs, int buf_size);
+/* doDecodeSingle overload 2 (:225-282), as driven per helper plane by
+ * ClayCodeHelper.getHelperPlanesAndDecode (ClayCodeHelper.kt:19-56).
+ * helper_coupled: [num_helper_planes][n] host pointers; outputs: alpha host pointers. */
+int ecx_clay_decode_single_helper(ecx_clay *clay, const uint8_t *const *helper_coupled, int helper_i,
+                                  uint8_t *const *outputs, int erased_index, int buf_size);
+/* The composed performCoding map for the standard null pattern (erased nodes
+ * absent, every other sub-chunk present): input slot z*n+node, output slot z*|E|+j. */
+int ecx_clay_map(ecx_clay *clay, const ecx_map **out);
+/* Batched device-resident performCoding over nstripes stripes: stripe s holds
+ * n*alpha sub-chunks of buf_size bytes at in + s*in_stripe_stride + slot*in_sub_stride
+ * and receives |E|*alpha sub-chunks at out + s*out_stripe_stride + slot*out_sub_stride. */
+int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
+                                  int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
+                                  int64_t out_sub_stride, int64_t nstripes, int64_t buf_size, void *stream);
+
+/* ---------------------------------------------------------------- synthetic data / verification (device) */
+/* Deterministic counter-based fill: byte i of the region = f(seed, i). */
+int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream);
+/* Count bytes that differ between two strided sets of nrows rows of row_bytes each;
+ * result accumulated into *d_count (device uint64). */
+int ecx_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
+                       int64_t row_bytes, uint64_t *d_count, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,565 @@
+"""repair_pipelining_amd -- MI355X-native GF(256) erasure engine.
+
+Host-side mirror of the reference's coding API (krishnarb3/repair-pipelining:
+rs/ ``com.backblaze.erasure``, clay/ ``distributed.erasure.coding.clay``,
+lrc/ ``distributed.erasure.coding``) over the C ABI of libecx.so
+(include/ecx.h).  Method names, argument meaning and error behaviour follow
+the Java classes; byte[] becomes a 1-D ``numpy.uint8`` array and Java
+exceptions become :class:`EcxError` carrying the ecx_status code.
+
+All arithmetic runs in hand-written HIP kernels on the MI355X; the host side
+only plans (GF tables, matrix inverses, the composed Clay map).  There is no
+CPU fallback.
+
+Batch (device-resident) APIs take torch CUDA tensors or raw device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from ._lib import EcxError, build, check, lib, LIB_PATH, HEADER  # noqa: F401
+
+__all__ = [
+    "EcxError", "Galois", "Matrix", "CodingLoop", "InputOutputByteTableCodingLoop",
+    "InputOutputByteTableCodingLoopSingle", "ReedSolomon", "GfMap", "ClayCodeUtil",
+    "ClayCodeErasureDecodingStep", "ClayCode", "LRCErasureCode", "LRCErasureUtil", "JavaRandom",
+    "lrc_encode", "lrc_encode_using_single", "lrc_decode", "sample_encode", "sample_decode",
+    "device_count", "set_device", "fill_random", "count_mismatch",
+]
+
+
+# ---------------------------------------------------------------- helpers
+def _u8(a) -> np.ndarray:
+    if not (isinstance(a, np.ndarray) and a.dtype == np.uint8 and a.flags.c_contiguous):
+        raise TypeError("byte buffers must be C-contiguous numpy.uint8 arrays")
+    return a
+
+
+def _ptr_array(bufs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * max(1, len(bufs)))()
+    for i, b in enumerate(bufs):
+        arr[i] = None if b is None else _u8(b).ctypes.data
+    return arr
+
+
+def _bytes(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.int64) & 0xFF, dtype=np.uint8)
+
+
+def _dev_ptr(x) -> int:
+    """Device pointer of a torch CUDA tensor or an int."""
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        if not x.is_cuda:
+            raise TypeError("batch APIs take device (CUDA/HIP) tensors")
+        return int(x.data_ptr())
+    raise TypeError("expected a device tensor or an integer pointer")
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        try:
+            import torch
+            return int(torch.cuda.current_stream().cuda_stream)
+        except Exception:  # pragma: no cover - no torch / no device
+            return None
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(lib().ecx_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def set_device(device: int) -> None:
+    check(lib().ecx_set_device(device))
+
+
+def fill_random(dst, nbytes: int, seed: int, stream=None) -> None:
+    """Deterministic counter-based synthetic bytes on the device (splitmix64)."""
+    check(lib().ecx_fill_random(_dev_ptr(dst), nbytes, seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))
+
+
+def count_mismatch(a, a_stride, b, b_stride, nrows, row_bytes, d_count, stream=None) -> None:
+    """Accumulate into the device uint64 ``d_count`` the bytes that differ."""
+    check(lib().ecx_count_mismatch(_dev_ptr(a), a_stride, None if b is None else _dev_ptr(b), b_stride, nrows,
+                                   row_bytes, _dev_ptr(d_count), _stream(stream)))
+
+
+# ---------------------------------------------------------------- Galois.java
+class Galois:
+    """GF(2^8) with generating polynomial 29 (Galois.java:43)."""
+    FIELD_SIZE = 256
+    GENERATING_POLYNOMIAL = 29
+
+    @staticmethod
+    def multiply(a: int, b: int) -> int:
+        return lib().ecx_gf_multiply(a & 0xFF, b & 0xFF)
+
+    @staticmethod
+    def divide(a: int, b: int) -> int:
+        return check(lib().ecx_gf_divide(a & 0xFF, b & 0xFF))
+
+    @staticmethod
+    def exp(a: int, n: int) -> int:
+        return check(lib().ecx_gf_exp(a & 0xFF, n))
+
+    @staticmethod
+    def add(a: int, b: int) -> int:
+        return (a ^ b) & 0xFF
+
+    subtract = add
+
+    @staticmethod
+    def tables():
+        log = np.zeros(256, np.int16)
+        exp = np.zeros(510, np.uint8)
+        mul = np.zeros((256, 256), np.uint8)
+        check(lib().ecx_gf_tables(log.ctypes.data, exp.ctypes.data, mul.ctypes.data))
+        return log, exp, mul
+
+
+# ---------------------------------------------------------------- Matrix.java
+class Matrix:
+    @staticmethod
+    def times(a, b) -> np.ndarray:
+        a, b = _bytes(a), _bytes(b)
+        out = np.zeros((a.shape[0], b.shape[1]), np.uint8)
+        check(lib().ecx_matrix_times(a.ctypes.data, a.shape[0], a.shape[1], b.ctypes.data, b.shape[0], b.shape[1],
+                                     out.ctypes.data))
+        return out
+
+    @staticmethod
+    def invert(m) -> np.ndarray:
+        m = _bytes(m)
+        out = np.zeros_like(m)
+        check(lib().ecx_matrix_invert(m.ctypes.data, m.shape[0], out.ctypes.data))
+        return out
+
+
+# ---------------------------------------------------------------- CodingLoop.java
+class CodingLoop:
+    """The reference's operator/plugin interface (CodingLoop.java:79-117),
+    implemented by one fused HIP kernel launch per call."""
+
+    def codeSomeShards(self, matrixRows, inputs, inputCount, outputs, outputCount, offset, byteCount):
+        m = _bytes([list(matrixRows[o])[:inputCount] for o in range(outputCount)]).reshape(outputCount, inputCount)
+        check(lib().ecx_code_some_shards(m.ctypes.data, _ptr_array(inputs[:inputCount]), inputCount,
+                                         _ptr_array(outputs[:outputCount]), outputCount, offset, byteCount))
+
+    def checkSomeShards(self, matrixRows, inputs, inputCount, toCheck, checkCount, offset, byteCount,
+                        tempBuffer=None) -> bool:
+        m = _bytes([list(matrixRows[o])[:inputCount] for o in range(checkCount)]).reshape(checkCount, inputCount)
+        return bool(check(lib().ecx_check_some_shards(m.ctypes.data, _ptr_array(inputs[:inputCount]), inputCount,
+                                                      _ptr_array(toCheck[:checkCount]), checkCount, offset,
+                                                      byteCount, None)))
+
+
+InputOutputByteTableCodingLoop = CodingLoop  # the default loop of ReedSolomon.create (ReedSolomon.java:35)
+
+
+class InputOutputByteTableCodingLoopSingle:
+    """InputOutputByteTableCodingLoopSingle.java:4-20."""
+
+    def codeSomeShards(self, matrixRows, input, index, output, outputIndex, offset, byteCount, isFirstTime):
+        rows = [list(r) for r in matrixRows]
+        width = max(len(r) for r in rows)
+        m = _bytes([r + [0] * (width - len(r)) for r in rows])
+        check(lib().ecx_code_single(m.ctypes.data, width, _u8(input).ctypes.data, index, _u8(output).ctypes.data,
+                                    outputIndex, offset, byteCount, 1 if isFirstTime else 0))
+
+
+# ---------------------------------------------------------------- compiled maps
+class GfMap:
+    """A compiled GF(256) linear map resident on the device (ecx_map)."""
+
+    def __init__(self, handle, owner=None, owned=False):
+        self._h = handle
+        self._owner = owner  # keeps a codec alive while its maps are used
+        self._owned = owned
+
+    @classmethod
+    def from_matrix(cls, matrix, in_slot=None, out_slot=None) -> "GfMap":
+        m = _bytes(matrix)
+        n_out, n_in = m.shape
+        ins = None if in_slot is None else np.ascontiguousarray(in_slot, np.int32)
+        outs = None if out_slot is None else np.ascontiguousarray(out_slot, np.int32)
+        h = ctypes.c_void_p()
+        check(lib().ecx_map_create(m.ctypes.data, n_out, n_in, None if ins is None else ins.ctypes.data,
+                                   None if outs is None else outs.ctypes.data, ctypes.byref(h)))
+        g = cls(h, owned=True)
+        g._keep = (ins, outs)
+        return g
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and self._h and lib is not None:
+            lib().ecx_map_destroy(self._h)
+            self._h = None
+
+    def info(self):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().ecx_map_info(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"n_out": a.value, "n_in": b.value, "nnz": c.value}
+
+    def matrix(self):
+        """(dense matrix n_out x n_in, in_slot, out_slot) of the composed map."""
+        inf = self.info()
+        m = np.zeros((inf["n_out"], inf["n_in"]), np.uint8)
+        ins = np.zeros(max(1, inf["n_in"]), np.int32)
+        outs = np.zeros(max(1, inf["n_out"]), np.int32)
+        check(lib().ecx_map_matrix(self._h, m.ctypes.data, ins.ctypes.data, outs.ctypes.data))
+        return m, ins[:inf["n_in"]].copy(), outs[:inf["n_out"]].copy()
+
+    def apply_batch(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                    byte_count, stream=None):
+        check(lib().ecx_map_apply_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_slot_stride, _dev_ptr(out),
+                                        out_stripe_stride, out_slot_stride, nstripes, byte_count, _stream(stream)))
+
+
+# ---------------------------------------------------------------- ReedSolomon.java
+class ReedSolomon:
+    """ReedSolomon.java: systematic RS over GF(2^8), Vandermonde-derived."""
+
+    def __init__(self, dataShardCount: int, parityShardCount: int, codingLoop=None):
+        h = ctypes.c_void_p()
+        check(lib().ecx_rs_create(dataShardCount, parityShardCount, ctypes.byref(h)))
+        self._h = h
+        self.dataShardCount = dataShardCount
+        self.parityShardCount = parityShardCount
+        self.totalShardCount = dataShardCount + parityShardCount
+
+    @classmethod
+    def create(cls, dataShardCount: int, parityShardCount: int) -> "ReedSolomon":
+        return cls(dataShardCount, parityShardCount)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ecx_rs_destroy(self._h)
+            self._h = None
+
+    def getDataShardCount(self):
+        return self.dataShardCount
+
+    def getParityShardCount(self):
+        return self.parityShardCount
+
+    def getTotalShardCount(self):
+        return self.totalShardCount
+
+    @property
+    def matrix(self) -> np.ndarray:
+        out = np.zeros((self.totalShardCount, self.dataShardCount), np.uint8)
+        check(lib().ecx_rs_matrix(self._h, out.ctypes.data))
+        return out
+
+    @property
+    def parityRows(self) -> np.ndarray:
+        return self.matrix[self.dataShardCount:]
+
+    @staticmethod
+    def _len(shards):
+        return len(shards[0]) if len(shards) and shards[0] is not None else 0
+
+    def encodeParity(self, shards, offset: int, byteCount: int) -> None:
+        check(lib().ecx_rs_encode_parity(self._h, _ptr_array(shards), len(shards), self._len(shards), offset,
+                                         byteCount))
+
+    def encodeParitySingle(self, shard, output, inputIndex, outputIndex, offset, byteCount) -> None:
+        check(lib().ecx_rs_encode_parity_single(self._h, _u8(shard).ctypes.data, _u8(output).ctypes.data,
+                                                inputIndex, outputIndex, offset, byteCount))
+
+    def isParityCorrect(self, shards, firstByte: int, byteCount: int, tempBuffer=None) -> bool:
+        t = None if tempBuffer is None else _u8(tempBuffer).ctypes.data
+        tl = 0 if tempBuffer is None else len(tempBuffer)
+        return bool(check(lib().ecx_rs_is_parity_correct(self._h, _ptr_array(shards), len(shards),
+                                                         self._len(shards), firstByte, byteCount, t, tl)))
+
+    def decodeMissing(self, shards, shardPresent, offset: int, byteCount: int) -> None:
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        check(lib().ecx_rs_decode_missing(self._h, _ptr_array(shards), pres.ctypes.data, len(shards),
+                                          self._len(shards), offset, byteCount))
+
+    def decodeMissingSingle(self, shard, shardIndex, index, shardPresent, outputs, offset, byteCount,
+                            isFirst) -> None:
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        check(lib().ecx_rs_decode_missing_single(self._h, _u8(shard).ctypes.data, shardIndex, index,
+                                                 pres.ctypes.data, _ptr_array(outputs), len(outputs), offset,
+                                                 byteCount, 1 if isFirst else 0))
+
+    # batched, device-resident
+    def encode_map(self) -> GfMap:
+        h = ctypes.c_void_p()
+        check(lib().ecx_rs_encode_map(self._h, ctypes.byref(h)))
+        return GfMap(h, owner=self)
+
+    def decode_map(self, shardPresent) -> GfMap:
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        h = ctypes.c_void_p()
+        check(lib().ecx_rs_decode_map(self._h, pres.ctypes.data, ctypes.byref(h)))
+        return GfMap(h, owner=self)
+
+
+# ---------------------------------------------------------------- Clay
+class ClayCodeUtil:
+    """ClayCodeErasureDecodingStep.ClayCodeUtil (:676-944) index arithmetic."""
+
+    def __init__(self, erasedIndexes, numDataUnits, numParityUnits):
+        self.q = numParityUnits
+        self.t = (numParityUnits + numDataUnits) // numParityUnits
+        self.erasedIndexes = list(erasedIndexes)
+        self.subPacketSize = self.q ** self.t
+
+    def getSubPacketSize(self):
+        return self.subPacketSize
+
+    def getZVector(self, z):
+        v = [0] * self.t
+        for i in range(self.t - 1, -1, -1):
+            v[i] = z % self.q
+            z //= self.q
+        return v
+
+    def getZ(self, v):
+        z = 0
+        for x in v:
+            z = z * self.q + x
+        return z
+
+    def getNodeIndex(self, x, y):
+        return x + self.q * y
+
+    def getNodeCoordinates(self, i):
+        return [i % self.q, i // self.q]
+
+    def getCouplePlaneIndex(self, coordinates, z):
+        v = self.getZVector(z)
+        v[coordinates[1]] = coordinates[0]
+        return self.getZ(v)
+
+    def getHelperPlanesIndexes(self, k):
+        x, y = self.getNodeCoordinates(k)
+        return [z for z in range(self.subPacketSize) if self.getZVector(z)[y] == x]
+
+
+class ClayCodeErasureDecodingStep:
+    """new ClayCodeErasureDecodingStep(erasedIndexes, RS(2,2), RS(k,m)) (:43-51)."""
+
+    def __init__(self, erasedIndexes, numDataUnits: int, numParityUnits: int):
+        er = np.ascontiguousarray(list(erasedIndexes), np.int32)
+        h = ctypes.c_void_p()
+        check(lib().ecx_clay_create(numDataUnits, numParityUnits, er.ctypes.data, len(er), ctypes.byref(h)))
+        self._h = h
+        self.erasedIndexes = list(erasedIndexes)
+        self.numDataUnits, self.numParityUnits = numDataUnits, numParityUnits
+        self.numTotalUnits = numDataUnits + numParityUnits
+        q, t, a = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().ecx_clay_geometry(h, ctypes.byref(q), ctypes.byref(t), ctypes.byref(a)))
+        self.q, self.t, self.subPacketSize = q.value, t.value, a.value
+        self.util = ClayCodeUtil(erasedIndexes, numDataUnits, numParityUnits)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ecx_clay_destroy(self._h)
+            self._h = None
+
+    def getHelperPlanesIndexes(self, erasedIndex: int):
+        out = np.zeros(self.subPacketSize, np.int32)
+        n = check(lib().ecx_clay_helper_planes(self._h, erasedIndex, out.ctypes.data))
+        return [int(x) for x in out[:n]]
+
+    def performCoding(self, inputs, outputs, bufSize: Optional[int] = None) -> None:
+        """inputs: n*alpha (plane-major, None = absent); outputs: |E|*alpha arrays."""
+        if len(inputs) != self.numTotalUnits * self.subPacketSize:
+            raise EcxError(-1, "Invalid inputs length")
+        if len(outputs) != len(self.erasedIndexes) * self.subPacketSize:
+            raise EcxError(-1, "Invalid outputs length")
+        if bufSize is None:
+            first = next((b for b in inputs if b is not None), None)
+            if first is None:
+                raise EcxError(-1, "Invalid inputs are found, all being null")
+            bufSize = len(first)
+        check(lib().ecx_clay_perform_coding(self._h, _ptr_array(inputs), _ptr_array(outputs), bufSize))
+
+    def doDecodeSingleHelper(self, helperCoupledPlanes, helperIndex: int, outputs, erasedIndex: int,
+                             bufSize: int) -> None:
+        """doDecodeSingle overload 2 (:225-282): helperCoupledPlanes[nh][n], outputs[alpha]."""
+        flat = [b for row in helperCoupledPlanes for b in row]
+        check(lib().ecx_clay_decode_single_helper(self._h, _ptr_array(flat), helperIndex, _ptr_array(outputs),
+                                                  erasedIndex, bufSize))
+
+    def map(self) -> GfMap:
+        h = ctypes.c_void_p()
+        check(lib().ecx_clay_map(self._h, ctypes.byref(h)))
+        return GfMap(h, owner=self)
+
+    def performCodingBatch(self, inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
+                           nstripes, bufSize, stream=None) -> None:
+        check(lib().ecx_clay_perform_coding_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_sub_stride,
+                                                  _dev_ptr(out), out_stripe_stride, out_sub_stride, nstripes,
+                                                  bufSize, _stream(stream)))
+
+
+class JavaRandom:
+    """java.util.Random (JDK specification), for ClayCode.getInputs."""
+
+    def __init__(self, seed: int):
+        self.seed = (seed ^ 0x5DEECE66D) & ((1 << 48) - 1)
+
+    def _next(self, bits):
+        self.seed = (self.seed * 0x5DEECE66D + 0xB) & ((1 << 48) - 1)
+        r = self.seed >> (48 - bits)
+        return r - (1 << bits) if r >= 1 << (bits - 1) else r
+
+    def nextInt(self):
+        return self._next(32)
+
+    def nextBytes(self, n: int) -> np.ndarray:
+        out = np.zeros(n, np.uint8)
+        i = 0
+        while i < n:
+            rnd = self.nextInt() & 0xFFFFFFFF
+            for _ in range(min(4, n - i)):
+                out[i] = rnd & 0xFF
+                rnd >>= 8
+                i += 1
+        return out
+
+
+class ClayCode:
+    """ClayCode.java facade: RS(2,2) pair transform + RS(k,m) per plane."""
+
+    def __init__(self, numDataUnits, numParityUnits, blockSize, erasedIndexes):
+        self.numDataUnits, self.numParityUnits, self.blockSize = numDataUnits, numParityUnits, blockSize
+        self.erasedIndexes = list(erasedIndexes)
+        self.erasureDecodingStep = ClayCodeErasureDecodingStep(erasedIndexes, numDataUnits, numParityUnits)
+        self.clayCodeUtil = ClayCodeUtil(erasedIndexes, numDataUnits, numParityUnits)
+
+    def performCoding(self, inputs, outputs):
+        self.erasureDecodingStep.performCoding(inputs, outputs, self.blockSize)
+
+    def getInputs(self):
+        """ClayCode.getInputs (ClayCode.java:47-77): Random(123456).nextBytes per data sub-chunk."""
+        n = self.numDataUnits + self.numParityUnits
+        a = self.clayCodeUtil.getSubPacketSize()
+        r = JavaRandom(123456)
+        out = [None] * (n * a)
+        counter = 0
+        for i in range(n):
+            for j in range(a):
+                k = i * a + j
+                if counter < self.numDataUnits:
+                    out[k] = r.nextBytes(self.blockSize)
+                counter = (counter + 1) % n
+        return out
+
+    def getOutputs(self):
+        return [np.zeros(self.blockSize, np.uint8) for _ in range(len(self.erasedIndexes) *
+                                                                 self.clayCodeUtil.getSubPacketSize())]
+
+    def encode(self, inputs, outputs):
+        """ClayCode.encode (:89-99) -- meaningful with erasedIndexes = parity nodes."""
+        step = ClayCodeErasureDecodingStep(self.erasedIndexes, self.numDataUnits, self.numParityUnits)
+        step.performCoding(inputs, outputs, self.blockSize)
+        return inputs, outputs
+
+
+# ---------------------------------------------------------------- LRC (lrc/)
+class LRCErasureUtil:
+    N = 16
+    K = 12
+    R = 3
+
+
+class LRCErasureCode:
+    """LRCErasureCode.kt:5-9 -- RS(R,1) local parity (coefficients [1,1,1]: XOR)."""
+
+    def __init__(self):
+        self.rs = ReedSolomon.create(LRCErasureUtil.R, 1)
+
+    def encodeParitySingle(self, shard, output, index, blockSize):
+        self.rs.encodeParitySingle(shard, output, index, 0, 0, blockSize)
+
+
+def lrc_encode(data: np.ndarray):
+    """LRCErasureCodeExample.encode (:30-57): K blocks -> N blocks (group g: 3 data + parity)."""
+    U = LRCErasureUtil
+    block = len(data) // U.K
+    rs = ReedSolomon.create(U.R, 1)
+    out, pos = [], 0
+    for _ in range(U.K // U.R):
+        shards = []
+        for _ in range(U.R):
+            shards.append(np.ascontiguousarray(data[pos:pos + block], np.uint8).copy())
+            pos += block
+        shards.append(np.zeros(block, np.uint8))
+        rs.encodeParity(shards, 0, block)
+        out.extend(shards)
+    return out
+
+
+def lrc_encode_using_single(data: np.ndarray):
+    """LRCErasureCodeExample.encodeUsingSingle (:59-90)."""
+    U = LRCErasureUtil
+    block = len(data) // U.K
+    code = LRCErasureCode()
+    out, pos = [], 0
+    for _ in range(U.K // U.R):
+        shards = []
+        for _ in range(U.R):
+            shards.append(np.ascontiguousarray(data[pos:pos + block], np.uint8).copy())
+            pos += block
+        acc = np.zeros(block, np.uint8)
+        for idx in range(U.R):
+            code.rs.encodeParitySingle(shards[idx], acc, idx, 0, 0, block)
+        shards.append(acc)
+        out.extend(shards)
+    return out
+
+
+def lrc_decode(blocks, missingIndices: Iterable[int], blockSize: int):
+    """LRCErasureCodeExample.decode (:92-131): returns (file bytes, repaired blocks)."""
+    U = LRCErasureUtil
+    missing = set(missingIndices)
+    rs = ReedSolomon.create(U.R, 1)
+    shards = [np.array(blocks[i], np.uint8) if (i not in missing and blocks[i] is not None)
+              else np.zeros(blockSize, np.uint8) for i in range(U.N)]
+    for g in range(U.K // U.R):
+        lo = g * (U.R + 1)
+        present = [(lo + j) not in missing for j in range(U.R + 1)]
+        rs.decodeMissing(shards[lo:lo + U.R + 1], present, 0, blockSize)
+    data = [shards[i] for i in range(U.N) if i == 0 or (i + 1) % (U.R + 1) != 0]
+    return np.concatenate(data), shards
+
+
+# ---------------------------------------------------------------- SampleEncoder / SampleDecoder
+def sample_encode(file_bytes: np.ndarray, data_shards: int = 4, parity_shards: int = 2):
+    """SampleEncoder.java:54-83: [int32 BE length][file][zero pad] -> data shards + RS parity."""
+    size = len(file_bytes)
+    shard = (size + 4 + data_shards - 1) // data_shards
+    allb = np.zeros(shard * data_shards, np.uint8)
+    allb[:4] = np.frombuffer(int(size).to_bytes(4, "big"), np.uint8)
+    allb[4:4 + size] = file_bytes
+    shards = [allb[i * shard:(i + 1) * shard].copy() for i in range(data_shards)]
+    shards += [np.zeros(shard, np.uint8) for _ in range(parity_shards)]
+    ReedSolomon.create(data_shards, parity_shards).encodeParity(shards, 0, shard)
+    return shards
+
+
+def sample_decode(shards: Sequence[Optional[np.ndarray]], data_shards: int = 4, parity_shards: int = 2):
+    """SampleDecoder.java:34-98: decodeMissing, then strip the length header."""
+    present = [s is not None for s in shards]
+    if sum(present) < data_shards:
+        raise EcxError(-2, "Not enough shards present")
+    size = next(len(s) for s in shards if s is not None)
+    work = [np.array(s, np.uint8) if s is not None else np.zeros(size, np.uint8) for s in shards]
+    ReedSolomon.create(data_shards, parity_shards).decodeMissing(work, present, 0, size)
+    allb = np.concatenate(work[:data_shards])
+    n = int.from_bytes(allb[:4].tobytes(), "big")
+    return allb[4:4 + n].copy(), work

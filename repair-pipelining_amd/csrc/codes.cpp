@@ -1,0 +1,395 @@
+// codes.cpp -- see codes.hpp.
+#include "codes.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace ecx {
+
+namespace {
+
+SymBuf zeros(int w) { return std::make_shared<std::vector<uint8_t>>((size_t)w, 0); }
+
+SymBuf unit(int w, int j) {
+    SymBuf b = zeros(w);
+    (*b)[(size_t)j] = 1;
+    return b;
+}
+
+SymBuf clone(const SymBuf &b) { return std::make_shared<std::vector<uint8_t>>(*b); }
+
+// y ^= c * x  (one GF(256) multiply-accumulate per coefficient)
+void axpy(std::vector<uint8_t> &y, uint8_t c, const std::vector<uint8_t> &x) {
+    if (!c) return;
+    const uint8_t *t = Field::get().row(c);
+    for (size_t i = 0; i < y.size(); ++i) y[i] ^= t[x[i]];
+}
+
+}  // namespace
+
+int LinearMap::nnz() const {
+    int s = 0;
+    for (uint8_t v : a) s += v != 0;
+    return s;
+}
+
+LinearMap LinearMap::pruned() const {
+    std::vector<int> keep;
+    for (int j = 0; j < n_in; ++j)
+        for (int o = 0; o < n_out; ++o)
+            if (at(o, j)) {
+                keep.push_back(j);
+                break;
+            }
+    LinearMap r;
+    r.n_out = n_out;
+    r.n_in = (int)keep.size();
+    r.out_slot = out_slot;
+    r.a.assign((size_t)r.n_out * r.n_in, 0);
+    for (int jj = 0; jj < r.n_in; ++jj) {
+        r.in_slot.push_back(in_slot[keep[jj]]);
+        for (int o = 0; o < n_out; ++o) r.a[(size_t)o * r.n_in + jj] = at(o, keep[jj]);
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------- RsCode
+RsCode::RsCode(int data_shards, int parity_shards) : k_(data_shards), m_(parity_shards) {
+    if (256 < data_shards + parity_shards) throw Error(ECX_E_TOO_MANY_SHARDS, "too many shards - max is 256");
+    if (data_shards <= 0 || parity_shards < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid shard counts");
+    const Field &f = Field::get();
+    const int n = k_ + m_;
+    Matrix v(n, k_);  // Vandermonde V[r][c] = r^c (0^0 = 1)
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < k_; ++c) v.at(r, c) = f.pow((uint8_t)r, c);
+    Matrix top(k_, k_);
+    for (int r = 0; r < k_; ++r)
+        for (int c = 0; c < k_; ++c) top.at(r, c) = v.at(r, c);
+    gen_ = v * top.inverse();
+}
+
+Matrix RsCode::data_decoder(const std::vector<bool> &present, std::vector<int> *rows_used) const {
+    Matrix sub(k_, k_);
+    int r = 0;
+    for (int i = 0; i < n() && r < k_; ++i)
+        if (present[i]) {
+            std::copy(gen_.row(i), gen_.row(i) + k_, sub.row(r));
+            if (rows_used) rows_used->push_back(i);
+            ++r;
+        }
+    if (r < k_) throw Error(ECX_E_NOT_ENOUGH_SHARDS, "Not enough shards present");
+    return sub.inverse();
+}
+
+void RsCode::decode_missing(std::vector<SymBuf> &shards, const std::vector<bool> &present) const {
+    int np = 0;
+    for (int i = 0; i < n(); ++i) np += present[i] ? 1 : 0;
+    if (np == n()) return;
+    if (np < k_) throw Error(ECX_E_NOT_ENOUGH_SHARDS, "Not enough shards present");
+    std::vector<int> used;
+    const Matrix dec = data_decoder(present, &used);
+    // Missing data shards from the k "sub shards" (the first k present).
+    for (int i = 0; i < k_; ++i) {
+        if (present[i]) continue;
+        std::vector<uint8_t> acc(shards[i]->size(), 0);
+        for (int r = 0; r < k_; ++r) axpy(acc, dec.at(i, r), *shards[used[r]]);
+        *shards[i] = std::move(acc);
+    }
+    // Missing parity shards from all data shards (now complete).
+    for (int p = 0; p < m_; ++p) {
+        if (present[k_ + p]) continue;
+        std::vector<uint8_t> acc(shards[k_ + p]->size(), 0);
+        for (int i = 0; i < k_; ++i) axpy(acc, parity_row(p)[i], *shards[i]);
+        *shards[k_ + p] = std::move(acc);
+    }
+}
+
+LinearMap RsCode::encode_map() const {
+    LinearMap mp;
+    mp.n_out = m_;
+    mp.n_in = k_;
+    mp.a.assign((size_t)m_ * k_, 0);
+    for (int p = 0; p < m_; ++p) std::copy(parity_row(p), parity_row(p) + k_, mp.a.begin() + (size_t)p * k_);
+    for (int i = 0; i < k_; ++i) mp.in_slot.push_back(i);
+    for (int p = 0; p < m_; ++p) mp.out_slot.push_back(k_ + p);
+    return mp;
+}
+
+LinearMap RsCode::decode_map(const std::vector<bool> &present) const {
+    const int w = n();
+    std::vector<SymBuf> sh(w);
+    for (int i = 0; i < w; ++i) sh[i] = present[i] ? unit(w, i) : zeros(w);
+    decode_missing(sh, present);
+    LinearMap mp;
+    mp.n_in = w;
+    for (int i = 0; i < w; ++i) mp.in_slot.push_back(i);
+    for (int i = 0; i < w; ++i) {
+        if (present[i]) continue;
+        mp.out_slot.push_back(i);
+        mp.a.insert(mp.a.end(), sh[i]->begin(), sh[i]->end());
+    }
+    mp.n_out = (int)mp.out_slot.size();
+    return mp.pruned();
+}
+
+// ---------------------------------------------------------------- ClayPlanner
+namespace {
+int ipow(int b, int e) {
+    int r = 1;
+    while (e-- > 0) r *= b;
+    return r;
+}
+}  // namespace
+
+ClayPlanner::ClayPlanner(int data_units, int parity_units, std::vector<int> erased)
+    : k_(data_units), m_(parity_units), erased_(std::move(erased)), pair_(2, 2), rs_(data_units, parity_units) {
+    if (parity_units <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "parity units must be positive");
+    q_ = parity_units;
+    t_ = (parity_units + data_units) / parity_units;  // integer division, ClayCodeUtil :692
+    if (t_ > 16) throw Error(ECX_E_ILLEGAL_ARGUMENT, "sub-packetization too large");
+    alpha_ = ipow(q_, t_);
+    if ((long long)n() * alpha_ > 16384)
+        throw Error(ECX_E_ILLEGAL_ARGUMENT, "n*alpha > 16384 sub-chunks per stripe is beyond the planner");
+}
+
+std::vector<int> ClayPlanner::zvec(int z) const {
+    std::vector<int> v(t_);
+    for (int i = t_ - 1; i >= 0; --i) {
+        v[i] = z % q_;
+        z /= q_;
+    }
+    return v;
+}
+
+int ClayPlanner::zindex(const std::vector<int> &v) const {
+    int z = 0;
+    for (int i = 0; i < t_; ++i) z = z * q_ + v[i];
+    return z;
+}
+
+int ClayPlanner::couple_plane(int x, int y, int z) const {
+    std::vector<int> v = zvec(z);
+    if (y >= t_) throw Error(ECX_E_INDEX, "node outside the q x t grid");
+    v[y] = x;
+    return zindex(v);
+}
+
+bool ClayPlanner::is_erased(int idx) const { return std::find(erased_.begin(), erased_.end(), idx) != erased_.end(); }
+
+int ClayPlanner::erasure_type(int idx, int z) const {
+    const std::vector<int> v = zvec(z);
+    const int x = nx(idx), y = ny(idx);
+    if (y >= t_) throw Error(ECX_E_INDEX, "node outside the q x t grid");
+    if (v[y] == x) return 0;
+    return is_erased(node(v[y], y)) ? 2 : 1;
+}
+
+int ClayPlanner::intersection_score(int z) const {
+    const std::vector<int> v = zvec(z);
+    int s = 0;
+    for (int e : erased_) {
+        if (ny(e) >= t_) throw Error(ECX_E_INDEX, "node outside the q x t grid");
+        s += v[ny(e)] == nx(e);
+    }
+    return s;
+}
+
+std::vector<int> ClayPlanner::helper_planes(int e) const {
+    const int x = nx(e), y = ny(e);
+    if (e < 0 || y >= t_) throw Error(ECX_E_INDEX, "erased node outside the q x t grid");
+    std::vector<int> out;
+    for (int z = 0; z < alpha_; ++z)
+        if (zvec(z)[y] == x) out.push_back(z);
+    return out;
+}
+
+// The Clay pair transform as RS(2,2) over (A, A', B, B') = (C(z,i), C(z',i'), U(z,i), U(z',i'))
+// with exactly two unknown (null) entries; returns the array at the first null
+// position (getPairWiseCouple, :630-666; callers use outputs[0] only).
+SymBuf ClayPlanner::pair_couple(SymBuf a, SymBuf a2, SymBuf b, SymBuf b2, int width) const {
+    std::vector<SymBuf> arr = {a, a2, b, b2};
+    int lost[2] = {0, 0}, nl = 0;
+    for (int i = 0; i < 4; ++i)
+        if (!arr[i]) {
+            if (nl == 2) throw Error(ECX_E_INDEX, "more than two unknowns in a coupled pair");
+            lost[nl++] = i;
+        }
+    for (auto &p : arr)
+        if (!p) p = zeros(width);
+    std::vector<bool> present(4, true);
+    present[lost[0]] = present[lost[1]] = false;
+    pair_.decode_missing(arr, present);
+    return arr[lost[0]];
+}
+
+// decodeDecoupledPlane (:542-597), default (non-isTest) branch.
+void ClayPlanner::decode_plane(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width) const {
+    int nulls = 0;
+    for (auto &p : plane) nulls += !p;
+    if (nulls > (int)erased.size()) throw Error(ECX_E_INDEX, "more absent shards than erasures in a plane");
+    std::vector<SymBuf> arr(plane.size());
+    for (size_t i = 0; i < plane.size(); ++i) arr[i] = plane[i] ? plane[i] : zeros(width);
+    std::vector<bool> present(plane.size(), true);
+    for (int e : erased)
+        if (e < (int)plane.size()) present[e] = false;
+    rs_.decode_missing(arr, present);
+    for (int e : erased) plane[e] = arr[e];
+    for (auto &p : plane)
+        if (!p) throw Error(ECX_E_NULL, "absent shard in a decoupled plane");
+}
+
+// Body of both doDecodeSingle overloads for helper plane i (:171-203, :255-281).
+void ClayPlanner::single_plane(const std::vector<SymBuf> &helper, const std::vector<int> &hidx, int i, int e,
+                               std::vector<SymBuf> &outputs, int width) const {
+    const int nn = n(), z = hidx[i], ey = ny(e);
+    const std::vector<int> v = zvec(z);
+    std::vector<SymBuf> plane(nn);
+    for (int j = 0; j < q_ * t_; ++j) {  // getDecoupledHelperPlane :435-492
+        const int x = nx(j), y = ny(j);
+        if (y == ey) continue;
+        if (v[y] == x) {
+            plane[j] = helper[(size_t)i * nn + j];
+        } else {
+            const int cz = couple_plane(x, y, z);
+            int chp = 0;
+            for (size_t h = 0; h < hidx.size(); ++h)
+                if (hidx[h] == cz) {
+                    chp = (int)h;
+                    break;
+                }
+            const int cc = node(v[y], y);
+            plane[j] = clone(pair_couple(helper[(size_t)i * nn + j], helper[(size_t)chp * nn + cc], nullptr, nullptr,
+                                         width));
+        }
+    }
+    std::vector<int> column;
+    for (int x = 0; x < q_; ++x) column.push_back(node(x, ey));
+    decode_plane(plane, column, width);
+    for (int x = 0; x < q_; ++x) {
+        const int nd = node(x, ey);
+        if (nd == e) {
+            outputs[z] = clone(plane[nd]);
+        } else {
+            const int cz = couple_plane(x, ey, z);
+            outputs[cz] = clone(pair_couple(nullptr, helper[(size_t)i * nn + nd], nullptr, plane[nd], width));
+        }
+    }
+}
+
+// doDecodeMulti (:311-421); `in` is the method's private newIn[][] copy.
+void ClayPlanner::decode_multi(std::vector<SymBuf> in, std::vector<SymBuf> &outputs, int width) const {
+    const int nn = n(), ne = (int)erased_.size();
+    int max_is = 0;
+    for (int z = 0; z < alpha_; ++z) max_is = std::max(max_is, intersection_score(z));
+    for (int is = 0; is <= max_is; ++is) {
+        std::vector<int> zs;
+        for (int z = 0; z < alpha_; ++z)
+            if (intersection_score(z) == is) zs.push_back(z);
+        if (zs.empty()) continue;
+        std::vector<std::vector<SymBuf>> temp(zs.size(), std::vector<SymBuf>(nn));
+        for (size_t j = 0; j < zs.size(); ++j) {
+            const int z = zs[j];
+            const std::vector<int> v = zvec(z);
+            for (int i = 0; i < q_ * t_; ++i) {  // getDecoupledPlane :500-534
+                const int x = nx(i), y = ny(i);
+                if (!in[(size_t)z * nn + i]) continue;
+                if (v[y] == x) {
+                    temp[j][i] = in[(size_t)z * nn + i];
+                } else {
+                    const int cz = couple_plane(x, y, z), cc = node(v[y], y);
+                    temp[j][i] = clone(pair_couple(in[(size_t)z * nn + i], in[(size_t)cz * nn + cc], nullptr, nullptr,
+                                                   width));
+                }
+            }
+            decode_plane(temp[j], erased_, width);
+        }
+        for (size_t j = 0; j < zs.size(); ++j) {
+            const int z = zs[j];
+            for (int kk = 0; kk < ne; ++kk) {
+                const int e = erased_[kk];
+                const int type = erasure_type(e, z);
+                if (type == 0) {
+                    in[(size_t)z * nn + e] = temp[j][e];
+                    outputs[(size_t)z * ne + kk] = clone(temp[j][e]);
+                    continue;
+                }
+                const std::vector<int> v = zvec(z);
+                const int cz = couple_plane(nx(e), ny(e), z);
+                const int cidx = node(v[ny(e)], ny(e));
+                SymBuf o;
+                if (type == 1) {
+                    o = pair_couple(nullptr, in[(size_t)cz * nn + cidx], temp[j][e], nullptr, width);
+                } else {
+                    auto it = std::find(zs.begin(), zs.end(), cz);
+                    if (it == zs.end()) throw Error(ECX_E_INDEX, "couple plane not in the current IS batch");
+                    o = pair_couple(nullptr, nullptr, temp[j][e], temp[it - zs.begin()][cidx], width);
+                }
+                in[(size_t)z * nn + e] = clone(o);
+                outputs[(size_t)z * ne + kk] = clone(o);
+            }
+        }
+    }
+}
+
+LinearMap ClayPlanner::perform_coding_map(const std::vector<bool> &input_present) const {
+    const int nn = n(), ne = (int)erased_.size();
+    const int width = nn * alpha_;
+    if ((int)input_present.size() != width) throw Error(ECX_E_ILLEGAL_ARGUMENT, "Invalid inputs length");
+    LinearMap mp;
+    mp.n_in = width;
+    for (int j = 0; j < width; ++j) mp.in_slot.push_back(j);
+    if (ne == 0) return mp;
+    if (std::none_of(input_present.begin(), input_present.end(), [](bool b) { return b; }))
+        throw Error(ECX_E_ILLEGAL_ARGUMENT, "Invalid inputs are found, all being null");
+    for (int e : erased_)
+        if (e < 0 || e >= nn) throw Error(ECX_E_INDEX, "erased index out of range");
+    std::vector<SymBuf> in(width);
+    for (int j = 0; j < width; ++j)
+        if (input_present[j]) in[j] = unit(width, j);
+    std::vector<SymBuf> outputs((size_t)ne * alpha_);
+    if (ne == 1) {
+        const int e = erased_[0];
+        const std::vector<int> hidx = helper_planes(e);
+        std::vector<SymBuf> helper(hidx.size() * nn);
+        for (size_t h = 0; h < hidx.size(); ++h)  // getHelperPlanes :291-300
+            for (int j = 0; j < nn; ++j) helper[h * nn + j] = in[(size_t)hidx[h] * nn + j];
+        for (size_t i = 0; i < hidx.size(); ++i) single_plane(helper, hidx, (int)i, e, outputs, width);
+    } else {
+        decode_multi(in, outputs, width);
+    }
+    mp.n_out = ne * alpha_;
+    for (int o = 0; o < mp.n_out; ++o) {
+        if (!outputs[o]) throw Error(ECX_E_INDEX, "output sub-chunk never written");
+        mp.out_slot.push_back(o);
+        mp.a.insert(mp.a.end(), outputs[o]->begin(), outputs[o]->end());
+    }
+    return mp.pruned();
+}
+
+LinearMap ClayPlanner::decode_single_helper_map(const std::vector<bool> &helper_present, int helper_i,
+                                                int erased_index, std::vector<bool> *written) const {
+    const int nn = n();
+    const std::vector<int> hidx = helper_planes(erased_index);
+    const int width = (int)hidx.size() * nn;
+    if ((int)helper_present.size() != width) throw Error(ECX_E_ILLEGAL_ARGUMENT, "helper plane array size");
+    if (helper_i < 0 || helper_i >= (int)hidx.size()) throw Error(ECX_E_INDEX, "helper plane index");
+    std::vector<SymBuf> helper(width);
+    for (int j = 0; j < width; ++j)
+        if (helper_present[j]) helper[j] = unit(width, j);
+    std::vector<SymBuf> outputs(alpha_);
+    single_plane(helper, hidx, helper_i, erased_index, outputs, width);
+    LinearMap mp;
+    mp.n_in = width;
+    for (int j = 0; j < width; ++j) mp.in_slot.push_back(j);
+    if (written) written->assign(alpha_, false);
+    for (int z = 0; z < alpha_; ++z) {
+        if (!outputs[z]) continue;
+        if (written) (*written)[z] = true;
+        mp.out_slot.push_back(z);
+        mp.a.insert(mp.a.end(), outputs[z]->begin(), outputs[z]->end());
+    }
+    mp.n_out = (int)mp.out_slot.size();
+    return mp.pruned();
+}
+
+}  // namespace ecx

@@ -1,0 +1,107 @@
+// codes.hpp -- the planner: Reed-Solomon, Clay and LRC repair/encode composed
+// into single GF(256) linear maps.
+//
+// Every reference stage (ReedSolomon.decodeMissing, the Clay pair transform,
+// the per-plane RS decode, re-coupling, ...) is linear over GF(2^8) and acts on
+// every byte position independently with the same coefficients.  The planner
+// therefore runs the reference's stage SEQUENCE once on symbolic buffers --
+// each buffer is its coefficient vector over the input slots -- and the result
+// is the exact linear map the JVM path computes for ANY input bytes (valid
+// codewords or not).  Aliasing and in-place writes follow the Java object
+// semantics (SymBuf = shared pointer), so that corner cases such as
+// non-null erased inputs in the multi-erasure path compose identically.
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "gf.hpp"
+
+namespace ecx {
+
+// A dense composed map: out[o] = sum_j a[o][j] * in[j]; in_slot / out_slot are
+// the slot indices of the caller's layout the rows / columns refer to.
+struct LinearMap {
+    int n_out = 0, n_in = 0;
+    std::vector<uint8_t> a;  // n_out x n_in
+    std::vector<int> in_slot, out_slot;
+    uint8_t at(int o, int j) const { return a[(size_t)o * n_in + j]; }
+    int nnz() const;
+    // Drop all-zero columns (inputs the map never reads).
+    LinearMap pruned() const;
+};
+
+using SymBuf = std::shared_ptr<std::vector<uint8_t>>;
+
+// ReedSolomon.java: systematic code built from Vandermonde * inv(top k rows)
+// (buildMatrix / vandermonde, ReedSolomon.java:373-404).
+class RsCode {
+public:
+    RsCode(int data_shards, int parity_shards);
+    int k() const { return k_; }
+    int m() const { return m_; }
+    int n() const { return k_ + m_; }
+    const Matrix &matrix() const { return gen_; }
+    const uint8_t *parity_row(int p) const { return gen_.row(k_ + p); }
+
+    // decodeMissing's row selection (ReedSolomon.java:224-244): the first k
+    // present rows in ascending order, and the inverse of their submatrix.
+    Matrix data_decoder(const std::vector<bool> &present, std::vector<int> *rows_used) const;
+
+    LinearMap encode_map() const;                                  // encodeParity :94-108
+    LinearMap decode_map(const std::vector<bool> &present) const;  // decodeMissing :189-286
+
+    // decodeMissing on symbolic shards, writing the non-present shard objects in place.
+    void decode_missing(std::vector<SymBuf> &shards, const std::vector<bool> &present) const;
+
+private:
+    int k_, m_;
+    Matrix gen_;
+};
+
+// ClayCodeErasureDecodingStep.java + ClayCodeUtil (:676-944), symbolically.
+class ClayPlanner {
+public:
+    ClayPlanner(int data_units, int parity_units, std::vector<int> erased);
+    int k() const { return k_; }
+    int m() const { return m_; }
+    int n() const { return k_ + m_; }
+    int q() const { return q_; }
+    int t() const { return t_; }
+    int alpha() const { return alpha_; }
+    const std::vector<int> &erased() const { return erased_; }
+
+    std::vector<int> helper_planes(int erased_index) const;  // getHelperPlanesIndexes :924-941
+
+    // performCoding (:64-107) for a given null pattern of the n*alpha inputs:
+    // returns the map (rows = |E|*alpha outputs, columns = n*alpha input slots).
+    LinearMap perform_coding_map(const std::vector<bool> &input_present) const;
+    // doDecodeSingle overload 2 (:225-282) for helper plane i: columns are the
+    // nh*n helper_coupled slots, rows are the alpha output planes (only the q
+    // planes this helper plane writes are non-empty; `written` marks them).
+    LinearMap decode_single_helper_map(const std::vector<bool> &helper_present, int helper_i, int erased_index,
+                                       std::vector<bool> *written) const;
+
+private:
+    int k_, m_, q_, t_, alpha_;
+    std::vector<int> erased_;
+    RsCode pair_, rs_;
+
+    std::vector<int> zvec(int z) const;
+    int zindex(const std::vector<int> &v) const;
+    int node(int x, int y) const { return x + q_ * y; }
+    int nx(int i) const { return i % q_; }
+    int ny(int i) const { return i / q_; }
+    int couple_plane(int x, int y, int z) const;
+    int erasure_type(int idx, int z) const;
+    int intersection_score(int z) const;
+    bool is_erased(int idx) const;
+
+    SymBuf pair_couple(SymBuf a, SymBuf a2, SymBuf b, SymBuf b2, int width) const;
+    void decode_plane(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width) const;
+    void single_plane(const std::vector<SymBuf> &helper, const std::vector<int> &hidx, int i, int e,
+                      std::vector<SymBuf> &outputs, int width) const;
+    void decode_multi(std::vector<SymBuf> in, std::vector<SymBuf> &outputs, int width) const;
+};
+
+}  // namespace ecx

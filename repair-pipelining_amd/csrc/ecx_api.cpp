@@ -1,0 +1,554 @@
+// ecx_api.cpp -- the C ABI (include/ecx.h).  Translates planner/HIP errors into
+// ecx_status codes; every arithmetic entry point executes on the HIP device.
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "engine.hpp"
+
+using namespace ecx;
+
+struct ecx_map {
+    explicit ecx_map(LinearMap m) : cm(std::move(m)) {}
+    CompiledMap cm;
+};
+
+struct ecx_rs {
+    explicit ecx_rs(int k, int m) : code(k, m) {}
+    RsCode code;
+    std::mutex mu;
+    std::unique_ptr<ecx_map> enc, check;
+    std::map<std::string, std::unique_ptr<ecx_map>> dec;
+};
+
+struct ecx_clay {
+    ecx_clay(int k, int m, std::vector<int> e) : pl(k, m, std::move(e)) {}
+    ClayPlanner pl;
+    std::mutex mu;
+    std::map<std::string, std::unique_ptr<ecx_map>> maps;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <class F>
+int guarded(F &&f) {
+    try {
+        return f();
+    } catch (const Error &e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_last_error = "out of memory";
+        return ECX_E_NOMEM;
+    } catch (const std::exception &e) {
+        g_last_error = e.what();
+        return ECX_E_ILLEGAL_ARGUMENT;
+    }
+}
+
+std::string key_of(const std::vector<bool> &v, int extra = 0) {
+    std::string s(v.size() + 8, '\0');
+    for (size_t i = 0; i < v.size(); ++i) s[i] = v[i] ? '1' : '0';
+    std::memcpy(&s[v.size()], &extra, sizeof(int));
+    return s;
+}
+
+// ReedSolomon.checkBuffersAndSizes, ReedSolomon.java:338-363.
+void check_buffers(const RsCode &c, uint8_t *const *shards, int shard_count, int shard_length, int offset,
+                   int byte_count) {
+    if (shard_count != c.n()) throw Error(ECX_E_ILLEGAL_ARGUMENT, "wrong number of shards: " + std::to_string(shard_count));
+    if (!shards) throw Error(ECX_E_NULL, "shards is null");
+    for (int i = 0; i < shard_count; ++i)
+        if (!shards[i]) throw Error(ECX_E_NULL, "shard " + std::to_string(i) + " is null");
+    if (offset < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "offset is negative: " + std::to_string(offset));
+    if (byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "byteCount is negative: " + std::to_string(byte_count));
+    if ((long long)shard_length < (long long)offset + byte_count)
+        throw Error(ECX_E_ILLEGAL_ARGUMENT, "buffers to small: " + std::to_string(byte_count) + std::to_string(offset));
+}
+
+LinearMap dense_map(const uint8_t *m, int n_out, int n_in) {
+    LinearMap lm;
+    lm.n_out = n_out;
+    lm.n_in = n_in;
+    lm.a.assign(m, m + (size_t)n_out * n_in);
+    for (int j = 0; j < n_in; ++j) lm.in_slot.push_back(j);
+    for (int o = 0; o < n_out; ++o) lm.out_slot.push_back(o);
+    return lm;
+}
+
+std::vector<bool> present_vec(const uint8_t *p, int n) {
+    std::vector<bool> v(n);
+    for (int i = 0; i < n; ++i) v[i] = p[i] != 0;
+    return v;
+}
+
+ecx_map *rs_decode_map(ecx_rs *rs, const std::vector<bool> &present) {
+    std::lock_guard<std::mutex> lk(rs->mu);
+    auto &slot = rs->dec[key_of(present)];
+    if (!slot) slot = std::make_unique<ecx_map>(rs->code.decode_map(present));
+    return slot.get();
+}
+
+ecx_map *clay_standard_map(ecx_clay *c) {
+    const int n = c->pl.n(), a = c->pl.alpha();
+    std::vector<bool> present((size_t)n * a, true);
+    for (int z = 0; z < a; ++z)
+        for (int e : c->pl.erased())
+            if (e >= 0 && e < n) present[(size_t)z * n + e] = false;
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto &slot = c->maps[key_of(present, -1)];
+    if (!slot) slot = std::make_unique<ecx_map>(c->pl.perform_coding_map(present));
+    return slot.get();
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *ecx_status_string(int s) {
+    switch (s) {
+    case ECX_OK: return "ok";
+    case ECX_E_ILLEGAL_ARGUMENT: return "IllegalArgumentException";
+    case ECX_E_NOT_ENOUGH_SHARDS: return "Not enough shards present";
+    case ECX_E_SINGULAR: return "Matrix is singular";
+    case ECX_E_TOO_MANY_SHARDS: return "too many shards - max is 256";
+    case ECX_E_INDEX: return "ArrayIndexOutOfBoundsException";
+    case ECX_E_NULL: return "NullPointerException";
+    case ECX_E_NOMEM: return "out of memory";
+    case ECX_E_DEVICE: return "HIP device error";
+    default: return "unknown status";
+    }
+}
+
+const char *ecx_last_error(void) { return g_last_error.c_str(); }
+int ecx_version(void) { return 100; }
+
+// ---------------------------------------------------------------- device
+int ecx_device_count(int *count) {
+    return guarded([&]() -> int {
+        int n = 0;
+        check_hip(hipGetDeviceCount(&n), "hipGetDeviceCount");
+        *count = n;
+        return ECX_OK;
+    });
+}
+
+int ecx_set_device(int device) {
+    return guarded([&]() -> int {
+        check_hip(hipSetDevice(device), "hipSetDevice");
+        return ECX_OK;
+    });
+}
+
+int ecx_synchronize(void *stream) {
+    return guarded([&]() -> int {
+        check_hip(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- Galois / Matrix
+int ecx_gf_multiply(int a, int b) { return Field::get().mul((uint8_t)a, (uint8_t)b); }
+
+int ecx_gf_divide(int a, int b) {
+    return guarded([&]() -> int { return (int)Field::get().div((uint8_t)a, (uint8_t)b); });
+}
+
+int ecx_gf_exp(int a, int n) {
+    return guarded([&]() -> int {
+        if (n < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative exponent");
+        return (int)Field::get().pow((uint8_t)a, n);
+    });
+}
+
+int ecx_gf_tables(int16_t *log_table, uint8_t *exp_table, uint8_t *mul_table) {
+    const Field &f = Field::get();
+    if (log_table)
+        for (int i = 0; i < 256; ++i) log_table[i] = f.log((uint8_t)i);
+    if (exp_table)
+        for (int i = 0; i < 510; ++i) exp_table[i] = f.exp(i);
+    if (mul_table)
+        for (int a = 0; a < 256; ++a) std::memcpy(mul_table + 256 * a, f.row((uint8_t)a), 256);
+    return ECX_OK;
+}
+
+int ecx_matrix_times(const uint8_t *a, int ar, int ac, const uint8_t *b, int br, int bc, uint8_t *out) {
+    return guarded([&]() -> int {
+        Matrix A(ar, ac), B(br, bc);
+        std::memcpy(A.row(0), a, (size_t)ar * ac);
+        std::memcpy(B.row(0), b, (size_t)br * bc);
+        Matrix C = A * B;
+        std::memcpy(out, C.row(0), (size_t)ar * bc);
+        return ECX_OK;
+    });
+}
+
+int ecx_matrix_invert(const uint8_t *m, int n, uint8_t *out) {
+    return guarded([&]() -> int {
+        Matrix A(n, n);
+        std::memcpy(A.row(0), m, (size_t)n * n);
+        Matrix I = A.inverse();
+        std::memcpy(out, I.row(0), (size_t)n * n);
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- CodingLoop
+int ecx_code_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inputs, int input_count,
+                         uint8_t *const *outputs, int output_count, int offset, int byte_count) {
+    return guarded([&]() -> int {
+        if (input_count <= 0 || output_count < 0 || offset < 0 || byte_count < 0)
+            throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
+        CompiledMap cm(dense_map(matrix_rows, output_count, input_count).pruned());
+        run_host(cm, inputs, outputs, offset, byte_count);
+        // Rows with every coefficient zero have no entries but are still written (as zeros) by the kernel.
+        return ECX_OK;
+    });
+}
+
+int ecx_check_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inputs, int input_count,
+                          const uint8_t *const *to_check, int check_count, int offset, int byte_count,
+                          uint8_t *temp_buffer) {
+    (void)temp_buffer;
+    return guarded([&]() -> int {
+        if (input_count <= 0 || check_count < 0 || offset < 0 || byte_count < 0)
+            throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
+        // row o: sum_i M[o][i]*in[i] + 1*to_check[o] == 0  <=>  to_check[o] is correct
+        const int w = input_count + check_count;
+        LinearMap lm;
+        lm.n_out = check_count;
+        lm.n_in = w;
+        lm.a.assign((size_t)check_count * w, 0);
+        for (int o = 0; o < check_count; ++o) {
+            std::memcpy(&lm.a[(size_t)o * w], matrix_rows + (size_t)o * input_count, (size_t)input_count);
+            lm.a[(size_t)o * w + input_count + o] = 1;
+            lm.out_slot.push_back(o);
+        }
+        for (int j = 0; j < w; ++j) lm.in_slot.push_back(j);
+        std::vector<const uint8_t *> ptrs(inputs, inputs + input_count);
+        ptrs.insert(ptrs.end(), to_check, to_check + check_count);
+        CompiledMap cm(lm.pruned());
+        return run_host_all_zero(cm, ptrs.data(), offset, byte_count) ? 1 : 0;
+    });
+}
+
+int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *input, int index, uint8_t *output,
+                    int output_index, int offset, int byte_count, int is_first_time) {
+    return guarded([&]() -> int {
+        if (index < 0 || index >= row_length || output_index < 0) throw Error(ECX_E_INDEX, "matrix index");
+        if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
+        const uint8_t c = matrix_rows[(size_t)output_index * row_length + index];
+        const uint8_t row[2] = {c, (uint8_t)(is_first_time ? 0 : 1)};
+        CompiledMap cm(dense_map(row, 1, 2));
+        const uint8_t *ins[2] = {input, output};
+        uint8_t *outs[1] = {output};
+        run_host(cm, ins, outs, offset, byte_count);
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- ReedSolomon
+int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out) {
+    return guarded([&]() -> int {
+        *out = nullptr;
+        *out = new ecx_rs(data_shards, parity_shards);
+        return ECX_OK;
+    });
+}
+
+void ecx_rs_destroy(ecx_rs *rs) { delete rs; }
+
+int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out) {
+    const Matrix &m = rs->code.matrix();
+    std::memcpy(out, m.row(0), (size_t)m.rows() * m.cols());
+    return ECX_OK;
+}
+
+int ecx_rs_encode_map(ecx_rs *rs, const ecx_map **out) {
+    return guarded([&]() -> int {
+        std::lock_guard<std::mutex> lk(rs->mu);
+        if (!rs->enc) rs->enc = std::make_unique<ecx_map>(rs->code.encode_map());
+        *out = rs->enc.get();
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **out) {
+    return guarded([&]() -> int {
+        std::vector<bool> present = present_vec(shard_present, rs->code.n());
+        int np = 0;
+        for (bool b : present) np += b;
+        if (np < rs->code.k()) throw Error(ECX_E_NOT_ENOUGH_SHARDS, "Not enough shards present");
+        *out = rs_decode_map(rs, present);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int offset,
+                         int byte_count) {
+    return guarded([&]() -> int {
+        check_buffers(rs->code, shards, shard_count, shard_length, offset, byte_count);
+        const ecx_map *m = nullptr;
+        int st = ecx_rs_encode_map(rs, &m);
+        if (st) return st;
+        run_host(const_cast<ecx_map *>(m)->cm, shards, shards, offset, byte_count);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *output, int input_index,
+                                int output_index, int offset, int byte_count) {
+    return guarded([&]() -> int {
+        const RsCode &c = rs->code;
+        if (output_index < 0 || output_index >= c.m() || input_index < 0 || input_index >= c.k())
+            throw Error(ECX_E_INDEX, "parity row / column index");
+        if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
+        const uint8_t row[2] = {c.parity_row(output_index)[input_index], 1};
+        CompiledMap cm(dense_map(row, 1, 2));
+        const uint8_t *ins[2] = {shard, output};
+        uint8_t *outs[1] = {output};
+        run_host(cm, ins, outs, offset, byte_count);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_is_parity_correct(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int first_byte,
+                             int byte_count, uint8_t *temp_buffer, int temp_length) {
+    return guarded([&]() -> int {
+        check_buffers(rs->code, shards, shard_count, shard_length, first_byte, byte_count);
+        if (temp_buffer && (long long)temp_length < (long long)first_byte + byte_count)
+            throw Error(ECX_E_ILLEGAL_ARGUMENT, "tempBuffer is not big enough");
+        const RsCode &c = rs->code;
+        ecx_map *m;
+        {
+            std::lock_guard<std::mutex> lk(rs->mu);
+            if (!rs->check) {
+                LinearMap lm;
+                lm.n_out = c.m();
+                lm.n_in = c.n();
+                lm.a.assign((size_t)c.m() * c.n(), 0);
+                for (int p = 0; p < c.m(); ++p) {
+                    std::memcpy(&lm.a[(size_t)p * c.n()], c.parity_row(p), (size_t)c.k());
+                    lm.a[(size_t)p * c.n() + c.k() + p] = 1;
+                    lm.out_slot.push_back(p);
+                }
+                for (int j = 0; j < c.n(); ++j) lm.in_slot.push_back(j);
+                rs->check = std::make_unique<ecx_map>(lm.pruned());
+            }
+            m = rs->check.get();
+        }
+        return run_host_all_zero(m->cm, shards, first_byte, byte_count) ? 1 : 0;
+    });
+}
+
+int ecx_rs_decode_missing(ecx_rs *rs, uint8_t *const *shards, const uint8_t *shard_present, int shard_count,
+                          int shard_length, int offset, int byte_count) {
+    return guarded([&]() -> int {
+        check_buffers(rs->code, shards, shard_count, shard_length, offset, byte_count);
+        std::vector<bool> present = present_vec(shard_present, rs->code.n());
+        int np = 0;
+        for (bool b : present) np += b;
+        if (np == rs->code.n()) return ECX_OK;
+        if (np < rs->code.k()) throw Error(ECX_E_NOT_ENOUGH_SHARDS, "Not enough shards present");
+        ecx_map *m = rs_decode_map(rs, present);
+        run_host(m->cm, shards, shards, offset, byte_count);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_decode_missing_single(ecx_rs *rs, const uint8_t *shard, int shard_index, int index,
+                                 const uint8_t *shard_present, uint8_t *const *outputs, int output_count, int offset,
+                                 int byte_count, int is_first) {
+    (void)shard_index;
+    return guarded([&]() -> int {
+        const RsCode &c = rs->code;
+        std::vector<bool> present = present_vec(shard_present, c.n());
+        int np = 0;
+        for (bool b : present) np += b;
+        // fewer than k present leaves zero rows in the sub-matrix: "Matrix is singular"
+        if (np < c.k()) throw Error(ECX_E_SINGULAR, "Matrix is singular");
+        const Matrix dec = c.data_decoder(present, nullptr);
+        std::vector<int> missing;
+        for (int i = 0; i < c.k(); ++i)
+            if (!present[i]) missing.push_back(i);
+        if (output_count > c.m() || (int)missing.size() > c.m()) throw Error(ECX_E_INDEX, "matrixRows index");
+        if (output_count > (int)missing.size()) throw Error(ECX_E_NULL, "no decode row for this output (no missing data shard)");
+        if (index < 0 || index >= c.k()) throw Error(ECX_E_INDEX, "matrix column index");
+        if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
+        if (output_count == 0) return ECX_OK;
+        // row j: out_j (=|^=) D^-1[missing_j][index] * shard
+        const int w = 1 + output_count;
+        LinearMap lm;
+        lm.n_out = output_count;
+        lm.n_in = w;
+        lm.a.assign((size_t)output_count * w, 0);
+        for (int j = 0; j < output_count; ++j) {
+            lm.a[(size_t)j * w] = dec.at(missing[j], index);
+            if (!is_first) lm.a[(size_t)j * w + 1 + j] = 1;
+            lm.out_slot.push_back(j);
+        }
+        for (int j = 0; j < w; ++j) lm.in_slot.push_back(j);
+        std::vector<const uint8_t *> ins(1, shard);
+        ins.insert(ins.end(), outputs, outputs + output_count);
+        CompiledMap cm(lm.pruned());
+        run_host(cm, ins.data(), outputs, offset, byte_count);
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- maps
+int ecx_map_create(const uint8_t *matrix, int n_out, int n_in, const int *in_slot, const int *out_slot,
+                   ecx_map **out) {
+    return guarded([&]() -> int {
+        *out = nullptr;
+        if (n_out < 0 || n_in <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "map shape");
+        LinearMap lm = dense_map(matrix, n_out, n_in);
+        if (in_slot) lm.in_slot.assign(in_slot, in_slot + n_in);
+        if (out_slot) lm.out_slot.assign(out_slot, out_slot + n_out);
+        for (int s : lm.in_slot)
+            if (s < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative slot");
+        for (int s : lm.out_slot)
+            if (s < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative slot");
+        *out = new ecx_map(lm.pruned());
+        return ECX_OK;
+    });
+}
+
+void ecx_map_destroy(ecx_map *map) { delete map; }
+
+int ecx_map_info(const ecx_map *map, int *n_out, int *n_in, int *nnz) {
+    const LinearMap &m = map->cm.map();
+    if (n_out) *n_out = m.n_out;
+    if (n_in) *n_in = m.n_in;
+    if (nnz) *nnz = m.nnz();
+    return ECX_OK;
+}
+
+int ecx_map_matrix(const ecx_map *map, uint8_t *matrix, int *in_slot, int *out_slot) {
+    const LinearMap &m = map->cm.map();
+    if (matrix) std::memcpy(matrix, m.a.data(), m.a.size());
+    if (in_slot) std::copy(m.in_slot.begin(), m.in_slot.end(), in_slot);
+    if (out_slot) std::copy(m.out_slot.begin(), m.out_slot.end(), out_slot);
+    return ECX_OK;
+}
+
+int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                        uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                        int64_t byte_count, void *stream) {
+    return guarded([&]() -> int {
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
+        launch_apply(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
+                     out_slot_stride, nstripes, byte_count, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- Clay
+int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_erased, ecx_clay **out) {
+    return guarded([&]() -> int {
+        *out = nullptr;
+        if (n_erased < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased");
+        *out = new ecx_clay(data_units, parity_units, std::vector<int>(erased, erased + n_erased));
+        return ECX_OK;
+    });
+}
+
+void ecx_clay_destroy(ecx_clay *clay) { delete clay; }
+
+int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha) {
+    if (q) *q = clay->pl.q();
+    if (t) *t = clay->pl.t();
+    if (alpha) *alpha = clay->pl.alpha();
+    return ECX_OK;
+}
+
+int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out) {
+    return guarded([&]() -> int {
+        std::vector<int> h = clay->pl.helper_planes(erased_index);
+        std::copy(h.begin(), h.end(), out);
+        return (int)h.size();
+    });
+}
+
+int ecx_clay_perform_coding(ecx_clay *clay, const uint8_t *const *inputs, uint8_t *const *outputs, int buf_size) {
+    return guarded([&]() -> int {
+        if (clay->pl.erased().empty()) return ECX_OK;
+        if (buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "buf_size");
+        const int w = clay->pl.n() * clay->pl.alpha();
+        std::vector<bool> present(w);
+        for (int j = 0; j < w; ++j) present[j] = inputs[j] != nullptr;
+        ecx_map *m;
+        {
+            std::lock_guard<std::mutex> lk(clay->mu);
+            auto &slot = clay->maps[key_of(present, -1)];
+            if (!slot) slot = std::make_unique<ecx_map>(clay->pl.perform_coding_map(present));
+            m = slot.get();
+        }
+        run_host(m->cm, inputs, outputs, 0, buf_size);
+        return ECX_OK;
+    });
+}
+
+int ecx_clay_decode_single_helper(ecx_clay *clay, const uint8_t *const *helper_coupled, int helper_i,
+                                  uint8_t *const *outputs, int erased_index, int buf_size) {
+    return guarded([&]() -> int {
+        if (buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "buf_size");
+        const int nh = (int)clay->pl.helper_planes(erased_index).size();
+        const int w = nh * clay->pl.n();
+        std::vector<bool> present(w);
+        for (int j = 0; j < w; ++j) present[j] = helper_coupled[j] != nullptr;
+        ecx_map *m;
+        {
+            std::lock_guard<std::mutex> lk(clay->mu);
+            auto &slot = clay->maps[key_of(present, helper_i * 4096 + erased_index)];
+            if (!slot) slot = std::make_unique<ecx_map>(clay->pl.decode_single_helper_map(present, helper_i, erased_index, nullptr));
+            m = slot.get();
+        }
+        run_host(m->cm, helper_coupled, outputs, 0, buf_size);
+        return ECX_OK;
+    });
+}
+
+int ecx_clay_map(ecx_clay *clay, const ecx_map **out) {
+    return guarded([&]() -> int {
+        *out = clay_standard_map(clay);
+        return ECX_OK;
+    });
+}
+
+int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride, int64_t in_sub_stride,
+                                  uint8_t *out, int64_t out_stripe_stride, int64_t out_sub_stride, int64_t nstripes,
+                                  int64_t buf_size, void *stream) {
+    return guarded([&]() -> int {
+        if (clay->pl.erased().empty()) return ECX_OK;
+        if (nstripes < 0 || buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
+        ecx_map *m = clay_standard_map(clay);
+        launch_apply(m->cm, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
+                     buf_size, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- synthetic data / verification
+int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream) {
+    return guarded([&]() -> int {
+        launch_fill_random(dst, nbytes, seed, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+int ecx_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
+                       int64_t row_bytes, uint64_t *d_count, void *stream) {
+    return guarded([&]() -> int {
+        launch_count_mismatch(a, a_stride, b, b_stride, nrows, row_bytes, d_count, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,203 @@
+// engine.cpp -- plan compilation, device contexts, host-pointer execution.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace ecx {
+
+void check_hip(hipError_t e, const char *what) {
+    if (e != hipSuccess) throw Error(ECX_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+namespace {
+
+uint32_t pack4(const uint8_t *t) {
+    return (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+}
+
+// The five split-table dwords of coefficient c (engine.hpp).
+void split_tables(uint8_t c, uint32_t *out) {
+    const Field &f = Field::get();
+    uint8_t lo[8], mid[8], hi[4];
+    for (int v = 0; v < 8; ++v) {
+        lo[v] = f.mul(c, (uint8_t)v);
+        mid[v] = f.mul(c, (uint8_t)(v << 3));
+    }
+    for (int v = 0; v < 4; ++v) hi[v] = f.mul(c, (uint8_t)(v << 6));
+    out[0] = pack4(lo);
+    out[1] = pack4(lo + 4);
+    out[2] = pack4(mid);
+    out[3] = pack4(mid + 4);
+    out[4] = pack4(hi);
+}
+
+}  // namespace
+
+CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
+    for (int s : map_.in_slot) max_in_slot_ = std::max(max_in_slot_, s);
+    for (int s : map_.out_slot) max_out_slot_ = std::max(max_out_slot_, s);
+    for (int r0 = 0; r0 < map_.n_out; r0 += kTileRows) {
+        const int rows = std::min(kTileRows, map_.n_out - r0);
+        const uint32_t begin = (uint32_t)(entries_.size() / kEntryDwords);
+        uint32_t count = 0;
+        for (int j = 0; j < map_.n_in; ++j) {
+            uint32_t mmul = 0, mone = 0;
+            for (int r = 0; r < rows; ++r) {
+                const uint8_t c = map_.at(r0 + r, j);
+                if (c == 1) mone |= 1u << r;
+                else if (c) mmul |= 1u << r;
+            }
+            if (!(mmul | mone)) continue;
+            uint32_t rec[kEntryDwords] = {0};
+            rec[0] = (uint32_t)map_.in_slot[j];
+            rec[1] = mmul;
+            rec[2] = mone;
+            for (int r = 0; r < rows; ++r)
+                if (mmul & (1u << r)) split_tables(map_.at(r0 + r, j), rec + 4 + 5 * r);
+            entries_.insert(entries_.end(), rec, rec + kEntryDwords);
+            ++count;
+        }
+        // Pad to a multiple of kDepth and add kDepth trailing dummies so the
+        // kernel's load ring never branches; dummies re-read the tile's first
+        // input slot (an L2 hit) and carry no coefficients.
+        const uint32_t first_slot = count ? entries_[(size_t)begin * kEntryDwords] : 0u;
+        const uint32_t padded = (count + kDepth - 1) / kDepth * kDepth;
+        for (uint32_t d = count; d < padded + kDepth; ++d) {
+            uint32_t rec[kEntryDwords] = {0};
+            rec[0] = first_slot;
+            entries_.insert(entries_.end(), rec, rec + kEntryDwords);
+        }
+        uint32_t tile[kTileDwords] = {0};
+        tile[0] = begin;
+        tile[1] = padded;
+        tile[2] = (uint32_t)rows;
+        for (int r = 0; r < rows; ++r) tile[4 + r] = (uint32_t)map_.out_slot[r0 + r];
+        tiles_.insert(tiles_.end(), tile, tile + kTileDwords);
+        ++n_tiles_;
+    }
+    if (tiles_.empty()) tiles_.assign(kTileDwords, 0);
+}
+
+CompiledMap::~CompiledMap() {
+    for (auto &kv : dev_) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) continue;
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second.entries);
+        (void)hipFree(kv.second.tiles);
+        (void)hipSetDevice(cur);
+    }
+}
+
+const DevicePlan &CompiledMap::plan_for_current_device() {
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = dev_.find(dev);
+    if (it != dev_.end()) return it->second;
+    DevicePlan p;
+    check_hip(hipMalloc(&p.entries, entries_.size() * 4), "hipMalloc(plan entries)");
+    check_hip(hipMalloc(&p.tiles, tiles_.size() * 4), "hipMalloc(plan tiles)");
+    check_hip(hipMemcpy(p.entries, entries_.data(), entries_.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    check_hip(hipMemcpy(p.tiles, tiles_.data(), tiles_.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    return dev_.emplace(dev, p).first->second;
+}
+
+// ---------------------------------------------------------------- contexts
+DeviceContext &DeviceContext::current() {
+    static std::mutex reg_mu;
+    static std::map<int, std::unique_ptr<DeviceContext>> reg;
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(reg_mu);
+    auto &slot = reg[dev];
+    if (!slot) {
+        auto ctx = std::make_unique<DeviceContext>();
+        ctx->device = dev;
+        check_hip(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
+        slot = std::move(ctx);
+    }
+    return *slot;
+}
+
+uint8_t *DeviceContext::ensure(size_t bytes) {
+    if (bytes <= staging_size_) return staging_;
+    if (staging_) check_hip(hipFree(staging_), "hipFree(staging)");
+    staging_ = nullptr;
+    staging_size_ = 0;
+    size_t sz = std::max<size_t>(bytes, 1 << 20);
+    check_hip(hipMalloc(&staging_, sz), "hipMalloc(staging)");
+    staging_size_ = sz;
+    return staging_;
+}
+
+uint64_t *DeviceContext::counter() {
+    if (!counter_) check_hip(hipMalloc(&counter_, sizeof(uint64_t)), "hipMalloc(counter)");
+    return counter_;
+}
+
+// ---------------------------------------------------------------- host execution
+namespace {
+
+struct Staged {
+    uint8_t *in;
+    uint8_t *out;
+    int64_t pitch;
+};
+
+Staged stage_inputs(DeviceContext &ctx, CompiledMap &cm, const uint8_t *const *inputs, int64_t offset,
+                    int64_t byte_count) {
+    const LinearMap &m = cm.map();
+    const int64_t pitch = (byte_count + 255) / 256 * 256;
+    const int64_t in_slots = cm.max_in_slot() + 1, out_slots = cm.max_out_slot() + 1;
+    uint8_t *base = ctx.ensure((size_t)(pitch * (in_slots + out_slots)));
+    Staged st{base, base + pitch * in_slots, pitch};
+    for (int j = 0; j < m.n_in; ++j) {
+        const int slot = m.in_slot[j];
+        if (!inputs[slot]) throw Error(ECX_E_NULL, "input buffer is null");
+        check_hip(hipMemcpyAsync(st.in + pitch * slot, inputs[slot] + offset, (size_t)byte_count,
+                                 hipMemcpyHostToDevice, ctx.stream),
+                  "hipMemcpyAsync H2D");
+    }
+    return st;
+}
+
+}  // namespace
+
+void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
+              int64_t byte_count) {
+    if (byte_count <= 0 || cm.map().n_out == 0) return;
+    DeviceContext &ctx = DeviceContext::current();
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    Staged st = stage_inputs(ctx, cm, inputs, offset, byte_count);
+    launch_apply(cm, st.in, 0, st.pitch, st.out, 0, st.pitch, 1, byte_count, ctx.stream);
+    const LinearMap &m = cm.map();
+    for (int o = 0; o < m.n_out; ++o) {
+        const int slot = m.out_slot[o];
+        if (!outputs[slot]) throw Error(ECX_E_NULL, "output buffer is null");
+        check_hip(hipMemcpyAsync(outputs[slot] + offset, st.out + st.pitch * slot, (size_t)byte_count,
+                                 hipMemcpyDeviceToHost, ctx.stream),
+                  "hipMemcpyAsync D2H");
+    }
+    check_hip(hipStreamSynchronize(ctx.stream), "hipStreamSynchronize");
+}
+
+bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count) {
+    if (byte_count <= 0 || cm.map().n_out == 0) return true;
+    DeviceContext &ctx = DeviceContext::current();
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    Staged st = stage_inputs(ctx, cm, inputs, offset, byte_count);
+    launch_apply(cm, st.in, 0, st.pitch, st.out, 0, st.pitch, 1, byte_count, ctx.stream);
+    uint64_t *cnt = ctx.counter();
+    check_hip(hipMemsetAsync(cnt, 0, sizeof(uint64_t), ctx.stream), "hipMemsetAsync");
+    const LinearMap &m = cm.map();
+    for (int o = 0; o < m.n_out; ++o)
+        launch_count_mismatch(st.out + st.pitch * m.out_slot[o], 0, nullptr, 0, 1, byte_count, cnt, ctx.stream);
+    uint64_t host = 0;
+    check_hip(hipMemcpyAsync(&host, cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, ctx.stream), "hipMemcpyAsync D2H");
+    check_hip(hipStreamSynchronize(ctx.stream), "hipStreamSynchronize");
+    return host == 0;
+}
+
+}  // namespace ecx

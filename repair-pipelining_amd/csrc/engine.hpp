@@ -1,0 +1,110 @@
+// engine.hpp -- compiled GF(256) maps, device contexts and kernel launches.
+//
+// Kernel plan format (one "entry" per (output tile, input slot) pair with a
+// non-zero coefficient; tiles of up to kTileRows output rows):
+//
+//   entry (kEntryDwords u32):
+//     [0] input slot   [1] rows with a general coefficient (bitmask)
+//     [2] rows whose coefficient is 1 (bitmask: plain XOR)   [3] 0
+//     [4+5r .. 8+5r]  split multiply tables for tile row r:
+//        T0a,T0b = c*v for v in 0..7        (low 3 bits of the byte)
+//        T1a,T1b = c*(v<<3) for v in 0..7   (middle 3 bits)
+//        T2      = c*(v<<6) for v in 0..3   (top 2 bits)
+//     so that c*b = T0[b&7] ^ T1[(b>>3)&7] ^ T2[b>>6]; each lookup is one
+//     v_perm_b32 over four bytes at once (GF(2)-linearity of c*b).
+//   tile (kTileDwords u32): [0] first entry [1] entry count (a multiple of
+//     kDepth, zero-coefficient padding included; kDepth more dummies follow)
+//     [2] rows
+//     [4..4+kTileRows) output slot of each row.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "codes.hpp"
+
+namespace ecx {
+
+constexpr int kTileRows = 8;
+constexpr int kEntryDwords = 48;
+constexpr int kTileDwords = 16;
+constexpr int kChunkBytes = 4096;  // one 256-thread workgroup x 16 bytes per lane
+constexpr int kBlockThreads = 256;
+constexpr int kDepth = 4;  // 16-B input loads in flight per lane (4 KiB per wave)
+
+void check_hip(hipError_t e, const char *what);
+
+struct DevicePlan {
+    uint32_t *entries = nullptr;
+    uint32_t *tiles = nullptr;
+};
+
+// A LinearMap compiled to the kernel's table format, uploaded lazily per device.
+class CompiledMap {
+public:
+    explicit CompiledMap(LinearMap m);
+    ~CompiledMap();
+    const LinearMap &map() const { return map_; }
+    int n_tiles() const { return n_tiles_; }
+    int max_in_slot() const { return max_in_slot_; }
+    int max_out_slot() const { return max_out_slot_; }
+    const DevicePlan &plan_for_current_device();
+
+private:
+    LinearMap map_;
+    std::vector<uint32_t> entries_, tiles_;
+    int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1;
+    std::mutex mu_;
+    std::map<int, DevicePlan> dev_;
+};
+
+struct ApplyArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    const uint32_t *entries;
+    const uint32_t *tiles;
+    int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
+    int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
+    int n_tiles;
+};
+
+// Enqueue out = M * in over nstripes stripes (kernels.hip).
+void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
+                  int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
+                  hipStream_t stream);
+void launch_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, hipStream_t stream);
+void launch_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
+                           int64_t row_bytes, uint64_t *d_count, hipStream_t stream);
+
+// Per-device context for the host (byte[][]) entry points: one stream and a
+// growable staging area, serialised by a mutex.
+class DeviceContext {
+public:
+    static DeviceContext &current();
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    int device = 0;
+    uint8_t *ensure(size_t bytes);
+    uint64_t *counter();
+
+private:
+    uint8_t *staging_ = nullptr;
+    size_t staging_size_ = 0;
+    uint64_t *counter_ = nullptr;
+};
+
+// Host-pointer execution of a compiled map: gathers each used input slot
+// (`inputs[slot] + offset`, byte_count bytes) into HBM, applies the map and
+// copies each output row back to `outputs[slot] + offset`.  Synchronous.
+void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
+              int64_t byte_count);
+// As run_host, but instead of copying outputs back, returns whether every
+// output byte is zero (used for checkSomeShards / isParityCorrect).
+bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count);
+
+}  // namespace ecx

@@ -1,0 +1,254 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of the GF(256) erasure engine.
+//
+// k_gf_apply applies one compiled GF(256) map (engine.hpp) to a batch of
+// stripes.  It replaces the reference's per-(input,output) byte loop
+// (InputOutputByteTableCodingLoop.java:27-29,39-41) and, through the planner,
+// the whole stage sequence of ClayCodeErasureDecodingStep.doDecodeSingle /
+// doDecodeMulti and ReedSolomon.decodeMissing in ONE pass over HBM:
+//
+//   * a 256-thread workgroup owns one (stripe, 4 KiB chunk, output tile);
+//     each lane owns 16 consecutive byte positions of every sub-chunk;
+//   * per input entry the lane issues one coalesced 16-B load (a wave moves
+//     1 KiB contiguous per instruction) -- the next entry's load is issued
+//     before the current one is consumed;
+//   * the byte is split into 3+3+2 bits once per input, and every GF multiply
+//     is three v_perm_b32 table lookups over four bytes (tables are wave-
+//     uniform scalar loads from the plan) plus XOR into register accumulators;
+//     coefficient 1 is a bare XOR (LRC local parity);
+//   * no LDS, no MFMA: this is HBM-bound byte work.
+#include "engine.hpp"
+
+namespace ecx {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ __forceinline__ bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+__device__ __forceinline__ u32x4 load16(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+
+__device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+
+// Byte-granular versions for the ragged tail / unaligned layouts.
+__device__ __forceinline__ u32x4 load_partial(const uint8_t *p, int valid) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int b = 0; b < valid; ++b) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
+    u32x4 r;
+    r.x = w[0];
+    r.y = w[1];
+    r.z = w[2];
+    r.w = w[3];
+    return r;
+}
+
+__device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, int valid) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int b = 0; b < valid; ++b) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+}
+
+// c*b for four packed bytes: three 8-entry lookups (v_perm_b32 selects bytes
+// 0-3 from its second operand and 4-7 from its first), XOR-folded with the
+// gfx950 three-input v_bitop3_b32 (0x96 = a^b^c).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t gf_mac4(uint32_t acc, const uint32_t *tb, uint32_t i0, uint32_t i1, uint32_t i2) {
+    const uint32_t p0 = __builtin_amdgcn_perm(tb[1], tb[0], i0);
+    const uint32_t p1 = __builtin_amdgcn_perm(tb[3], tb[2], i1);
+    const uint32_t p2 = __builtin_amdgcn_perm(tb[4], tb[4], i2);
+    return xor3(acc, p0, xor3(p1, p2, 0u));
+}
+
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+// One plan entry (input slot) against the tile's accumulators.  The 40 table
+// dwords are fetched as five 8-dword scalar loads that straddle the per-row
+// groups, so they are issued once per entry (not sunk into the per-row
+// branches); rows without a coefficient are skipped by scalar branches.
+__device__ __forceinline__ void apply_entry(const uint32_t *__restrict__ r, const u32x4 x, u32x4 (&acc)[kTileRows]) {
+    const uint32_t mmul = r[1], mone = r[2];
+    const u32x8 *__restrict__ tv = reinterpret_cast<const u32x8 *>(r + 4);
+    const u32x8 v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3], v4 = tv[4];
+    const uint32_t tb[40] = {v0[0], v0[1], v0[2], v0[3], v0[4], v0[5], v0[6], v0[7], v1[0], v1[1],
+                             v1[2], v1[3], v1[4], v1[5], v1[6], v1[7], v2[0], v2[1], v2[2], v2[3],
+                             v2[4], v2[5], v2[6], v2[7], v3[0], v3[1], v3[2], v3[3], v3[4], v3[5],
+                             v3[6], v3[7], v4[0], v4[1], v4[2], v4[3], v4[4], v4[5], v4[6], v4[7]};
+    const u32x4 i0 = x & 0x07070707u;
+    const u32x4 i1 = (x >> 3) & 0x07070707u;
+    const u32x4 i2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+    for (int o = 0; o < kTileRows; ++o) {
+        if (mmul & (1u << o)) {
+            const uint32_t *t = tb + 5 * o;
+            acc[o].x = gf_mac4(acc[o].x, t, i0.x, i1.x, i2.x);
+            acc[o].y = gf_mac4(acc[o].y, t, i0.y, i1.y, i2.y);
+            acc[o].z = gf_mac4(acc[o].z, t, i0.z, i1.z, i2.z);
+            acc[o].w = gf_mac4(acc[o].w, t, i0.w, i1.w, i2.w);
+        }
+    }
+    if (mone) {
+#pragma unroll
+        for (int o = 0; o < kTileRows; ++o)
+            if (mone & (1u << o)) acc[o] ^= x;
+    }
+}
+
+template <bool SAFE>
+__global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
+    const uint32_t w = blockIdx.x;
+    const uint32_t tl = w % (uint32_t)a.n_tiles;
+    const uint32_t rest = w / (uint32_t)a.n_tiles;
+    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
+    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+
+    const uint32_t *__restrict__ tile = a.tiles + tl * kTileDwords;
+    const int ebeg = (int)tile[0];
+    const int ecnt = (int)tile[1];
+    const int nrows = (int)tile[2];
+
+    const int64_t off = c * kChunkBytes + (int64_t)threadIdx.x * 16;
+    const uint8_t *ib = a.in + s * a.in_stripe_stride + off;
+    uint8_t *ob = a.out + s * a.out_stripe_stride + off;
+    int valid = 16;
+    if (SAFE) {
+        const int64_t v = a.nbytes - off;
+        valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
+    }
+    auto load = [&](uint32_t slot) -> u32x4 {
+        const uint8_t *p = ib + (int64_t)slot * a.in_slot_stride;
+        return SAFE ? load_partial(p, valid) : load16(p);
+    };
+
+    u32x4 acc[kTileRows];
+#pragma unroll
+    for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
+
+    const uint32_t *__restrict__ ent = a.entries + (int64_t)ebeg * kEntryDwords;
+    // The host pads every tile's entry list to a multiple of kDepth and appends
+    // kDepth dummy entries (no coefficients, slot = an input this tile reads),
+    // so the ring refill below is unconditional and never copies a register
+    // whose load is still in flight.
+    u32x4 ring[kDepth];
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) ring[u] = load(ent[u * kEntryDwords]);
+    for (int e0 = 0; e0 < ecnt; e0 += kDepth) {
+#pragma unroll
+        for (int u = 0; u < kDepth; ++u) {
+            const uint32_t *__restrict__ r = ent + (int64_t)(e0 + u) * kEntryDwords;
+            apply_entry(r, ring[u], acc);  // consume the slot, then refill it:
+            ring[u] = load(r[kDepth * kEntryDwords]);  // kDepth-1 loads stay in flight
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < kTileRows; ++o) {
+        if (o < nrows) {
+            uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
+            if (SAFE) store_partial(p, acc[o], valid);
+            else store16(p, acc[o]);
+        }
+    }
+}
+
+void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
+                  int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
+                  hipStream_t stream) {
+    if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
+    const DevicePlan &plan = cm.plan_for_current_device();
+    const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
+                         (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
+    const int64_t full = aligned ? nbytes / kChunkBytes : 0;
+    const int64_t tail_chunks = (nbytes - full * kChunkBytes + kChunkBytes - 1) / kChunkBytes;
+
+    ApplyArgs a;
+    a.in = in;
+    a.out = out;
+    a.entries = plan.entries;
+    a.tiles = plan.tiles;
+    a.in_stripe_stride = in_stripe_stride;
+    a.in_slot_stride = in_slot_stride;
+    a.out_stripe_stride = out_stripe_stride;
+    a.out_slot_stride = out_slot_stride;
+    a.nbytes = nbytes;
+    a.n_tiles = cm.n_tiles();
+
+    auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
+        if (n_chunks <= 0) return;
+        a.chunk_begin = chunk_begin;
+        a.n_chunks = n_chunks;
+        const int64_t per_stripe = n_chunks * a.n_tiles;
+        const int64_t max_blocks = (int64_t)1 << 30;
+        const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / per_stripe);
+        for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
+            const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
+            a.stripe_begin = s0;
+            const dim3 grid((unsigned)(ns * per_stripe));
+            if (safe) hipLaunchKernelGGL(k_gf_apply<true>, grid, dim3(kBlockThreads), 0, stream, a);
+            else hipLaunchKernelGGL(k_gf_apply<false>, grid, dim3(kBlockThreads), 0, stream, a);
+        }
+    };
+    run(false, 0, full);
+    run(true, full, tail_chunks);
+    check_hip(hipGetLastError(), "k_gf_apply launch");
+}
+
+// ---------------------------------------------------------------- synthetic data
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// Byte i of the region is byte (i % 8) of splitmix64(seed + (i / 8) * golden).
+__global__ void __launch_bounds__(256) k_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 16;
+    for (int64_t off = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; off < nbytes; off += stride) {
+        const uint64_t w0 = splitmix64(seed + (uint64_t)(off / 8) * 0x9E3779B97F4A7C15ull);
+        const uint64_t w1 = splitmix64(seed + (uint64_t)(off / 8 + 1) * 0x9E3779B97F4A7C15ull);
+        if (off + 16 <= nbytes && aligned16(dst + off)) {
+            u32x4 v;
+            v.x = (uint32_t)w0;
+            v.y = (uint32_t)(w0 >> 32);
+            v.z = (uint32_t)w1;
+            v.w = (uint32_t)(w1 >> 32);
+            store16(dst + off, v);
+        } else {
+            for (int b = 0; b < 16 && off + b < nbytes; ++b) dst[off + b] = (uint8_t)((b < 8 ? w0 : w1) >> (8 * (b & 7)));
+        }
+    }
+}
+
+void launch_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, hipStream_t stream) {
+    if (nbytes <= 0) return;
+    const int64_t granules = (nbytes + 15) / 16;
+    const unsigned blocks = (unsigned)std::min<int64_t>((granules + 255) / 256, 256 * 32);
+    hipLaunchKernelGGL(k_fill_random, dim3(blocks), dim3(256), 0, stream, dst, nbytes, seed);
+    check_hip(hipGetLastError(), "k_fill_random launch");
+}
+
+// ---------------------------------------------------------------- verification
+__global__ void __launch_bounds__(256) k_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b,
+                                                        int64_t b_stride, int64_t nrows, int64_t row_bytes,
+                                                        uint64_t *count) {
+    uint64_t n = 0;
+    const int64_t total = nrows * row_bytes;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int64_t r = i / row_bytes, c = i - r * row_bytes;
+        n += a[r * a_stride + c] != (b ? b[r * b_stride + c] : 0);
+    }
+    for (int sh = 32; sh > 0; sh >>= 1) n += __shfl_xor(n, sh);
+    if ((threadIdx.x & 63) == 0 && n) atomicAdd((unsigned long long *)count, (unsigned long long)n);
+}
+
+void launch_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
+                           int64_t row_bytes, uint64_t *d_count, hipStream_t stream) {
+    const int64_t total = nrows * row_bytes;
+    if (total <= 0) return;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(k_count_mismatch, dim3(blocks), dim3(256), 0, stream, a, a_stride, b, b_stride, nrows, row_bytes,
+                       d_count);
+    check_hip(hipGetLastError(), "k_count_mismatch launch");
+}
+
+}  // namespace ecx

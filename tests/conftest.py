@@ -19,3 +19,26 @@ def pytest_configure(config):
 def kats():
     import json
     return json.loads((ROOT / "tests" / "golden" / "reference_kats.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def ecx():
+    """The product package (repair-pipelining_amd/), loaded via rpamd."""
+    import rpamd
+    return rpamd.load()
+
+
+def gf_apply_numpy(matrix, inputs):
+    """Test-side reference application of a dense GF(256) map with the oracle's
+    multiplication table: out[o] = XOR_j M[o][j] * in[j]."""
+    import numpy as np
+    import oracle as O
+    mt = O.mul_table()
+    outs = []
+    for row in matrix:
+        acc = np.zeros(len(inputs[0]), np.uint8)
+        for c, x in zip(row, inputs):
+            if c:
+                acc ^= mt[c][x]
+        outs.append(acc)
+    return outs

@@ -1,0 +1,82 @@
+"""The C-ABI library loads and exports every symbol include/ecx.h declares
+(no compute calls: this container has no GPU)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_symbols():
+    text = (ROOT / "include" / "ecx.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ecx_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for must in ["ecx_code_some_shards", "ecx_check_some_shards", "ecx_code_single", "ecx_rs_encode_parity",
+                 "ecx_rs_decode_missing", "ecx_rs_decode_missing_single", "ecx_rs_encode_parity_single",
+                 "ecx_rs_is_parity_correct", "ecx_clay_perform_coding", "ecx_clay_decode_single_helper",
+                 "ecx_clay_perform_coding_batch", "ecx_map_apply_batch"]:
+        assert must in syms
+
+
+def test_library_exports_every_declared_symbol(ecx):
+    lib = ctypes.CDLL(str(ecx.LIB_PATH))
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_binding_table_matches_header(ecx):
+    from importlib import import_module
+    sigs = import_module("repair_pipelining_amd._lib").SIGNATURES
+    assert sorted(sigs) == declared_symbols()
+
+
+def test_no_gpu_fails_loudly(ecx):
+    """Without a HIP device the arithmetic entry points raise (no CPU fallback)."""
+    import numpy as np
+    if ecx.device_count() if _has_device(ecx) else 0:
+        pytest.skip("a device is present")
+    rs = ecx.ReedSolomon.create(4, 2)
+    with pytest.raises(ecx.EcxError) as e:
+        rs.encodeParity([np.zeros(16, np.uint8) for _ in range(6)], 0, 16)
+    assert e.value.code == -10
+
+
+def _has_device(ecx):
+    try:
+        return ecx.device_count() > 0
+    except ecx.EcxError:
+        return False
+
+
+def test_status_strings(ecx):
+    lib = ecx.lib()
+    assert lib.ecx_status_string(-3) == b"Matrix is singular"
+    assert lib.ecx_version() >= 100
+
+
+def test_host_planner_errors(ecx):
+    """Exceptions of the reference map to status codes before any device work."""
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.ReedSolomon.create(200, 57)
+    assert e.value.code == -4
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.Matrix.invert([[1, 1], [1, 1]])
+    assert e.value.code == -3
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.Galois.divide(3, 0)
+    assert e.value.code == -1
+    rs = ecx.ReedSolomon.create(4, 2)
+    with pytest.raises(ecx.EcxError) as e:
+        rs.decode_map([True, False, False, False, True, True])
+    assert e.value.code == -2
+    # Clay(10,4): t = 14 // 4 = 3 -> nodes 12, 13 are off the grid (bug B7)
+    step = ecx.ClayCodeErasureDecodingStep([13], 10, 4)
+    with pytest.raises(ecx.EcxError) as e:
+        step.getHelperPlanesIndexes(13)
+    assert e.value.code == -5

@@ -1,0 +1,391 @@
+"""GPU parity: every entry point of the C ABI, executed by the HIP kernels on
+the MI355X, is bit-exact against the oracle (the CPU restatement of the
+reference JVM path) on the same seeded inputs; at BASELINE sizes through
+size-independent properties (encode -> erase -> repair round trips)."""
+import hashlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def h16(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+# ---------------------------------------------------------------- CodingLoop
+@pytest.mark.parametrize("nin,nout,L,offset", [(1, 1, 1, 0), (3, 2, 15, 0), (5, 5, 17, 3), (17, 3, 4095, 0),
+                                               (17, 3, 4097, 5), (4, 8, 10000, 100), (20, 8, 65536, 0),
+                                               (2, 9, 333, 7)])
+def test_code_some_shards(ecx, nin, nout, L, offset):
+    rng = np.random.default_rng(nin * 100 + nout)
+    rows = rng.integers(0, 256, (nout, nin), dtype=np.uint8)
+    rows[0, 0] = 1
+    if nin > 1:
+        rows[-1, 1] = 0
+    ins = [rng.integers(0, 256, L + offset, dtype=np.uint8) for _ in range(nin)]
+    outs = [rng.integers(0, 256, L + offset, dtype=np.uint8) for _ in range(nout)]
+    ref = [o.copy() for o in outs]
+    O.code_some_shards(list(rows), ins, ref, offset, L)
+    ecx.CodingLoop().codeSomeShards(rows, ins, nin, outs, nout, offset, L)
+    for a, b in zip(outs, ref):
+        assert (a == b).all()
+
+
+def test_check_some_shards(ecx):
+    rng = np.random.default_rng(2)
+    rows = rng.integers(0, 256, (3, 6), dtype=np.uint8)
+    ins = [rng.integers(0, 256, 777, dtype=np.uint8) for _ in range(6)]
+    outs = [np.zeros(777, np.uint8) for _ in range(3)]
+    O.code_some_shards(list(rows), ins, outs, 0, 777)
+    loop = ecx.CodingLoop()
+    assert loop.checkSomeShards(rows, ins, 6, outs, 3, 0, 777)
+    outs[2][776] ^= 1
+    assert not loop.checkSomeShards(rows, ins, 6, outs, 3, 0, 777)
+    assert loop.checkSomeShards(rows, ins, 6, outs, 3, 0, 776)
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_code_single(ecx, first):
+    rng = np.random.default_rng(3)
+    rows = rng.integers(0, 256, (4, 4), dtype=np.uint8)
+    x = rng.integers(0, 256, 1000, dtype=np.uint8)
+    out = rng.integers(0, 256, 1000, dtype=np.uint8)
+    exp = out.copy()
+    mt = O.mul_table()
+    prod = mt[rows[2][3]][x[10:990]]
+    exp[10:990] = prod if first else exp[10:990] ^ prod
+    ecx.InputOutputByteTableCodingLoopSingle().codeSomeShards(rows, x, 3, out, 2, 10, 980, first)
+    assert (out == exp).all()
+
+
+# ---------------------------------------------------------------- ReedSolomon
+def test_rs_one_encode_kat(ecx, kats):
+    r = kats["reed_solomon"]
+    rs = ecx.ReedSolomon.create(5, 5)
+    shards = [np.array(x, np.uint8) for x in r["rs55_data"]] + [np.zeros(2, np.uint8) for _ in range(5)]
+    rs.encodeParity(shards, 0, 2)
+    assert [s.tolist() for s in shards[5:]] == r["rs55_parity"]
+    assert rs.isParityCorrect(shards, 0, 2)
+    shards[8][0] += 1
+    assert not rs.isParityCorrect(shards, 0, 2)
+    assert not rs.isParityCorrect(shards, 0, 2, np.zeros(2, np.uint8))
+
+
+def test_rs_zero_size_encode(ecx):
+    ecx.ReedSolomon.create(2, 1).encodeParity([np.zeros(0, np.uint8) for _ in range(3)], 0, 0)
+
+
+@pytest.mark.parametrize("k,m,L", [(4, 2, 104449), (5, 5, 2000), (17, 3, 200000), (12, 4, 4096 + 13)])
+def test_rs_encode_vs_oracle(ecx, k, m, L):
+    rng = np.random.default_rng(k + m)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    a = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+    b = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+    ecx.ReedSolomon.create(k, m).encodeParity(a, 0, L)
+    O.ReedSolomon(k, m).encode_parity(b, 0, L)
+    assert all((x == y).all() for x, y in zip(a, b))
+
+
+def test_rs_decode_all_subsets(ecx):
+    """ReedSolomonTest.runEncodeDecode (:111-169) for RS(5,5) over every erasure subset."""
+    import itertools
+    k, m, L = 5, 5, 300
+    rng = np.random.default_rng(9)
+    allsh = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+    rs = ecx.ReedSolomon.create(k, m)
+    rs.encodeParity(allsh, 0, L)
+    for nmiss in range(m + 1):
+        for subset in itertools.combinations(range(10), nmiss):
+            test = [s.copy() for s in allsh]
+            present = [True] * 10
+            for s in subset:
+                test[s][:] = 0
+                present[s] = False
+            rs.decodeMissing(test, present, 0, L)
+            assert all((x == y).all() for x, y in zip(allsh, test)), subset
+
+
+def test_rs_decode_noncodeword_vs_oracle(ecx):
+    rng = np.random.default_rng(12)
+    for present in ([1, 0, 1, 1, 0, 1], [0, 1, 1, 1, 1, 1], [1, 1, 1, 1, 0, 0], [0, 0, 1, 1, 1, 1]):
+        shards = [rng.integers(0, 256, 5000, dtype=np.uint8) for _ in range(6)]
+        a = [s.copy() for s in shards]
+        b = [s.copy() for s in shards]
+        pres = [bool(p) for p in present]
+        ecx.ReedSolomon.create(4, 2).decodeMissing(a, pres, 7, 4000)
+        O.ReedSolomon(4, 2).decode_missing(b, pres, 7, 4000)
+        assert all((x == y).all() for x, y in zip(a, b))
+
+
+def test_rs_not_enough_shards(ecx):
+    rs = ecx.ReedSolomon.create(4, 2)
+    with pytest.raises(ecx.EcxError) as e:
+        rs.decodeMissing([np.zeros(8, np.uint8) for _ in range(6)], [1, 0, 0, 0, 1, 1], 0, 8)
+    assert e.value.code == -2
+    with pytest.raises(ecx.EcxError) as e:
+        rs.encodeParity([np.zeros(8, np.uint8) for _ in range(5)], 0, 8)
+    assert e.value.code == -1
+    with pytest.raises(ecx.EcxError):
+        rs.encodeParity([np.zeros(8, np.uint8) for _ in range(6)], 4, 8)
+
+
+def test_rs_single_apis(ecx):
+    """encodeParitySingle chains (LRC) and decodeMissingSingle chains (pipelined RS)."""
+    rng = np.random.default_rng(4)
+    k, m, L = 4, 2, 3000
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    rs, ors = ecx.ReedSolomon.create(k, m), O.ReedSolomon(k, m)
+    for p in range(m):
+        a = rng.integers(0, 256, L, dtype=np.uint8)
+        b = a.copy()
+        for i in range(k):
+            rs.encodeParitySingle(data[i], a, i, p, 0, L)
+            ors.encode_parity_single(data[i], b, i, p, 0, L)
+        assert (a == b).all()
+    shards = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k + m)]
+    present = [True, False, True, False, True, True]
+    a = [np.zeros(L, np.uint8) for _ in range(2)]
+    b = [np.zeros(L, np.uint8) for _ in range(2)]
+    chain = [0, 2, 4, 5]
+    for c, idx in enumerate(chain):
+        rs.decodeMissingSingle(shards[idx], idx, c, present, a, 0, L, c == 0)
+        ors.decode_missing_single(shards[idx], idx, c, present, b, 0, L, c == 0)
+    assert all((x == y).all() for x, y in zip(a, b))
+    with pytest.raises(ecx.EcxError) as e:  # bug B3: parity-only erasure -> NPE
+        rs.decodeMissingSingle(shards[0], 0, 0, [True] * 5 + [False], [np.zeros(L, np.uint8)], 0, L, True)
+    assert e.value.code == -6
+
+
+# ---------------------------------------------------------------- files / LRC
+def test_sample_encoder_lp_block(ecx, kats):
+    lp = np.fromfile(GOLDEN / "LP-block.jpg", dtype=np.uint8)
+    shards = ecx.sample_encode(lp)
+    assert [h16(s) for s in shards] == kats["survey_digests"]["sample_encoder_lp_block"]
+    for missing in range(6):
+        out, _ = ecx.sample_decode([None if i == missing else s for i, s in enumerate(shards)])
+        assert (out == lp).all()
+
+
+def test_lrc_lp_block(ecx, kats):
+    lp = np.fromfile(GOLDEN / "LP-block.jpg", dtype=np.uint8)
+    blocks = ecx.lrc_encode(lp)
+    assert [h16(blocks[i]) for i in (3, 7, 11, 15)] == kats["survey_digests"]["lrc_local_parities_3_7_11_15"]
+    single = ecx.lrc_encode_using_single(lp)
+    assert all((a == b).all() for a, b in zip(blocks, single))
+    for missing in (2, 7, 12):
+        out, shards = ecx.lrc_decode(blocks, [missing], len(blocks[0]))
+        assert (shards[missing] == blocks[missing]).all()
+
+
+# ---------------------------------------------------------------- Clay (per call)
+CLAY_CASES = [(2, 2, [0]), (4, 2, [0]), (4, 2, [1]), (4, 2, [2]), (4, 2, [3]), (4, 2, [4]), (4, 2, [5]),
+              (4, 2, [4, 5]), (4, 2, [0, 1]), (4, 2, [1, 4]), (6, 3, [2]), (6, 3, [6, 7, 8]), (12, 4, [5]),
+              (12, 4, [12, 13, 14, 15])]
+
+
+@pytest.mark.parametrize("k,m,erased", CLAY_CASES)
+def test_clay_perform_coding_vs_oracle(ecx, k, m, erased):
+    n = k + m
+    step = ecx.ClayCodeErasureDecodingStep(erased, k, m)
+    a = step.subPacketSize
+    B = 64 if a >= 64 else 2174  # 2174 = ClayCodeHelper.kt:90's CLAY_BLOCK_SIZE (ragged, not 16-aligned)
+    rng = np.random.default_rng(len(erased) * 13 + k)
+    inputs = [None if (i % n) in erased else rng.integers(0, 256, B, dtype=np.uint8) for i in range(n * a)]
+    oc = O.Clay(k, m, erased)
+    ref = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
+    oc.perform_coding(inputs, ref, B)
+    got = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
+    step.performCoding(inputs, got, B)
+    for o in range(len(got)):
+        assert (got[o] == ref[o]).all(), o
+
+
+def test_clay_multi_nonnull_erased_inputs(ecx):
+    """doDecodeMulti with non-null buffers at erased slots (the reference reads them)."""
+    k, m, erased, B = 4, 2, [0, 1], 100
+    n, a = 6, 8
+    rng = np.random.default_rng(21)
+    inputs = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(n * a)]
+    ref = [np.zeros(B, np.uint8) for _ in range(2 * a)]
+    O.Clay(k, m, erased).perform_coding([x.copy() for x in inputs], ref, B)
+    got = [np.zeros(B, np.uint8) for _ in range(2 * a)]
+    ecx.ClayCodeErasureDecodingStep(erased, k, m).performCoding(inputs, got, B)
+    assert all((x == y).all() for x, y in zip(got, ref))
+
+
+def test_clay_getinputs_encode_digests(ecx, kats):
+    d = kats["survey_digests"]
+    cc = ecx.ClayCode(4, 2, 32768, [4, 5])
+    inp = cc.getInputs()
+    assert bytes(inp[0][:8]).hex() == d["clay42_first_bytes"]
+    outs = cc.getOutputs()
+    cc.encode(inp, outs)
+    assert [h16(outs[z * 2]) for z in range(8)] == d["clay42_parity_node4"]
+    assert [h16(outs[z * 2 + 1]) for z in range(8)] == d["clay42_parity_node5"]
+
+
+def test_clay_helper_overload(ecx):
+    """ClayCodeHelper.getHelperPlanesAndDecode: overload 2, one helper plane at a time."""
+    k, m, B, n = 4, 2, 2174, 6
+    rng = np.random.default_rng(8)
+    for e in range(n):
+        oc = O.Clay(k, m, [e])
+        hidx = oc.helper_planes(e)
+        helper = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(len(hidx) * n)]
+        ref = [np.zeros(B, np.uint8) for _ in range(oc.alpha)]
+        got = [np.zeros(B, np.uint8) for _ in range(oc.alpha)]
+        step = ecx.ClayCodeErasureDecodingStep([e], k, m)
+        rows = [helper[i * n:(i + 1) * n] for i in range(len(hidx))]
+        for i in range(len(hidx)):
+            oc.decode_single_helper(helper, i, ref, e, B)
+            step.doDecodeSingleHelper(rows, i, got, e, B)
+        assert all((x == y).all() for x, y in zip(got, ref))
+
+
+# ---------------------------------------------------------------- batched, device-resident
+def _clay_pool(ecx, torch, k, m, B, S, seed=1):
+    """S valid Clay stripes [S][n*alpha][B] built on the device: random data + GPU encode."""
+    n = k + m
+    enc = ecx.ClayCodeErasureDecodingStep(list(range(k, n)), k, m)
+    a = enc.subPacketSize
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), seed)
+    par = torch.empty((S, m * a, B), dtype=torch.uint8, device="cuda")
+    enc.performCodingBatch(pool, n * a * B, B, par, m * a * B, B, S, B)
+    pv = pool.view(S, a, n, B)
+    pv[:, :, k:, :] = par.view(S, a, m, B)
+    torch.cuda.synchronize()
+    return pool, a
+
+
+def test_clay_batch_encode_vs_oracle(ecx, torch_dev):
+    torch = torch_dev
+    k, m, B, S = 4, 2, 4096 + 48, 3
+    pool, a = _clay_pool(ecx, torch, k, m, B, S)
+    host = pool.cpu().numpy()
+    for s in range(S):
+        inputs = [host[s, i].copy() if (i % 6) < k else None for i in range(6 * a)]
+        ref = [np.zeros(B, np.uint8) for _ in range(2 * a)]
+        O.Clay(k, m, [4, 5]).perform_coding(inputs, ref, B)
+        for z in range(a):
+            for j in range(2):
+                assert (host[s, z * 6 + 4 + j] == ref[z * 2 + j]).all()
+
+
+@pytest.mark.parametrize("e", range(6))
+def test_clay42_batch_repair_headline_roundtrip(ecx, torch_dev, e):
+    """BASELINE config 2 shape (B = 32 KiB): repair every stripe's node e and compare
+    with the original sub-chunks on the device; sampled stripes also vs the oracle."""
+    torch = torch_dev
+    k, m, B, S = 4, 2, 32768, 64
+    pool, a = _clay_pool(ecx, torch, k, m, B, S, seed=100 + e)
+    out = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m)
+    step.performCodingBatch(pool, 6 * a * B, B, out, a * B, B, S, B)
+    torch.cuda.synchronize()
+    orig = pool.view(S, a, 6, B)[:, :, e, :]
+    assert torch.equal(out, orig)
+    host = pool[0].cpu().numpy()
+    inputs = [None if (i % 6) == e else host[i].copy() for i in range(6 * a)]
+    ref = [np.zeros(B, np.uint8) for _ in range(a)]
+    O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
+    got = out[0].cpu().numpy()
+    assert all((got[z] == ref[z]).all() for z in range(a))
+
+
+def test_clay_batch_noncodeword_vs_oracle(ecx, torch_dev):
+    """Random (non-codeword) stripes: the batch kernel reproduces the reference's linear map."""
+    torch = torch_dev
+    k, m, B, S, e = 4, 2, 8192 + 16, 4, 1
+    pool = torch.empty((S, 48, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 77)
+    out = torch.empty((S, 8, B), dtype=torch.uint8, device="cuda")
+    ecx.ClayCodeErasureDecodingStep([e], k, m).performCodingBatch(pool, 48 * B, B, out, 8 * B, B, S, B)
+    torch.cuda.synchronize()
+    host, got = pool.cpu().numpy(), out.cpu().numpy()
+    for s in range(S):
+        inputs = [None if (i % 6) == e else host[s, i].copy() for i in range(48)]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
+        assert all((got[s, z] == ref[z]).all() for z in range(8))
+
+
+def test_clay_batch_unaligned_layout(ecx, torch_dev):
+    """Unaligned base/strides take the byte-safe kernel path; results unchanged."""
+    torch = torch_dev
+    k, m, B, S, e = 4, 2, 1001, 3, 3
+    stride = 48 * B + 5
+    raw = torch.empty((S * stride + 64,), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(raw, raw.numel(), 5)
+    base = raw[3:]
+    outraw = torch.zeros((S * 8 * B + 64,), dtype=torch.uint8, device="cuda")
+    ecx.ClayCodeErasureDecodingStep([e], k, m).performCodingBatch(base, stride, B, outraw[1:], 8 * B, B, S, B)
+    torch.cuda.synchronize()
+    host, got = base.cpu().numpy(), outraw[1:].cpu().numpy()
+    for s in range(S):
+        inputs = [None if (i % 6) == e else host[s * stride + i * B: s * stride + (i + 1) * B].copy()
+                  for i in range(48)]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
+        for z in range(8):
+            assert (got[s * 8 * B + z * B: s * 8 * B + (z + 1) * B] == ref[z]).all()
+
+
+def test_rs124_two_erasure_batch_roundtrip(ecx, torch_dev):
+    """BASELINE config 5 shape: RS(12,4), 4 MiB shards, erasures {0,1}, in place."""
+    torch = torch_dev
+    k, m, L, S = 12, 4, 4 << 20, 2
+    rs = ecx.ReedSolomon.create(k, m)
+    pool = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 9)
+    rs.encode_map().apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L)
+    orig = pool.clone()
+    pool[:, 0:2, :] = 0
+    present = [False, False] + [True] * 14
+    rs.decode_map(present).apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L)
+    torch.cuda.synchronize()
+    assert torch.equal(pool, orig)
+    # oracle parity on a 64 KiB window of stripe 0
+    host = orig[0, :, :65536].cpu().numpy()
+    b = [host[i].copy() for i in range(16)]
+    O.ReedSolomon(k, m).encode_parity(b, 0, 65536)
+    assert all((b[i] == host[i]).all() for i in range(12, 16))
+
+
+def test_lrc_batch_config3(ecx, torch_dev):
+    """BASELINE config 3 shape: LRC (12 data, 4 XOR groups), 64 KiB blocks, repair block 2."""
+    torch = torch_dev
+    B, S = 65536, 16
+    enc = np.zeros((4, 16), np.uint8)
+    for g in range(4):
+        enc[g, 4 * g:4 * g + 3] = 1
+    encmap = ecx.GfMap.from_matrix(enc, in_slot=list(range(16)), out_slot=[3, 7, 11, 15])
+    pool = torch.empty((S, 16, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 31)
+    encmap.apply_batch(pool, 16 * B, B, pool, 16 * B, B, S, B)
+    torch.cuda.synchronize()
+    host = pool[0].cpu().numpy()
+    ref = O.lrc_encode(np.concatenate([host[i] for i in range(16) if (i + 1) % 4 != 0]))
+    assert all((ref[i] == host[i]).all() for i in range(16))
+    rs = ecx.ReedSolomon.create(3, 1)
+    dm = rs.decode_map([True, True, False, True])
+    out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+    mat, ins, outs = dm.matrix()
+    assert mat.tolist() == [[1, 1, 1]] and outs.tolist() == [2]
+    repair = ecx.GfMap.from_matrix(mat, in_slot=[0, 1, 3], out_slot=[0])
+    repair.apply_batch(pool, 16 * B, B, out, B, B, S, B)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, 0], pool[:, 2])

@@ -1,0 +1,121 @@
+"""Host-planner parity on CPU: the composed GF(256) maps that the HIP kernels
+apply, applied here in numpy, must reproduce the oracle's stage-by-stage
+restatement of the reference on the same (random, non-codeword) inputs.
+This pins the planner independently of the GPU; tests/test_gpu_parity.py then
+pins the kernels against the same oracle."""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import gf_apply_numpy
+
+
+def test_field_tables_match_reference(ecx, kats):
+    log, exp, mul = ecx.Galois.tables()
+    g = kats["galois"]
+    assert log.tolist() == g["log_table"]
+    assert exp.tolist() == g["exp_table"]
+    assert (mul == O.mul_table()).all()
+    for a, b, r in g["multiply"]:
+        assert ecx.Galois.multiply(a, b) == r
+    for a, n, r in g["exp"]:
+        assert ecx.Galois.exp(a, n) == r
+
+
+def test_matrix_kats(ecx, kats):
+    t = kats["matrix"]["times"]
+    assert ecx.Matrix.times(t["a"], t["b"]).tolist() == t["out"]
+    for case in kats["matrix"]["invert"]:
+        assert ecx.Matrix.invert(case["m"]).tolist() == case["inv"]
+
+
+def test_rs_generator_matrix(ecx, kats):
+    for key, rows in kats["rs_parity_rows"].items():
+        if key == "17,3_row0":
+            assert ecx.ReedSolomon.create(17, 3).parityRows[0].tolist() == rows
+        else:
+            k, m = map(int, key.split(","))
+            assert ecx.ReedSolomon.create(k, m).parityRows.tolist() == rows
+    for k, m in [(5, 5), (64, 64), (10, 4)]:
+        assert (ecx.ReedSolomon.create(k, m).matrix == O.ReedSolomon(k, m).matrix).all()
+
+
+@pytest.mark.parametrize("k,m,present", [
+    (4, 2, [1, 0, 1, 1, 1, 1]), (4, 2, [0, 1, 1, 0, 1, 1]), (4, 2, [1, 1, 1, 1, 0, 0]),
+    (4, 2, [1, 1, 0, 1, 0, 1]), (12, 4, [0, 0] + [1] * 14), (5, 5, [0, 1, 0, 1, 0, 1, 1, 1, 1, 1]),
+    (3, 1, [1, 1, 0, 1]),
+])
+def test_rs_decode_map_vs_oracle(ecx, k, m, present):
+    """decodeMissing's composed map on NON-codeword shards == the oracle (first-k-present rule)."""
+    rng = np.random.default_rng(k * 31 + m)
+    L = 64
+    shards = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k + m)]
+    ref = [s.copy() for s in shards]
+    O.ReedSolomon(k, m).decode_missing(ref, [bool(p) for p in present], 0, L)
+    mat, ins, outs = ecx.ReedSolomon.create(k, m).decode_map([bool(p) for p in present]).matrix()
+    got = gf_apply_numpy(mat, [shards[j] for j in ins])
+    for o, slot in enumerate(outs):
+        assert (got[o] == ref[slot]).all()
+    assert sorted(outs.tolist()) == [i for i in range(k + m) if not present[i]]
+
+
+def _oracle_perform(k, m, erased, inputs, B):
+    c = O.Clay(k, m, erased)
+    outs = [np.zeros(B, np.uint8) for _ in range(len(erased) * c.alpha)]
+    c.perform_coding(inputs, outs, B)
+    return outs
+
+
+CLAY_CASES = [(2, 2, [0]), (2, 2, [3]), (4, 2, [0]), (4, 2, [1]), (4, 2, [2]), (4, 2, [3]), (4, 2, [4]),
+              (4, 2, [5]), (4, 2, [4, 5]), (4, 2, [0, 1]), (4, 2, [1, 4]), (6, 3, [2]), (6, 3, [6, 7, 8]),
+              (6, 3, [0, 4]), (12, 4, [5]), (12, 4, [12, 13, 14, 15]), (12, 4, [0, 15])]
+
+
+@pytest.mark.parametrize("k,m,erased", CLAY_CASES)
+def test_clay_map_vs_oracle_random_inputs(ecx, k, m, erased):
+    """The composed Clay map equals the reference stage sequence on random (non-codeword) inputs."""
+    n = k + m
+    step = ecx.ClayCodeErasureDecodingStep(erased, k, m)
+    a = step.subPacketSize
+    B = 8 if a >= 64 else 24
+    rng = np.random.default_rng(sum(erased) + 7 * k)
+    inputs = [None if (i % n) in erased else rng.integers(0, 256, B, dtype=np.uint8) for i in range(n * a)]
+    ref = _oracle_perform(k, m, erased, inputs, B)
+    mat, ins, outs = step.map().matrix()
+    got = gf_apply_numpy(mat, [inputs[j] for j in ins])
+    assert outs.tolist() == list(range(len(erased) * a))
+    for o in range(len(outs)):
+        assert (got[o] == ref[o]).all(), o
+
+
+def test_clay42_map_shape(ecx):
+    """Clay(4,2) single repair is an 8 x 20 map with 52 non-zeros
+    for every erased node; the encode map is 16 x 32 with 144 non-zeros."""
+    for e in range(6):
+        inf = ecx.ClayCodeErasureDecodingStep([e], 4, 2).map().info()
+        assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (8, 20, 52)
+    inf = ecx.ClayCodeErasureDecodingStep([4, 5], 4, 2).map().info()
+    assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (16, 32, 144)
+
+
+def test_clay124_map_shape(ecx):
+    inf = ecx.ClayCodeErasureDecodingStep([5], 12, 4).map().info()
+    assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (256, 960, 5568)
+
+
+def test_helper_overload_maps(ecx):
+    """ClayCodeHelper drives doDecodeSingle overload 2 per helper plane; the union of
+    the per-plane maps reproduces the oracle's overload-2 outputs."""
+    import ctypes
+    k, m, B = 4, 2, 16
+    n = 6
+    rng = np.random.default_rng(5)
+    for e in range(n):
+        oc = O.Clay(k, m, [e])
+        hidx = oc.helper_planes(e)
+        helper = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(len(hidx) * n)]
+        ref = [np.zeros(B, np.uint8) for _ in range(oc.alpha)]
+        for i in range(len(hidx)):
+            oc.decode_single_helper(helper, i, ref, e, B)
+        step = ecx.ClayCodeErasureDecodingStep([e], k, m)
+        assert step.getHelperPlanesIndexes(e) == hidx
