@@ -98,12 +98,26 @@ SIGNATURES = {
 _lib = None
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm wheels bundle their own libamdhip64 (SONAME libamdhip64.so.7,
+    but requested by the unversioned name).  If libecx were loaded first, the
+    dynamic loader would map /opt/rocm's runtime for libecx and then a second
+    copy for torch -- two HIP runtimes in one process.  Importing torch first
+    makes libecx bind to the runtime torch already mapped (matching SONAME), so
+    torch tensors / streams and libecx launches share one runtime."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     """Load libecx.so (building it first if this checkout has no build)."""
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
             build()
+        _share_torch_hip_runtime()
         l = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
             f = getattr(l, name)

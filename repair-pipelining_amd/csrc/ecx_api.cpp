@@ -535,6 +535,16 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
     });
 }
 
+// ---------------------------------------------------------------- tuning hook (include/ecx_tune.h)
+int ecx_tune(const char *key, int value) {
+    const std::string k = key ? key : "";
+    Tuning &t = tuning();
+    if (k == "items_per_block") t.items_per_block = value < 0 ? 0 : value;
+    else if (k == "nontemporal") t.nontemporal = value != 0;
+    else return ECX_E_ILLEGAL_ARGUMENT;
+    return ECX_OK;
+}
+
 // ---------------------------------------------------------------- synthetic data / verification
 int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream) {
     return guarded([&]() -> int {

@@ -6,6 +6,11 @@
 
 namespace ecx {
 
+Tuning &tuning() {
+    static Tuning t;
+    return t;
+}
+
 void check_hip(hipError_t e, const char *what) {
     if (e != hipSuccess) throw Error(ECX_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }

@@ -70,8 +70,17 @@ struct ApplyArgs {
     const uint32_t *tiles;
     int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
     int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
+    int64_t total_items;  // k_gf_stream: (stripe, chunk) items in this launch
     int n_tiles;
+    int items_per_block;  // k_gf_stream: consecutive chunks per workgroup
 };
+
+// Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
+struct Tuning {
+    int items_per_block = 8;  // 0 = one chunk per workgroup (k_gf_apply)
+    int nontemporal = 0;      // non-temporal (streaming) loads/stores in k_gf_stream
+};
+Tuning &tuning();
 
 // Enqueue out = M * in over nstripes stripes (kernels.hip).
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,

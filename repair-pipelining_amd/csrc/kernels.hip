@@ -21,12 +21,32 @@
 namespace ecx {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+// The plan is read-only for the whole launch: read it through the constant
+// address space so every access is a scalar (s_load) fetch even in loops that
+// also store outputs (the compiler cannot otherwise prove no aliasing).
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+typedef const __attribute__((address_space(4))) u32x8 cu32x8;
+__device__ __forceinline__ cu32 *plan_ptr(const uint32_t *p) { return (cu32 *)p; }
 
 __host__ __device__ __forceinline__ bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
 __device__ __forceinline__ u32x4 load16(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
 
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
+    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return *reinterpret_cast<const u32x4 *>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
+    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else *reinterpret_cast<u32x4 *>(p) = v;
+}
 
 // Byte-granular versions for the ragged tail / unaligned layouts.
 __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, int valid) {
@@ -59,15 +79,13 @@ __device__ __forceinline__ uint32_t gf_mac4(uint32_t acc, const uint32_t *tb, ui
     return xor3(acc, p0, xor3(p1, p2, 0u));
 }
 
-typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-
 // One plan entry (input slot) against the tile's accumulators.  The 40 table
 // dwords are fetched as five 8-dword scalar loads that straddle the per-row
 // groups, so they are issued once per entry (not sunk into the per-row
 // branches); rows without a coefficient are skipped by scalar branches.
-__device__ __forceinline__ void apply_entry(const uint32_t *__restrict__ r, const u32x4 x, u32x4 (&acc)[kTileRows]) {
+__device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)[kTileRows]) {
     const uint32_t mmul = r[1], mone = r[2];
-    const u32x8 *__restrict__ tv = reinterpret_cast<const u32x8 *>(r + 4);
+    cu32x8 *tv = (cu32x8 *)(r + 4);
     const u32x8 v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3], v4 = tv[4];
     const uint32_t tb[40] = {v0[0], v0[1], v0[2], v0[3], v0[4], v0[5], v0[6], v0[7], v1[0], v1[1],
                              v1[2], v1[3], v1[4], v1[5], v1[6], v1[7], v2[0], v2[1], v2[2], v2[3],
@@ -101,7 +119,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
     const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
 
-    const uint32_t *__restrict__ tile = a.tiles + tl * kTileDwords;
+    cu32 *tile = plan_ptr(a.tiles) + tl * kTileDwords;
     const int ebeg = (int)tile[0];
     const int ecnt = (int)tile[1];
     const int nrows = (int)tile[2];
@@ -123,7 +141,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
 #pragma unroll
     for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
 
-    const uint32_t *__restrict__ ent = a.entries + (int64_t)ebeg * kEntryDwords;
+    cu32 *ent = plan_ptr(a.entries) + (int64_t)ebeg * kEntryDwords;
     // The host pads every tile's entry list to a multiple of kDepth and appends
     // kDepth dummy entries (no coefficients, slot = an input this tile reads),
     // so the ring refill below is unconditional and never copies a register
@@ -134,7 +152,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     for (int e0 = 0; e0 < ecnt; e0 += kDepth) {
 #pragma unroll
         for (int u = 0; u < kDepth; ++u) {
-            const uint32_t *__restrict__ r = ent + (int64_t)(e0 + u) * kEntryDwords;
+            cu32 *r = ent + (int64_t)(e0 + u) * kEntryDwords;
             apply_entry(r, ring[u], acc);  // consume the slot, then refill it:
             ring[u] = load(r[kDepth * kEntryDwords]);  // kDepth-1 loads stay in flight
         }
@@ -145,6 +163,76 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
             uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
             if (SAFE) store_partial(p, acc[o], valid);
             else store16(p, acc[o]);
+        }
+    }
+}
+
+// Streaming form of k_gf_apply for aligned layouts: one workgroup walks
+// `items_per_block` consecutive 4 KiB chunks (same output tile) and the load
+// ring runs straight across chunk boundaries, so a wave keeps kDepth-1 loads
+// in flight from its first entry to its last store -- no fill/drain bubble
+// per chunk and no dummy prefetches inside the block.
+template <bool NT>
+__global__ void __launch_bounds__(kBlockThreads) k_gf_stream(ApplyArgs a) {
+    const uint32_t tl = blockIdx.x % (uint32_t)a.n_tiles;
+    const uint32_t grp = blockIdx.x / (uint32_t)a.n_tiles;
+    cu32 *tile = plan_ptr(a.tiles) + tl * kTileDwords;
+    const int ecnt = (int)tile[1];  // multiple of kDepth (host padding)
+    const int nrows = (int)tile[2];
+    cu32 *ent = plan_ptr(a.entries) + (int64_t)tile[0] * kEntryDwords;
+
+    const uint32_t item0 = grp * (uint32_t)a.items_per_block;
+    const int nit = (int)min((uint32_t)a.items_per_block, (uint32_t)a.total_items - item0);
+    const uint32_t nch = (uint32_t)a.n_chunks;
+    auto in_off = [&](int it) -> int64_t {
+        const uint32_t gi = item0 + (uint32_t)it;
+        return (a.stripe_begin + gi / nch) * a.in_stripe_stride + (a.chunk_begin + gi % nch) * kChunkBytes;
+    };
+    auto out_off = [&](int it) -> int64_t {
+        const uint32_t gi = item0 + (uint32_t)it;
+        return (a.stripe_begin + gi / nch) * a.out_stripe_stride + (a.chunk_begin + gi % nch) * kChunkBytes;
+    };
+    const int64_t lane = (int64_t)threadIdx.x * 16;
+    const uint8_t *ib = a.in + lane;
+    uint8_t *ob = a.out + lane;
+
+    u32x4 acc[kTileRows];
+#pragma unroll
+    for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
+
+    if (ecnt == 0) {  // all-zero rows
+        for (int it = 0; it < nit; ++it)
+            for (int o = 0; o < nrows; ++o) st16<NT>(ob + out_off(it) + (int64_t)tile[4 + o] * a.out_slot_stride, acc[0]);
+        return;
+    }
+
+    int64_t cur = in_off(0), nxt = in_off(nit > 1 ? 1 : 0);
+    u32x4 ring[kDepth];
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) ring[u] = ld16<NT>(ib + cur + (int64_t)ent[u * kEntryDwords] * a.in_slot_stride);
+    int item = 0, e = 0;
+    const int total = nit * ecnt;
+    for (int g = 0; g < total; g += kDepth) {
+#pragma unroll
+        for (int u = 0; u < kDepth; ++u) {
+            apply_entry(ent + (int64_t)(e + u) * kEntryDwords, ring[u], acc);
+            const int ep = e + u + kDepth;
+            const bool wrap = ep >= ecnt;  // wave-uniform
+            cu32 *rp = ent + (int64_t)(wrap ? ep - ecnt : ep) * kEntryDwords;
+            ring[u] = ld16<NT>(ib + (wrap ? nxt : cur) + (int64_t)rp[0] * a.in_slot_stride);
+        }
+        e += kDepth;
+        if (e == ecnt) {
+            const int64_t oo = out_off(item);
+#pragma unroll
+            for (int o = 0; o < kTileRows; ++o) {
+                if (o < nrows) st16<NT>(ob + oo + (int64_t)tile[4 + o] * a.out_slot_stride, acc[o]);
+                acc[o] = (u32x4){0u, 0u, 0u, 0u};
+            }
+            e = 0;
+            ++item;
+            cur = nxt;
+            nxt = in_off(item + 1 < nit ? item + 1 : nit - 1);
         }
     }
 }
@@ -171,10 +259,26 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
 
+    const Tuning &tu = tuning();
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
         a.n_chunks = n_chunks;
+        if (!safe && tu.items_per_block > 0) {
+            const int64_t ipb = tu.items_per_block;
+            const int64_t max_items = ((int64_t)1 << 30) / a.n_tiles * ipb;
+            const int64_t stripes_per_launch = std::max<int64_t>(1, max_items / n_chunks);
+            for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
+                const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
+                a.stripe_begin = s0;
+                a.total_items = ns * n_chunks;
+                a.items_per_block = (int)ipb;
+                const dim3 grid((unsigned)(((a.total_items + ipb - 1) / ipb) * a.n_tiles));
+                if (tu.nontemporal) hipLaunchKernelGGL(k_gf_stream<true>, grid, dim3(kBlockThreads), 0, stream, a);
+                else hipLaunchKernelGGL(k_gf_stream<false>, grid, dim3(kBlockThreads), 0, stream, a);
+            }
+            return;
+        }
         const int64_t per_stripe = n_chunks * a.n_tiles;
         const int64_t max_blocks = (int64_t)1 << 30;
         const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / per_stripe);

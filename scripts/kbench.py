@@ -1,0 +1,85 @@
+"""In-process A/B of k_gf_apply / k_gf_stream launch shapes on the headline
+workload (Clay(4,2) repair, B = 32 KiB, resident pool), interleaved rounds
+(cdna_hip_programming.md 5.4 rule 24), plus two ceilings for this access
+pattern: an XOR-only map with the identical 20-read / 8-write layout, and a
+plain device-to-device copy.  Prints one JSON object per variant."""
+import argparse
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import rpamd  # noqa: E402
+
+K, M, B, ALPHA = 4, 2, 32768, 8
+ALGO = 20 * B + 8 * B
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pool", type=int, default=1 << 14)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="0:0,1:0,2:0,4:0,8:0,16:0,8:1,4:1")
+    args = ap.parse_args()
+    import torch
+    ecx = rpamd.load()
+    lib = ecx.lib()
+    import ctypes
+    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.ecx_tune.restype = ctypes.c_int
+    P = args.pool
+    pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 1)
+    out = torch.empty((P, ALPHA, B), dtype=torch.uint8, device="cuda")
+    step = ecx.ClayCodeErasureDecodingStep([1], K, M)
+    mat, ins, outs = step.map().matrix()
+    xor_map = ecx.GfMap.from_matrix((mat != 0).astype("uint8"), in_slot=ins, out_slot=outs)
+    copy_src = pool.view(-1)[: P * ALPHA * B]
+
+    def clay():
+        step.performCodingBatch(pool, 48 * B, B, out, ALPHA * B, B, P, B)
+
+    def xor_only():
+        xor_map.apply_batch(pool, 48 * B, B, out, ALPHA * B, B, P, B)
+
+    def copy():
+        out.view(-1).copy_(copy_src)
+
+    variants = []
+    for v in args.variants.split(","):
+        ipb, nt = map(int, v.split(":"))
+        variants.append((f"clay ipb={ipb} nt={nt}", clay, ipb, nt, P * ALGO))
+    variants.append(("xor-only ipb=8 nt=0", xor_only, 8, 0, P * ALGO))
+    variants.append(("xor-only ipb=8 nt=1", xor_only, 8, 1, P * ALGO))
+    variants.append(("d2d copy (torch)", copy, 8, 0, 2 * P * ALPHA * B))
+
+    res = {name: [] for name, *_ in variants}
+    for r in range(args.rounds):
+        for name, fn, ipb, nt, nbytes in variants:
+            lib.ecx_tune(b"items_per_block", ipb)
+            lib.ecx_tune(b"nontemporal", nt)
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.launches):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.launches
+            res[name].append(nbytes / (ms * 1e-3) / 1e9)
+    for name, *_ in variants:
+        v = res[name]
+        print(json.dumps({"variant": name, "GBps_median": round(statistics.median(v), 1),
+                          "GBps_max": round(max(v), 1), "frac_of_8TBps": round(statistics.median(v) / 8000, 4)}))
+    lib.ecx_tune(b"items_per_block", 8)
+    lib.ecx_tune(b"nontemporal", 0)
+
+
+if __name__ == "__main__":
+    main()
