@@ -3,16 +3,21 @@
  * Not part of the reference's coding interface (include/ecx.h is the boundary);
  * results are bit-identical for every setting, only speed changes.
  *
- *   "items_per_block"  consecutive 4 KiB chunks one workgroup streams (default 8;
- *                      0 = one chunk per workgroup, the simple k_gf_apply form)
- *   "nontemporal"      1 = non-temporal (streaming) loads/stores in the streaming kernel
+ *   "items_per_block"  consecutive 4 KiB chunks one workgroup streams through the
+ *                      k_gf_stream kernel (default 0 = one chunk per workgroup, k_gf_apply)
+ *   "nontemporal"      1 = non-temporal (streaming) loads/stores (default 1)
+ *   "block_threads"    256 / 512 / 1024: k_gf_apply workgroup width (4 / 8 / 16 KiB per input)
  */
 #ifndef ECX_TUNE_H
 #define ECX_TUNE_H
+#include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
 #endif
 int ecx_tune(const char *key, int value); /* 0, or ECX_E_ILLEGAL_ARGUMENT for an unknown key */
+/* Pure-bandwidth probes over nbytes (multiple of 16 KiB) of device memory:
+ * kind 0 = read-only stream, kind 1 = copy src -> dst.  Enqueued on `stream`. */
+int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -541,8 +541,18 @@ int ecx_tune(const char *key, int value) {
     Tuning &t = tuning();
     if (k == "items_per_block") t.items_per_block = value < 0 ? 0 : value;
     else if (k == "nontemporal") t.nontemporal = value != 0;
-    else return ECX_E_ILLEGAL_ARGUMENT;
+    else if (k == "block_threads") {
+        if (value != 256 && value != 512 && value != 1024) return ECX_E_ILLEGAL_ARGUMENT;
+        t.block_threads = value;
+    } else return ECX_E_ILLEGAL_ARGUMENT;
     return ECX_OK;
+}
+
+int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream) {
+    return guarded([&]() -> int {
+        launch_probe(kind, src, dst, nbytes, nontemporal != 0, (hipStream_t)stream);
+        return ECX_OK;
+    });
 }
 
 // ---------------------------------------------------------------- synthetic data / verification

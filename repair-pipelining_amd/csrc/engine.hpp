@@ -77,9 +77,13 @@ struct ApplyArgs {
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
 struct Tuning {
-    int items_per_block = 8;  // 0 = one chunk per workgroup (k_gf_apply)
-    int nontemporal = 0;      // non-temporal (streaming) loads/stores in k_gf_stream
+    // Defaults are the fastest shape measured on MI355X (profiles/r01_kbench.txt):
+    // one 4 KiB chunk per workgroup with non-temporal loads/stores.
+    int items_per_block = 0;  // 0 = one chunk per workgroup (k_gf_apply); >0 = k_gf_stream
+    int nontemporal = 1;      // non-temporal (streaming) loads/stores
+    int block_threads = 256;  // k_gf_apply workgroup size (256 / 512 / 1024): chunk = 16 B x threads
 };
+void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();
 
 // Enqueue out = M * in over nstripes stripes (kernels.hip).

@@ -111,8 +111,8 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
     }
 }
 
-template <bool SAFE>
-__global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
+template <bool SAFE, bool NT, int THREADS>
+__global__ void __launch_bounds__(THREADS) k_gf_apply(ApplyArgs a) {
     const uint32_t w = blockIdx.x;
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     const int ecnt = (int)tile[1];
     const int nrows = (int)tile[2];
 
-    const int64_t off = c * kChunkBytes + (int64_t)threadIdx.x * 16;
+    const int64_t off = c * (THREADS * 16) + (int64_t)threadIdx.x * 16;
     const uint8_t *ib = a.in + s * a.in_stripe_stride + off;
     uint8_t *ob = a.out + s * a.out_stripe_stride + off;
     int valid = 16;
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     }
     auto load = [&](uint32_t slot) -> u32x4 {
         const uint8_t *p = ib + (int64_t)slot * a.in_slot_stride;
-        return SAFE ? load_partial(p, valid) : load16(p);
+        return SAFE ? load_partial(p, valid) : ld16<NT>(p);
     };
 
     u32x4 acc[kTileRows];
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
         if (o < nrows) {
             uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
             if (SAFE) store_partial(p, acc[o], valid);
-            else store16(p, acc[o]);
+            else st16<NT>(p, acc[o]);
         }
     }
 }
@@ -244,8 +244,11 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const DevicePlan &plan = cm.plan_for_current_device();
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
-    const int64_t full = aligned ? nbytes / kChunkBytes : 0;
-    const int64_t tail_chunks = (nbytes - full * kChunkBytes + kChunkBytes - 1) / kChunkBytes;
+    const Tuning &tu = tuning();
+    const int threads = tu.items_per_block > 0 ? kBlockThreads : tu.block_threads;
+    const int64_t chunk = (int64_t)threads * 16;
+    const int64_t full = aligned ? nbytes / chunk : 0;  // in units of `chunk`
+    const int64_t tail_chunks = (nbytes - full * chunk + kChunkBytes - 1) / kChunkBytes;  // 4 KiB units
 
     ApplyArgs a;
     a.in = in;
@@ -259,7 +262,6 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
 
-    const Tuning &tu = tuning();
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
@@ -286,12 +288,22 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
             a.stripe_begin = s0;
             const dim3 grid((unsigned)(ns * per_stripe));
-            if (safe) hipLaunchKernelGGL(k_gf_apply<true>, grid, dim3(kBlockThreads), 0, stream, a);
-            else hipLaunchKernelGGL(k_gf_apply<false>, grid, dim3(kBlockThreads), 0, stream, a);
+            if (safe) {
+                hipLaunchKernelGGL((k_gf_apply<true, false, kBlockThreads>), grid, dim3(kBlockThreads), 0, stream, a);
+            } else if (threads == 1024) {
+                if (tu.nontemporal) hipLaunchKernelGGL((k_gf_apply<false, true, 1024>), grid, dim3(1024), 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply<false, false, 1024>), grid, dim3(1024), 0, stream, a);
+            } else if (threads == 512) {
+                if (tu.nontemporal) hipLaunchKernelGGL((k_gf_apply<false, true, 512>), grid, dim3(512), 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply<false, false, 512>), grid, dim3(512), 0, stream, a);
+            } else {
+                if (tu.nontemporal) hipLaunchKernelGGL((k_gf_apply<false, true, 256>), grid, dim3(256), 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply<false, false, 256>), grid, dim3(256), 0, stream, a);
+            }
         }
     };
     run(false, 0, full);
-    run(true, full, tail_chunks);
+    run(true, full * (chunk / kChunkBytes), tail_chunks);
     check_hip(hipGetLastError(), "k_gf_apply launch");
 }
 
@@ -328,6 +340,42 @@ void launch_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, hipStream_t
     const unsigned blocks = (unsigned)std::min<int64_t>((granules + 255) / 256, 256 * 32);
     hipLaunchKernelGGL(k_fill_random, dim3(blocks), dim3(256), 0, stream, dst, nbytes, seed);
     check_hip(hipGetLastError(), "k_fill_random launch");
+}
+
+// ---------------------------------------------------------------- bandwidth probes (diagnostics)
+// Each workgroup streams a 16 KiB contiguous region: 4 x (256 lanes x 16 B).
+template <bool NT>
+__global__ void __launch_bounds__(256) k_probe_read(const uint8_t *src, int64_t nbytes, uint32_t *sink) {
+    const int64_t base = (int64_t)blockIdx.x * 16384 + threadIdx.x * 16;
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = ld16<NT>(src + base + k * 4096);
+    u32x4 x = v[0] ^ v[1] ^ v[2] ^ v[3];
+    uint32_t r = x.x ^ x.y ^ x.z ^ x.w;
+    if (r == 0x9E3779B9u) atomicXor(sink, r);  // practically never taken; keeps the loads live
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256) k_probe_copy(const uint8_t *src, uint8_t *dst, int64_t nbytes) {
+    const int64_t base = (int64_t)blockIdx.x * 16384 + threadIdx.x * 16;
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = ld16<NT>(src + base + k * 4096);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st16<NT>(dst + base + k * 4096, v[k]);
+}
+
+void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream) {
+    const unsigned blocks = (unsigned)(nbytes / 16384);
+    if (!blocks) return;
+    if (kind == 0) {
+        if (nt) hipLaunchKernelGGL(k_probe_read<true>, dim3(blocks), dim3(256), 0, stream, src, nbytes, (uint32_t *)dst);
+        else hipLaunchKernelGGL(k_probe_read<false>, dim3(blocks), dim3(256), 0, stream, src, nbytes, (uint32_t *)dst);
+    } else {
+        if (nt) hipLaunchKernelGGL(k_probe_copy<true>, dim3(blocks), dim3(256), 0, stream, src, dst, nbytes);
+        else hipLaunchKernelGGL(k_probe_copy<false>, dim3(blocks), dim3(256), 0, stream, src, dst, nbytes);
+    }
+    check_hip(hipGetLastError(), "probe launch");
 }
 
 // ---------------------------------------------------------------- verification

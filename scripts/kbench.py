@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--pool", type=int, default=1 << 14)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0:0,1:0,2:0,4:0,8:0,16:0,8:1,4:1")
+    ap.add_argument("--variants", default="0:0:256,0:1:256,0:1:512,0:1:1024,0:0:512,2:1:256,4:1:256,1:1:256")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
@@ -32,6 +32,9 @@ def main():
     import ctypes
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.ecx_tune.restype = ctypes.c_int
+    lib.ecx_probe_bandwidth.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.c_void_p]
+    lib.ecx_probe_bandwidth.restype = ctypes.c_int
     P = args.pool
     pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 1)
@@ -50,19 +53,30 @@ def main():
     def copy():
         out.view(-1).copy_(copy_src)
 
+    PROBE = (P * 48 * B) // 2 // 16384 * 16384
+    src, dst = pool.view(-1)[:PROBE], pool.view(-1)[PROBE:2 * PROBE]
+    cs = torch.cuda.current_stream().cuda_stream
+
+    def probe(kind, nt):
+        return lambda: lib.ecx_probe_bandwidth(kind, src.data_ptr(), dst.data_ptr(), PROBE, nt, cs)
+
     variants = []
     for v in args.variants.split(","):
-        ipb, nt = map(int, v.split(":"))
-        variants.append((f"clay ipb={ipb} nt={nt}", clay, ipb, nt, P * ALGO))
-    variants.append(("xor-only ipb=8 nt=0", xor_only, 8, 0, P * ALGO))
-    variants.append(("xor-only ipb=8 nt=1", xor_only, 8, 1, P * ALGO))
-    variants.append(("d2d copy (torch)", copy, 8, 0, 2 * P * ALPHA * B))
+        ipb, nt, th = map(int, v.split(":"))
+        variants.append((f"clay ipb={ipb} nt={nt} threads={th}", clay, ipb, nt, th, P * ALGO))
+    variants.append(("xor-only ipb=0 nt=1 threads=256", xor_only, 0, 1, 256, P * ALGO))
+    variants.append(("probe read nt=0", probe(0, 0), 0, 0, 256, PROBE))
+    variants.append(("probe read nt=1", probe(0, 1), 0, 0, 256, PROBE))
+    variants.append(("probe copy nt=0", probe(1, 0), 0, 0, 256, 2 * PROBE))
+    variants.append(("probe copy nt=1", probe(1, 1), 0, 0, 256, 2 * PROBE))
+    variants.append(("d2d copy (torch)", copy, 0, 0, 256, 2 * P * ALPHA * B))
 
     res = {name: [] for name, *_ in variants}
     for r in range(args.rounds):
-        for name, fn, ipb, nt, nbytes in variants:
+        for name, fn, ipb, nt, th, nbytes in variants:
             lib.ecx_tune(b"items_per_block", ipb)
             lib.ecx_tune(b"nontemporal", nt)
+            lib.ecx_tune(b"block_threads", th)
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -77,8 +91,7 @@ def main():
         v = res[name]
         print(json.dumps({"variant": name, "GBps_median": round(statistics.median(v), 1),
                           "GBps_max": round(max(v), 1), "frac_of_8TBps": round(statistics.median(v) / 8000, 4)}))
-    lib.ecx_tune(b"items_per_block", 8)
-    lib.ecx_tune(b"nontemporal", 0)
+
 
 
 if __name__ == "__main__":
