@@ -34,6 +34,7 @@ READ_BYTES = 20 * B                          # helper sub-chunks read by one rep
 WRITE_BYTES = ALPHA * B                      # repaired sub-chunks written
 ALGO_BYTES = READ_BYTES + WRITE_BYTES        # 917,504 B per stripe
 HBM_PEAK_GBS = 8000.0                        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KERNEL = "k_gf_apply<false,true,256>"  # dominant kernel (SAFE=false, NT=true, 256 threads)
 METRIC = "GiB/s repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU"
 
 
@@ -92,7 +93,7 @@ def pmc_traffic(pool: int):
         return None
     try:
         d = json.loads(f.read_text())
-        if d.get("pool_stripes") == pool and d.get("kernel") == "k_gf_apply<false>":
+        if d.get("pool_stripes") == pool and d.get("kernel") == KERNEL:
             return d["hbm_bytes_per_launch"]
     except Exception:
         return None
@@ -210,7 +211,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_gf_apply<false>",
+                "kernel": KERNEL,
                 "avg_launch_ms": round(launch_ms, 4),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
             },
