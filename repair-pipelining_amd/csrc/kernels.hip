@@ -142,20 +142,25 @@ __global__ void __launch_bounds__(THREADS) k_gf_apply(ApplyArgs a) {
     for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
 
     cu32 *ent = plan_ptr(a.entries) + (int64_t)ebeg * kEntryDwords;
-    // The host pads every tile's entry list to a multiple of kDepth and appends
-    // kDepth dummy entries (no coefficients, slot = an input this tile reads),
-    // so the ring refill below is unconditional and never copies a register
-    // whose load is still in flight.
-    u32x4 ring[kDepth];
+    // The host pads every tile's entry list to a multiple of kDepth, so the
+    // ring refill inside the loop is unconditional and never copies a
+    // register whose load is still in flight; the last group is peeled and
+    // issues no refill (no loads past the tile's real entries).
+    if (ecnt > 0) {
+        u32x4 ring[kDepth];
 #pragma unroll
-    for (int u = 0; u < kDepth; ++u) ring[u] = load(ent[u * kEntryDwords]);
-    for (int e0 = 0; e0 < ecnt; e0 += kDepth) {
+        for (int u = 0; u < kDepth; ++u) ring[u] = load(ent[u * kEntryDwords]);
+        const int last = ecnt - kDepth;
+        for (int e0 = 0; e0 < last; e0 += kDepth) {
 #pragma unroll
-        for (int u = 0; u < kDepth; ++u) {
-            cu32 *r = ent + (int64_t)(e0 + u) * kEntryDwords;
-            apply_entry(r, ring[u], acc);  // consume the slot, then refill it:
-            ring[u] = load(r[kDepth * kEntryDwords]);  // kDepth-1 loads stay in flight
+            for (int u = 0; u < kDepth; ++u) {
+                cu32 *r = ent + (int64_t)(e0 + u) * kEntryDwords;
+                apply_entry(r, ring[u], acc);              // consume the slot, then refill it:
+                ring[u] = load(r[kDepth * kEntryDwords]);  // kDepth-1 loads stay in flight
+            }
         }
+#pragma unroll
+        for (int u = 0; u < kDepth; ++u) apply_entry(ent + (int64_t)(last + u) * kEntryDwords, ring[u], acc);
     }
 #pragma unroll
     for (int o = 0; o < kTileRows; ++o) {
