@@ -27,8 +27,19 @@ __all__ = [
     "InputOutputByteTableCodingLoopSingle", "ReedSolomon", "GfMap", "ClayCodeUtil",
     "ClayCodeErasureDecodingStep", "ClayCode", "LRCErasureCode", "LRCErasureUtil", "JavaRandom",
     "lrc_encode", "lrc_encode_using_single", "lrc_decode", "sample_encode", "sample_decode",
-    "device_count", "set_device", "fill_random", "count_mismatch",
+    "device_count", "set_device", "fill_random", "count_mismatch", "shard_stripes",
 ]
+
+
+def shard_stripes(n_stripes: int, world: int, rank: int):
+    """Stripe range [begin, end) that rank `rank` of `world` owns.  Stripes are
+    independent (every repair reads only its own stripe), so the batch is split
+    into contiguous ranges with no data exchange between GPUs."""
+    if world <= 0 or not 0 <= rank < world or n_stripes < 0:
+        raise ValueError("invalid partition request")
+    base, extra = divmod(n_stripes, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
 
 
 # ---------------------------------------------------------------- helpers

@@ -1,0 +1,109 @@
+"""End-to-end (host-memory) Clay(4,2) repair rate, PCIe included.
+
+The reference path starts and ends in host memory (helper sub-chunks arrive
+on sockets, ClayCoordinator.kt:372-395).  Here the 20 helper sub-chunks of
+each stripe sit in pinned host memory in arrival order ([S][20][B]); chunks of
+stripes are pipelined H2D (copy stream) -> repair kernel (compute stream) ->
+D2H (copy stream) over NB device buffer sets, and the wall time of the whole
+batch is measured.  Prints one JSON line (recorded in DESIGN.md; never the
+bench `value`)."""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import rpamd  # noqa: E402
+
+B = 32768
+ALGO = 28 * B
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=8192)
+    ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--buffers", type=int, default=3)
+    ap.add_argument("--repeats", type=int, default=3)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    ecx = rpamd.load()
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    mat, ins, outs = step.map().matrix()
+    cmap = ecx.GfMap.from_matrix(mat, in_slot=list(range(20)), out_slot=list(range(8)))
+
+    S, C, NB = args.stripes, args.chunk, args.buffers
+    h_in = torch.empty((S, 20, B), dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty((S, 8, B), dtype=torch.uint8, pin_memory=True)
+    d_tmp = torch.empty((S, 20, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(d_tmp, d_tmp.numel(), 99)
+    h_in.copy_(d_tmp)
+    del d_tmp
+    d_in = [torch.empty((C, 20, B), dtype=torch.uint8, device="cuda") for _ in range(NB)]
+    d_out = [torch.empty((C, 8, B), dtype=torch.uint8, device="cuda") for _ in range(NB)]
+    s_h2d, s_cmp, s_d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+
+    def run():
+        free = [None] * NB
+        nchunks = (S + C - 1) // C
+        for i in range(nchunks):
+            k = i % NB
+            lo, hi = i * C, min(S, (i + 1) * C)
+            n = hi - lo
+            with torch.cuda.stream(s_h2d):
+                if free[k] is not None:
+                    s_h2d.wait_event(free[k])
+                d_in[k][:n].copy_(h_in[lo:hi], non_blocking=True)
+                ev_in = torch.cuda.Event()
+                ev_in.record(s_h2d)
+            s_cmp.wait_event(ev_in)
+            cmap.apply_batch(d_in[k], 20 * B, B, d_out[k], 8 * B, B, n, B, stream=s_cmp)
+            ev_c = torch.cuda.Event()
+            ev_c.record(s_cmp)
+            with torch.cuda.stream(s_d2h):
+                s_d2h.wait_event(ev_c)
+                h_out[lo:hi].copy_(d_out[k][:n], non_blocking=True)
+                ev_o = torch.cuda.Event()
+                ev_o.record(s_d2h)
+                free[k] = ev_o
+        torch.cuda.synchronize()
+
+    run()  # warm-up
+    times = []
+    for _ in range(args.repeats):
+        t0 = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    # one sampled stripe against the oracle
+    import oracle as O
+    s = S // 2
+    hin = h_in[s].numpy()
+    inputs = [None] * 48
+    for j, slot in enumerate(ins):
+        inputs[int(slot)] = hin[j].copy()
+    for i in range(48):
+        if inputs[i] is None and (i % 6) != 1:
+            inputs[i] = np.zeros(B, np.uint8)  # never read by the e=1 repair (not a helper slot)
+    ref = [np.zeros(B, np.uint8) for _ in range(8)]
+    O.Clay(4, 2, [1]).perform_coding(inputs, ref, B)
+    ok = all((h_out[s, z].numpy() == ref[z]).all() for z in range(8))
+    print(json.dumps({
+        "what": "end-to-end Clay(4,2) repair, host pinned -> H2D -> kernel -> D2H -> host pinned",
+        "stripes": S, "chunk_stripes": C, "buffers": NB,
+        "seconds": round(best, 4),
+        "GiB_per_s_algorithmic": round(S * ALGO / best / 2**30, 2),
+        "h2d_GB_per_s": round(S * 20 * B / best / 1e9, 2),
+        "d2h_GB_per_s": round(S * 8 * B / best / 1e9, 2),
+        "oracle_check_sampled_stripe": ok,
+    }))
+
+
+if __name__ == "__main__":
+    main()
