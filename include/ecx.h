@@ -129,6 +129,14 @@ int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **
 typedef struct ecx_clay ecx_clay;
 /* new ClayCodeErasureDecodingStep(erasedIndexes, RS(2,2), RS(k,m)) -- ClayCode.java:28-41, :43-51 */
 int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_erased, ecx_clay **out);
+/* Shortened Clay: Clay(data+virtual, parity) whose data nodes
+ * [data, data+virtual) are virtual all-zero nodes, e.g. Clay(10,4) = Clay(12,4)
+ * with 2 virtual nodes (the reference's integer t = (k+m)/m cannot build
+ * Clay(10,4), ClayCodeErasureDecodingStep.java:692).  Every slot index, erased
+ * index and geometry query then refers to the data+parity REAL nodes; the
+ * results equal the reference Clay(12,4) run with the virtual nodes zero-filled. */
+int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
+                              ecx_clay **out);
 void ecx_clay_destroy(ecx_clay *clay);
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha); /* ClayCodeUtil :690-695 */
 int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out /* alpha */); /* :924-941 */

@@ -362,10 +362,16 @@ class ClayCodeUtil:
 class ClayCodeErasureDecodingStep:
     """new ClayCodeErasureDecodingStep(erasedIndexes, RS(2,2), RS(k,m)) (:43-51)."""
 
-    def __init__(self, erasedIndexes, numDataUnits: int, numParityUnits: int):
+    def __init__(self, erasedIndexes, numDataUnits: int, numParityUnits: int, virtualUnits: int = 0):
+        """virtualUnits > 0: shortened code, Clay(k+v, m) with v virtual zero data nodes
+        (e.g. Clay(10,4) = ClayCodeErasureDecodingStep(e, 10, 4, virtualUnits=2))."""
         er = np.ascontiguousarray(list(erasedIndexes), np.int32)
         h = ctypes.c_void_p()
-        check(lib().ecx_clay_create(numDataUnits, numParityUnits, er.ctypes.data, len(er), ctypes.byref(h)))
+        if virtualUnits:
+            check(lib().ecx_clay_create_shortened(numDataUnits, numParityUnits, virtualUnits, er.ctypes.data,
+                                                  len(er), ctypes.byref(h)))
+        else:
+            check(lib().ecx_clay_create(numDataUnits, numParityUnits, er.ctypes.data, len(er), ctypes.byref(h)))
         self._h = h
         self.erasedIndexes = list(erasedIndexes)
         self.numDataUnits, self.numParityUnits = numDataUnits, numParityUnits
@@ -373,7 +379,8 @@ class ClayCodeErasureDecodingStep:
         q, t, a = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib().ecx_clay_geometry(h, ctypes.byref(q), ctypes.byref(t), ctypes.byref(a)))
         self.q, self.t, self.subPacketSize = q.value, t.value, a.value
-        self.util = ClayCodeUtil(erasedIndexes, numDataUnits, numParityUnits)
+        self.virtualUnits = virtualUnits
+        self.util = ClayCodeUtil(erasedIndexes, numDataUnits + virtualUnits, numParityUnits)
 
     def __del__(self):
         if getattr(self, "_h", None):

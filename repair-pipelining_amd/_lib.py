@@ -84,6 +84,7 @@ SIGNATURES = {
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_rs_decode_map": (I, [P, P, ctypes.POINTER(P)]),
     "ecx_clay_create": (I, [I, I, P, I, ctypes.POINTER(P)]),
+    "ecx_clay_create_shortened": (I, [I, I, I, P, I, ctypes.POINTER(P)]),
     "ecx_clay_destroy": (None, [P]),
     "ecx_clay_geometry": (I, [P, PI, PI, PI]),
     "ecx_clay_helper_planes": (I, [P, I, P]),

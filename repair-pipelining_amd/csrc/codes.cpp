@@ -141,11 +141,16 @@ int ipow(int b, int e) {
 }
 }  // namespace
 
-ClayPlanner::ClayPlanner(int data_units, int parity_units, std::vector<int> erased)
-    : k_(data_units), m_(parity_units), erased_(std::move(erased)), pair_(2, 2), rs_(data_units, parity_units) {
-    if (parity_units <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "parity units must be positive");
+ClayPlanner::ClayPlanner(int data_units, int parity_units, std::vector<int> erased, int virtual_units)
+    : k_(data_units + virtual_units), m_(parity_units), v_(virtual_units), erased_real_(std::move(erased)),
+      pair_(2, 2), rs_(data_units + virtual_units, parity_units) {
+    if (parity_units <= 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid unit counts");
+    for (int e : erased_real_) {
+        if (v_ > 0 && (e < 0 || e >= n_real())) throw Error(ECX_E_INDEX, "erased index out of range");
+        erased_.push_back(under(e));
+    }
     q_ = parity_units;
-    t_ = (parity_units + data_units) / parity_units;  // integer division, ClayCodeUtil :692
+    t_ = (parity_units + k_) / parity_units;  // integer division, ClayCodeUtil :692
     if (t_ > 16) throw Error(ECX_E_ILLEGAL_ARGUMENT, "sub-packetization too large");
     alpha_ = ipow(q_, t_);
     if ((long long)n() * alpha_ > 16384)
@@ -194,7 +199,8 @@ int ClayPlanner::intersection_score(int z) const {
     return s;
 }
 
-std::vector<int> ClayPlanner::helper_planes(int e) const {
+std::vector<int> ClayPlanner::helper_planes(int e_real) const {
+    const int e = v_ > 0 ? under(e_real) : e_real;
     const int x = nx(e), y = ny(e);
     if (e < 0 || y >= t_) throw Error(ECX_E_INDEX, "erased node outside the q x t grid");
     std::vector<int> out;
@@ -332,8 +338,8 @@ void ClayPlanner::decode_multi(std::vector<SymBuf> in, std::vector<SymBuf> &outp
 }
 
 LinearMap ClayPlanner::perform_coding_map(const std::vector<bool> &input_present) const {
-    const int nn = n(), ne = (int)erased_.size();
-    const int width = nn * alpha_;
+    const int nn = n(), nr = n_real(), ne = (int)erased_.size();
+    const int width = nr * alpha_;  // symbolic inputs = the real slots
     if ((int)input_present.size() != width) throw Error(ECX_E_ILLEGAL_ARGUMENT, "Invalid inputs length");
     LinearMap mp;
     mp.n_in = width;
@@ -343,13 +349,18 @@ LinearMap ClayPlanner::perform_coding_map(const std::vector<bool> &input_present
         throw Error(ECX_E_ILLEGAL_ARGUMENT, "Invalid inputs are found, all being null");
     for (int e : erased_)
         if (e < 0 || e >= nn) throw Error(ECX_E_INDEX, "erased index out of range");
-    std::vector<SymBuf> in(width);
-    for (int j = 0; j < width; ++j)
-        if (input_present[j]) in[j] = unit(width, j);
+    // underlying n*alpha inputs; virtual nodes are present, all-zero buffers
+    std::vector<SymBuf> in((size_t)nn * alpha_);
+    for (int z = 0; z < alpha_; ++z) {
+        for (int r = 0; r < nr; ++r)
+            if (input_present[(size_t)z * nr + r]) in[(size_t)z * nn + under(r)] = unit(width, z * nr + r);
+        for (int u = 0; u < nn; ++u)
+            if (is_virtual(u)) in[(size_t)z * nn + u] = zeros(width);
+    }
     std::vector<SymBuf> outputs((size_t)ne * alpha_);
     if (ne == 1) {
         const int e = erased_[0];
-        const std::vector<int> hidx = helper_planes(e);
+        const std::vector<int> hidx = helper_planes(erased_real_[0]);
         std::vector<SymBuf> helper(hidx.size() * nn);
         for (size_t h = 0; h < hidx.size(); ++h)  // getHelperPlanes :291-300
             for (int j = 0; j < nn; ++j) helper[h * nn + j] = in[(size_t)hidx[h] * nn + j];
@@ -368,16 +379,20 @@ LinearMap ClayPlanner::perform_coding_map(const std::vector<bool> &input_present
 
 LinearMap ClayPlanner::decode_single_helper_map(const std::vector<bool> &helper_present, int helper_i,
                                                 int erased_index, std::vector<bool> *written) const {
-    const int nn = n();
+    const int nn = n(), nr = n_real();
     const std::vector<int> hidx = helper_planes(erased_index);
-    const int width = (int)hidx.size() * nn;
+    const int width = (int)hidx.size() * nr;
     if ((int)helper_present.size() != width) throw Error(ECX_E_ILLEGAL_ARGUMENT, "helper plane array size");
     if (helper_i < 0 || helper_i >= (int)hidx.size()) throw Error(ECX_E_INDEX, "helper plane index");
-    std::vector<SymBuf> helper(width);
-    for (int j = 0; j < width; ++j)
-        if (helper_present[j]) helper[j] = unit(width, j);
+    std::vector<SymBuf> helper(hidx.size() * nn);
+    for (size_t h = 0; h < hidx.size(); ++h) {
+        for (int r = 0; r < nr; ++r)
+            if (helper_present[h * nr + r]) helper[h * nn + under(r)] = unit(width, (int)h * nr + r);
+        for (int u = 0; u < nn; ++u)
+            if (is_virtual(u)) helper[h * nn + u] = zeros(width);
+    }
     std::vector<SymBuf> outputs(alpha_);
-    single_plane(helper, hidx, helper_i, erased_index, outputs, width);
+    single_plane(helper, hidx, helper_i, v_ > 0 ? under(erased_index) : erased_index, outputs, width);
     LinearMap mp;
     mp.n_in = width;
     for (int j = 0; j < width; ++j) mp.in_slot.push_back(j);

@@ -60,16 +60,23 @@ private:
 };
 
 // ClayCodeErasureDecodingStep.java + ClayCodeUtil (:676-944), symbolically.
+//
+// virtual_units > 0 builds a SHORTENED code: Clay(k + v, m) whose data nodes
+// [k, k+v) are virtual, always-zero nodes (Clay(10,4) as
+// Clay(12,4) with 2 zero data nodes).  All public slot numbering is over the
+// k + m REAL nodes (real node r < k is underlying r, r >= k is r + v).
 class ClayPlanner {
 public:
-    ClayPlanner(int data_units, int parity_units, std::vector<int> erased);
+    ClayPlanner(int data_units, int parity_units, std::vector<int> erased, int virtual_units = 0);
     int k() const { return k_; }
     int m() const { return m_; }
-    int n() const { return k_ + m_; }
+    int n() const { return k_ + m_; }           // underlying code
+    int n_real() const { return k_ + m_ - v_; }  // nodes that exist (slot numbering)
+    int virtual_units() const { return v_; }
     int q() const { return q_; }
     int t() const { return t_; }
     int alpha() const { return alpha_; }
-    const std::vector<int> &erased() const { return erased_; }
+    const std::vector<int> &erased() const { return erased_real_; }
 
     std::vector<int> helper_planes(int erased_index) const;  // getHelperPlanesIndexes :924-941
 
@@ -83,8 +90,11 @@ public:
                                        std::vector<bool> *written) const;
 
 private:
-    int k_, m_, q_, t_, alpha_;
-    std::vector<int> erased_;
+    int k_, m_, v_, q_, t_, alpha_;
+    std::vector<int> erased_;       // underlying node indices
+    std::vector<int> erased_real_;  // as given (real node indices)
+    int under(int real_node) const { return real_node < k_ - v_ ? real_node : real_node + v_; }
+    bool is_virtual(int u) const { return u >= k_ - v_ && u < k_; }
     RsCode pair_, rs_;
 
     std::vector<int> zvec(int z) const;

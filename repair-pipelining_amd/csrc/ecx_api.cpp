@@ -24,7 +24,7 @@ struct ecx_rs {
 };
 
 struct ecx_clay {
-    ecx_clay(int k, int m, std::vector<int> e) : pl(k, m, std::move(e)) {}
+    ecx_clay(int k, int m, std::vector<int> e, int v = 0) : pl(k, m, std::move(e), v) {}
     ClayPlanner pl;
     std::mutex mu;
     std::map<std::string, std::unique_ptr<ecx_map>> maps;
@@ -94,7 +94,7 @@ ecx_map *rs_decode_map(ecx_rs *rs, const std::vector<bool> &present) {
 }
 
 ecx_map *clay_standard_map(ecx_clay *c) {
-    const int n = c->pl.n(), a = c->pl.alpha();
+    const int n = c->pl.n_real(), a = c->pl.alpha();
     std::vector<bool> present((size_t)n * a, true);
     for (int z = 0; z < a; ++z)
         for (int e : c->pl.erased())
@@ -458,6 +458,16 @@ int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_e
     });
 }
 
+int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
+                              ecx_clay **out) {
+    return guarded([&]() -> int {
+        *out = nullptr;
+        if (n_erased < 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased / virtual_units");
+        *out = new ecx_clay(data_units, parity_units, std::vector<int>(erased, erased + n_erased), virtual_units);
+        return ECX_OK;
+    });
+}
+
 void ecx_clay_destroy(ecx_clay *clay) { delete clay; }
 
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha) {
@@ -479,7 +489,7 @@ int ecx_clay_perform_coding(ecx_clay *clay, const uint8_t *const *inputs, uint8_
     return guarded([&]() -> int {
         if (clay->pl.erased().empty()) return ECX_OK;
         if (buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "buf_size");
-        const int w = clay->pl.n() * clay->pl.alpha();
+        const int w = clay->pl.n_real() * clay->pl.alpha();
         std::vector<bool> present(w);
         for (int j = 0; j < w; ++j) present[j] = inputs[j] != nullptr;
         ecx_map *m;
@@ -499,7 +509,7 @@ int ecx_clay_decode_single_helper(ecx_clay *clay, const uint8_t *const *helper_c
     return guarded([&]() -> int {
         if (buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "buf_size");
         const int nh = (int)clay->pl.helper_planes(erased_index).size();
-        const int w = nh * clay->pl.n();
+        const int w = nh * clay->pl.n_real();
         std::vector<bool> present(w);
         for (int j = 0; j < w; ++j) present[j] = helper_coupled[j] != nullptr;
         ecx_map *m;

@@ -389,3 +389,40 @@ def test_lrc_batch_config3(ecx, torch_dev):
     repair.apply_batch(pool, 16 * B, B, out, B, B, S, B)
     torch.cuda.synchronize()
     assert torch.equal(out[:, 0], pool[:, 2])
+
+
+def test_clay104_shortened_batch_roundtrip(ecx, torch_dev):
+    """BASELINE config 4 shape: shortened Clay(10,4) (= Clay(12,4) with 2 virtual zero
+    data nodes), 1 MiB node blocks = 256 planes x 4 KiB; encode on the GPU, erase,
+    repair, compare; one stripe against the oracle (reference Clay(12,4), zero-filled)."""
+    torch = torch_dev
+    k, m, v, B, S = 10, 4, 2, 4096, 4
+    n = k + m
+    enc = ecx.ClayCodeErasureDecodingStep(list(range(k, n)), k, m, virtualUnits=v)
+    a = enc.subPacketSize
+    assert a == 256
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 404)
+    par = torch.empty((S, m * a, B), dtype=torch.uint8, device="cuda")
+    enc.performCodingBatch(pool, n * a * B, B, par, m * a * B, B, S, B)
+    pool.view(S, a, n, B)[:, :, k:, :] = par.view(S, a, m, B)
+    for e in (0, 3, 9, 10, 13):
+        out = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
+        ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v).performCodingBatch(
+            pool, n * a * B, B, out, a * B, B, S, B)
+        torch.cuda.synchronize()
+        assert torch.equal(out, pool.view(S, a, n, B)[:, :, e, :]), e
+    # oracle: reference Clay(12,4) with the virtual nodes zero-filled, stripe 0, parity of plane 0..255
+    host = pool[0].cpu().numpy()
+    und = lambda r: r if r < k else r + v
+    inputs = [None] * (16 * a)
+    for z in range(a):
+        for r in range(k):
+            inputs[z * 16 + und(r)] = host[z * n + r].copy()
+        for u in range(k, k + v):
+            inputs[z * 16 + u] = np.zeros(B, np.uint8)
+    ref = [np.zeros(B, np.uint8) for _ in range(m * a)]
+    O.Clay(12, 4, [12, 13, 14, 15]).perform_coding(inputs, ref, B)
+    for z in range(0, a, 17):
+        for j in range(m):
+            assert (host[z * n + k + j] == ref[z * m + j]).all()

@@ -119,3 +119,44 @@ def test_helper_overload_maps(ecx):
             oc.decode_single_helper(helper, i, ref, e, B)
         step = ecx.ClayCodeErasureDecodingStep([e], k, m)
         assert step.getHelperPlanesIndexes(e) == hidx
+
+
+def _shortened_oracle(k, m, v, erased_real, inputs_real, B):
+    """Oracle for a shortened code: the reference Clay(k+v, m) with the v virtual
+    data nodes zero-filled."""
+    n_r, n_u = k + m, k + v + m
+    und = lambda r: r if r < k else r + v
+    c = O.Clay(k + v, m, [und(e) for e in erased_real])
+    a = c.alpha
+    inputs = [None] * (n_u * a)
+    for z in range(a):
+        for r in range(n_r):
+            inputs[z * n_u + und(r)] = inputs_real[z * n_r + r]
+        for u in range(k, k + v):
+            inputs[z * n_u + u] = np.zeros(B, np.uint8)
+    outs = [np.zeros(B, np.uint8) for _ in range(len(erased_real) * a)]
+    c.perform_coding(inputs, outs, B)
+    return outs
+
+
+@pytest.mark.parametrize("k,m,v,erased", [(10, 4, 2, [3]), (10, 4, 2, [13]), (10, 4, 2, [10, 11, 12, 13]),
+                                          (3, 2, 1, [1]), (3, 2, 1, [3, 4])])
+def test_shortened_clay_map_vs_oracle(ecx, k, m, v, erased):
+    step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
+    n = k + m
+    a = step.subPacketSize
+    B = 8
+    rng = np.random.default_rng(3 + sum(erased))
+    inputs = [None if (i % n) in erased else rng.integers(0, 256, B, dtype=np.uint8) for i in range(n * a)]
+    ref = _shortened_oracle(k, m, v, erased, inputs, B)
+    mat, ins, outs = step.map().matrix()
+    assert ins.max() < n * a
+    got = gf_apply_numpy(mat, [inputs[j] for j in ins])
+    for o in range(len(outs)):
+        assert (got[o] == ref[o]).all(), o
+
+
+def test_clay104_shortened_shape(ecx):
+    """BASELINE config 4: Clay(10,4) repair reads 13 real helper nodes x 64 planes."""
+    inf = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2).map().info()
+    assert inf["n_out"] == 256 and inf["n_in"] == 13 * 64
