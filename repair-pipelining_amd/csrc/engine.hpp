@@ -73,6 +73,7 @@ struct ApplyArgs {
     int64_t total_items;  // k_gf_stream: (stripe, chunk) items in this launch
     int n_tiles;
     int items_per_block;  // k_gf_stream: consecutive chunks per workgroup
+    int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -82,6 +83,7 @@ struct Tuning {
     int items_per_block = 0;  // 0 = one chunk per workgroup (k_gf_apply); >0 = k_gf_stream
     int nontemporal = 1;      // non-temporal (streaming) loads/stores
     int block_threads = 256;  // k_gf_apply workgroup size (256 / 512 / 1024): chunk = 16 B x threads
+    int xcd_group = 1;        // multi-tile maps: tiles of a chunk on one XCD (logical_block)
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();

@@ -111,9 +111,21 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
     }
 }
 
+// Logical work index of this workgroup.  Multi-tile maps re-read inputs across
+// the tiles of one (stripe, chunk); with `xcd_group` the tiles of a chunk are
+// given consecutive workgroups of ONE XCD (blocks b and b+8 share an XCD under
+// the observed round-robin dispatch; a speed choice only) so the re-reads are
+// served by that XCD's L2.  Bijective for any grid size.
+__device__ __forceinline__ uint32_t logical_block(bool xcd_group) {
+    const uint32_t b = blockIdx.x;
+    if (!xcd_group) return b;
+    const uint32_t g = gridDim.x, q = g / 8, r = g % 8, xcd = b % 8, j = b / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+}
+
 template <bool SAFE, bool NT, int THREADS>
 __global__ void __launch_bounds__(THREADS) k_gf_apply(ApplyArgs a) {
-    const uint32_t w = blockIdx.x;
+    const uint32_t w = logical_block(a.xcd_group != 0);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
     const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
@@ -266,6 +278,9 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.out_slot_stride = out_slot_stride;
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
+    a.xcd_group = (tuning().xcd_group && a.n_tiles > 1) ? 1 : 0;
+    a.items_per_block = 0;
+    a.total_items = 0;
 
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;

@@ -71,9 +71,17 @@ def main():
     out = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
     step = ecx.ClayCodeErasureDecodingStep([3], k, m, virtualUnits=v)
     inf = step.map().info()
-    t = timed(lambda: step.performCodingBatch(pool, n * a * B, B, out, a * B, B, S, B), reps=5)
-    report("Clay(10,4) shortened, 1 MiB blocks, single repair (e=3)", (inf["n_in"] + inf["n_out"]) * B, S, t,
-           {"map": inf})
+    import ctypes
+    lib = ecx.lib()
+    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    for xcd, nt in ((1, 1), (0, 1), (1, 0), (0, 0)):
+        lib.ecx_tune(b"xcd_group", xcd)
+        lib.ecx_tune(b"nontemporal", nt)
+        t = timed(lambda: step.performCodingBatch(pool, n * a * B, B, out, a * B, B, S, B), reps=5)
+        report("Clay(10,4) shortened, 1 MiB blocks, single repair (e=3)", (inf["n_in"] + inf["n_out"]) * B, S, t,
+               {"map": inf, "xcd_group": xcd, "nontemporal": nt})
+    lib.ecx_tune(b"xcd_group", 1)
+    lib.ecx_tune(b"nontemporal", 1)
     del pool, out
     # ---- config 5: RS(12,4), 4 MiB shards, erasures {0,1}, in place
     L, S = 4 << 20, 256
