@@ -5,9 +5,9 @@
  *
  *   "items_per_block"  consecutive 4 KiB chunks one workgroup streams through the
  *                      k_gf_stream kernel (default 0 = one chunk per workgroup, k_gf_apply)
- *   "nontemporal"      1 = non-temporal (streaming) loads/stores (default 1)
- *   "xcd_group"        1 = multi-tile maps keep the tiles of one chunk on one XCD (default 1)
- *   "block_threads"    256 / 512 / 1024: k_gf_apply workgroup width (4 / 8 / 16 KiB per input)
+ *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
+ *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
+ *   "xcd_group"        1 = multi-tile maps keep the tiles of one chunk on one XCD (default 0)
  */
 #ifndef ECX_TUNE_H
 #define ECX_TUNE_H

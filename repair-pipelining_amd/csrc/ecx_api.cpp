@@ -550,12 +550,12 @@ int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
     Tuning &t = tuning();
     if (k == "items_per_block") t.items_per_block = value < 0 ? 0 : value;
-    else if (k == "nontemporal") t.nontemporal = value != 0;
+    else if (k == "nontemporal") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.nontemporal = value;
+    }
     else if (k == "xcd_group") t.xcd_group = value != 0;
-    else if (k == "block_threads") {
-        if (value != 256 && value != 512 && value != 1024) return ECX_E_ILLEGAL_ARGUMENT;
-        t.block_threads = value;
-    } else return ECX_E_ILLEGAL_ARGUMENT;
+    else return ECX_E_ILLEGAL_ARGUMENT;
     return ECX_OK;
 }
 

@@ -81,9 +81,8 @@ struct Tuning {
     // Defaults are the fastest shape measured on MI355X (profiles/r01_kbench.txt):
     // one 4 KiB chunk per workgroup with non-temporal loads/stores.
     int items_per_block = 0;  // 0 = one chunk per workgroup (k_gf_apply); >0 = k_gf_stream
-    int nontemporal = 1;      // non-temporal (streaming) loads/stores
-    int block_threads = 256;  // k_gf_apply workgroup size (256 / 512 / 1024): chunk = 16 B x threads
-    int xcd_group = 1;        // multi-tile maps: tiles of a chunk on one XCD (logical_block)
+    int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
+    int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();

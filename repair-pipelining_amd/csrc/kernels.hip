@@ -123,8 +123,12 @@ __device__ __forceinline__ uint32_t logical_block(bool xcd_group) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
 }
 
-template <bool SAFE, bool NT, int THREADS>
-__global__ void __launch_bounds__(THREADS) k_gf_apply(ApplyArgs a) {
+// NTL / NTS: non-temporal loads / stores.  Outputs are never re-read, so stores
+// are always streamed; loads are streamed only when the map has one tile (no
+// input is read twice), otherwise the re-reads of other tiles hit the caches.
+template <bool SAFE, bool NTL, bool NTS>
+__global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
+    constexpr int THREADS = kBlockThreads;
     const uint32_t w = logical_block(a.xcd_group != 0);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
@@ -146,7 +150,7 @@ __global__ void __launch_bounds__(THREADS) k_gf_apply(ApplyArgs a) {
     }
     auto load = [&](uint32_t slot) -> u32x4 {
         const uint8_t *p = ib + (int64_t)slot * a.in_slot_stride;
-        return SAFE ? load_partial(p, valid) : ld16<NT>(p);
+        return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
     };
 
     u32x4 acc[kTileRows];
@@ -179,7 +183,7 @@ __global__ void __launch_bounds__(THREADS) k_gf_apply(ApplyArgs a) {
         if (o < nrows) {
             uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
             if (SAFE) store_partial(p, acc[o], valid);
-            else st16<NT>(p, acc[o]);
+            else st16<NTS>(p, acc[o]);
         }
     }
 }
@@ -262,8 +266,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
     const Tuning &tu = tuning();
-    const int threads = tu.items_per_block > 0 ? kBlockThreads : tu.block_threads;
-    const int64_t chunk = (int64_t)threads * 16;
+    const int64_t chunk = kChunkBytes;
     const int64_t full = aligned ? nbytes / chunk : 0;  // in units of `chunk`
     const int64_t tail_chunks = (nbytes - full * chunk + kChunkBytes - 1) / kChunkBytes;  // 4 KiB units
 
@@ -308,22 +311,15 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
             a.stripe_begin = s0;
             const dim3 grid((unsigned)(ns * per_stripe));
-            if (safe) {
-                hipLaunchKernelGGL((k_gf_apply<true, false, kBlockThreads>), grid, dim3(kBlockThreads), 0, stream, a);
-            } else if (threads == 1024) {
-                if (tu.nontemporal) hipLaunchKernelGGL((k_gf_apply<false, true, 1024>), grid, dim3(1024), 0, stream, a);
-                else hipLaunchKernelGGL((k_gf_apply<false, false, 1024>), grid, dim3(1024), 0, stream, a);
-            } else if (threads == 512) {
-                if (tu.nontemporal) hipLaunchKernelGGL((k_gf_apply<false, true, 512>), grid, dim3(512), 0, stream, a);
-                else hipLaunchKernelGGL((k_gf_apply<false, false, 512>), grid, dim3(512), 0, stream, a);
-            } else {
-                if (tu.nontemporal) hipLaunchKernelGGL((k_gf_apply<false, true, 256>), grid, dim3(256), 0, stream, a);
-                else hipLaunchKernelGGL((k_gf_apply<false, false, 256>), grid, dim3(256), 0, stream, a);
-            }
+            const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (a.n_tiles == 1 ? 2 : 1) : 0);
+            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false>), grid, dim3(kBlockThreads), 0, stream, a);
+            else if (ntmode == 2) hipLaunchKernelGGL((k_gf_apply<false, true, true>), grid, dim3(kBlockThreads), 0, stream, a);
+            else if (ntmode == 1) hipLaunchKernelGGL((k_gf_apply<false, false, true>), grid, dim3(kBlockThreads), 0, stream, a);
+            else hipLaunchKernelGGL((k_gf_apply<false, false, false>), grid, dim3(kBlockThreads), 0, stream, a);
         }
     };
     run(false, 0, full);
-    run(true, full * (chunk / kChunkBytes), tail_chunks);
+    run(true, full, tail_chunks);
     check_hip(hipGetLastError(), "k_gf_apply launch");
 }
 

@@ -26,6 +26,20 @@ def timed(fn, reps=10):
     return e0.elapsed_time(e1) / reps * 1e-3
 
 
+SWEEP = [(0, 1), (0, 0), (0, 2), (4, 1), (4, 0)]  # (items_per_block, nontemporal); first = default
+
+
+def sweep(lib, name, unit_bytes, units, fn, reps=10, extra=None):
+    """Time fn under each launch shape of SWEEP (results are bit-identical)."""
+    for ipb, nt in SWEEP:
+        lib.ecx_tune(b"items_per_block", ipb)
+        lib.ecx_tune(b"nontemporal", nt)
+        t = timed(fn, reps)
+        report(name, unit_bytes, units, t, dict(extra or {}, items_per_block=ipb, nontemporal=nt))
+    lib.ecx_tune(b"items_per_block", 0)
+    lib.ecx_tune(b"nontemporal", 1)
+
+
 def report(name, unit_bytes, units, sec, extra=None):
     gbs = unit_bytes * units / sec / 1e9
     d = {"config": name, "units": units, "bytes_per_unit": unit_bytes, "ms_per_launch": round(sec * 1e3, 3),
@@ -36,16 +50,19 @@ def report(name, unit_bytes, units, sec, extra=None):
 
 
 def main():
+    import ctypes
     import torch
     ecx = rpamd.load()
+    lib = ecx.lib()
+    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
     # ---- config 2 encode (stripe generation): Clay(4,2), 32 KiB
     B, P = 32768, 1 << 13
     pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 1)
     par = torch.empty((P, 16, B), dtype=torch.uint8, device="cuda")
     enc = ecx.ClayCodeErasureDecodingStep([4, 5], 4, 2)
-    t = timed(lambda: enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B))
-    report("Clay(4,2) encode, 32 KiB (16x32 map)", 32 * B + 16 * B, P, t)
+    sweep(lib, "Clay(4,2) encode, 32 KiB (16x32 map)", 32 * B + 16 * B, P,
+          lambda: enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B))
     del pool, par
     # ---- config 3: LRC 12+4 XOR groups, 64 KiB blocks: encode and repair of block 2
     B, S = 65536, 1 << 14
@@ -56,12 +73,10 @@ def main():
     for g in range(4):
         encm[g, 4 * g:4 * g + 3] = 1
     emap = ecx.GfMap.from_matrix(encm, in_slot=list(range(16)), out_slot=[3, 7, 11, 15])
-    t = timed(lambda: emap.apply_batch(pool, 16 * B, B, pool, 16 * B, B, S, B))
-    report("LRC encode, 64 KiB blocks", 16 * B, S, t)
+    sweep(lib, "LRC encode, 64 KiB blocks", 16 * B, S, lambda: emap.apply_batch(pool, 16 * B, B, pool, 16 * B, B, S, B))
     rmap = ecx.GfMap.from_matrix(np.array([[1, 1, 1]], np.uint8), in_slot=[0, 1, 3], out_slot=[0])
     out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
-    t = timed(lambda: rmap.apply_batch(pool, 16 * B, B, out, B, B, S, B))
-    report("LRC repair of block 2, 64 KiB", 4 * B, S, t)
+    sweep(lib, "LRC repair of block 2, 64 KiB", 4 * B, S, lambda: rmap.apply_batch(pool, 16 * B, B, out, B, B, S, B))
     del pool, out
     # ---- config 4: shortened Clay(10,4), 1 MiB node block = 256 x 4 KiB, single repair
     k, m, v, B, S = 10, 4, 2, 4096, 2048
@@ -71,17 +86,8 @@ def main():
     out = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
     step = ecx.ClayCodeErasureDecodingStep([3], k, m, virtualUnits=v)
     inf = step.map().info()
-    import ctypes
-    lib = ecx.lib()
-    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
-    for xcd, nt in ((1, 1), (0, 1), (1, 0), (0, 0)):
-        lib.ecx_tune(b"xcd_group", xcd)
-        lib.ecx_tune(b"nontemporal", nt)
-        t = timed(lambda: step.performCodingBatch(pool, n * a * B, B, out, a * B, B, S, B), reps=5)
-        report("Clay(10,4) shortened, 1 MiB blocks, single repair (e=3)", (inf["n_in"] + inf["n_out"]) * B, S, t,
-               {"map": inf, "xcd_group": xcd, "nontemporal": nt})
-    lib.ecx_tune(b"xcd_group", 1)
-    lib.ecx_tune(b"nontemporal", 1)
+    sweep(lib, "Clay(10,4) shortened, 1 MiB blocks, single repair (e=3)", (inf["n_in"] + inf["n_out"]) * B, S,
+          lambda: step.performCodingBatch(pool, n * a * B, B, out, a * B, B, S, B), reps=5, extra={"map": inf})
     del pool, out
     # ---- config 5: RS(12,4), 4 MiB shards, erasures {0,1}, in place
     L, S = 4 << 20, 256
@@ -89,8 +95,8 @@ def main():
     pool = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 4)
     dmap = rs.decode_map([False, False] + [True] * 14)
-    t = timed(lambda: dmap.apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L), reps=5)
-    report("RS(12,4) 2-erasure decode, 4 MiB", 14 * L, S, t)
+    sweep(lib, "RS(12,4) 2-erasure decode, 4 MiB", 14 * L, S,
+          lambda: dmap.apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L), reps=5)
 
 
 if __name__ == "__main__":

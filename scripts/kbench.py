@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--pool", type=int, default=1 << 14)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0:0:256,0:1:256,0:1:512,0:1:1024,0:0:512,2:1:256,4:1:256,1:1:256")
+    ap.add_argument("--variants", default="0:0,0:1,0:2,4:1,8:1")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
@@ -62,21 +62,20 @@ def main():
 
     variants = []
     for v in args.variants.split(","):
-        ipb, nt, th = map(int, v.split(":"))
-        variants.append((f"clay ipb={ipb} nt={nt} threads={th}", clay, ipb, nt, th, P * ALGO))
-    variants.append(("xor-only ipb=0 nt=1 threads=256", xor_only, 0, 1, 256, P * ALGO))
-    variants.append(("probe read nt=0", probe(0, 0), 0, 0, 256, PROBE))
-    variants.append(("probe read nt=1", probe(0, 1), 0, 0, 256, PROBE))
-    variants.append(("probe copy nt=0", probe(1, 0), 0, 0, 256, 2 * PROBE))
-    variants.append(("probe copy nt=1", probe(1, 1), 0, 0, 256, 2 * PROBE))
-    variants.append(("d2d copy (torch)", copy, 0, 0, 256, 2 * P * ALPHA * B))
+        ipb, nt = map(int, v.split(":"))
+        variants.append((f"clay ipb={ipb} nt={nt}", clay, ipb, nt, P * ALGO))
+    variants.append(("xor-only ipb=0 nt=1", xor_only, 0, 1, P * ALGO))
+    variants.append(("probe read nt=0", probe(0, 0), 0, 0, PROBE))
+    variants.append(("probe read nt=1", probe(0, 1), 0, 0, PROBE))
+    variants.append(("probe copy nt=0", probe(1, 0), 0, 0, 2 * PROBE))
+    variants.append(("probe copy nt=1", probe(1, 1), 0, 0, 2 * PROBE))
+    variants.append(("d2d copy (torch)", copy, 0, 0, 2 * P * ALPHA * B))
 
     res = {name: [] for name, *_ in variants}
     for r in range(args.rounds):
-        for name, fn, ipb, nt, th, nbytes in variants:
+        for name, fn, ipb, nt, nbytes in variants:
             lib.ecx_tune(b"items_per_block", ipb)
             lib.ecx_tune(b"nontemporal", nt)
-            lib.ecx_tune(b"block_threads", th)
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -87,6 +86,8 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.launches
             res[name].append(nbytes / (ms * 1e-3) / 1e9)
+    lib.ecx_tune(b"items_per_block", 0)
+    lib.ecx_tune(b"nontemporal", 1)
     for name, *_ in variants:
         v = res[name]
         print(json.dumps({"variant": name, "GBps_median": round(statistics.median(v), 1),
