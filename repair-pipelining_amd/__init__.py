@@ -28,6 +28,7 @@ __all__ = [
     "ClayCodeErasureDecodingStep", "ClayCode", "LRCErasureCode", "LRCErasureUtil", "JavaRandom",
     "lrc_encode", "lrc_encode_using_single", "lrc_decode", "sample_encode", "sample_decode",
     "device_count", "set_device", "fill_random", "count_mismatch", "shard_stripes",
+    "ECChunk", "ECBlock", "ClayCodeHelper", "write_subchunk", "read_subchunk",
 ]
 
 
@@ -40,6 +41,59 @@ def shard_stripes(n_stripes: int, world: int, rank: int):
     base, extra = divmod(n_stripes, world)
     begin = rank * base + min(rank, extra)
     return begin, begin + base + (1 if rank < extra else 0)
+
+
+# ---------------------------------------------------------------- ECChunk.java / ECBlock.java
+class ECChunk:
+    """Hadoop-style chunk wrapper (ECChunk.java:37-109); the buffer may be None."""
+
+    def __init__(self, buffer=None, offset: int = 0, length: Optional[int] = None):
+        if buffer is not None and (offset or length is not None):
+            buffer = buffer[offset:offset + (len(buffer) - offset if length is None else length)]
+        self.buffer = buffer
+        self.allZero = False
+
+    def getBuffer(self):
+        return self.buffer
+
+    def isAllZero(self):
+        return self.allZero
+
+    def setAllZero(self, v: bool):
+        self.allZero = v
+
+    def toBytesArray(self) -> np.ndarray:
+        return np.array(self.buffer, np.uint8)
+
+    @staticmethod
+    def toBuffers(chunks):
+        """ECChunk.toBuffers (ECChunk.java:81-95): null chunks map to null buffers."""
+        return [None if c is None else c.getBuffer() for c in chunks]
+
+
+class ECBlock:
+    """ECBlock.java:36-99 -- flags are carried but, as in the reference, unused by the math."""
+
+    def __init__(self, chunk: Optional[ECChunk] = None, isParity: bool = False, isErased: bool = False):
+        self.chunk, self.isParity, self.isErased = chunk, isParity, isErased
+
+    def getChunk(self):
+        return self.chunk
+
+    def setChunk(self, c):
+        self.chunk = c
+
+
+def _buffers(items):
+    """Accept ndarray / None / ECChunk / ECBlock entries (the reference passes ECChunk[])."""
+    out = []
+    for it in items:
+        if isinstance(it, ECBlock):
+            it = it.chunk
+        if isinstance(it, ECChunk):
+            it = it.buffer
+        out.append(it)
+    return out
 
 
 # ---------------------------------------------------------------- helpers
@@ -393,7 +447,9 @@ class ClayCodeErasureDecodingStep:
         return [int(x) for x in out[:n]]
 
     def performCoding(self, inputs, outputs, bufSize: Optional[int] = None) -> None:
-        """inputs: n*alpha (plane-major, None = absent); outputs: |E|*alpha arrays."""
+        """inputs: n*alpha (plane-major, None = absent); outputs: |E|*alpha arrays.
+        Entries may be numpy arrays, None, ECChunk or ECBlock (ECChunk.toBuffers)."""
+        inputs, outputs = _buffers(inputs), _buffers(outputs)
         if len(inputs) != self.numTotalUnits * self.subPacketSize:
             raise EcxError(-1, "Invalid inputs length")
         if len(outputs) != len(self.erasedIndexes) * self.subPacketSize:
@@ -451,7 +507,8 @@ class JavaRandom:
 
 
 class ClayCode:
-    """ClayCode.java facade: RS(2,2) pair transform + RS(k,m) per plane."""
+    """ClayCode.java facade: RS(2,2) pair transform + RS(k,m) per plane.
+    Buffers are numpy arrays inside ECChunk/ECBlock wrappers, as in the reference."""
 
     def __init__(self, numDataUnits, numParityUnits, blockSize, erasedIndexes):
         self.numDataUnits, self.numParityUnits, self.blockSize = numDataUnits, numParityUnits, blockSize
@@ -460,10 +517,12 @@ class ClayCode:
         self.clayCodeUtil = ClayCodeUtil(erasedIndexes, numDataUnits, numParityUnits)
 
     def performCoding(self, inputs, outputs):
+        """ClayCode.performCoding (:43-45) -> ClayCodeErasureDecodingStep.performCoding."""
         self.erasureDecodingStep.performCoding(inputs, outputs, self.blockSize)
 
     def getInputs(self):
-        """ClayCode.getInputs (ClayCode.java:47-77): Random(123456).nextBytes per data sub-chunk."""
+        """ClayCode.getInputs (ClayCode.java:47-77): one Random(123456), nextBytes per data
+        sub-chunk in flat order k; sub-chunk k is data iff k % n < numDataUnits."""
         n = self.numDataUnits + self.numParityUnits
         a = self.clayCodeUtil.getSubPacketSize()
         r = JavaRandom(123456)
@@ -473,19 +532,109 @@ class ClayCode:
             for j in range(a):
                 k = i * a + j
                 if counter < self.numDataUnits:
-                    out[k] = r.nextBytes(self.blockSize)
+                    out[k] = ECBlock(ECChunk(r.nextBytes(self.blockSize)), False, False)
+                else:
+                    out[k] = ECBlock(ECChunk(None), True, True)
                 counter = (counter + 1) % n
         return out
 
     def getOutputs(self):
-        return [np.zeros(self.blockSize, np.uint8) for _ in range(len(self.erasedIndexes) *
-                                                                 self.clayCodeUtil.getSubPacketSize())]
+        """ClayCode.getOutputs (:79-87)."""
+        return [ECBlock(ECChunk(np.zeros(self.blockSize, np.uint8)), True, True)
+                for _ in range(len(self.erasedIndexes) * self.clayCodeUtil.getSubPacketSize())]
 
     def encode(self, inputs, outputs):
-        """ClayCode.encode (:89-99) -- meaningful with erasedIndexes = parity nodes."""
+        """ClayCode.encode (:89-99): performCoding with erasedIndexes = the parity nodes;
+        returns [inputChunks, outputChunks]."""
         step = ClayCodeErasureDecodingStep(self.erasedIndexes, self.numDataUnits, self.numParityUnits)
-        step.performCoding(inputs, outputs, self.blockSize)
-        return inputs, outputs
+        ic, oc = self.getChunks(inputs), self.getChunks(outputs)
+        step.performCoding(ic, oc, self.blockSize)
+        return [ic, oc]
+
+    def getChunks(self, blocks):
+        """ClayCode.getChunks (:168-177)."""
+        return [None if b is None else b.getChunk() for b in blocks]
+
+    def getTestOutputs(self, erasedIndexesSize: int):
+        """ClayCode.getTestOutputs (:157-166)."""
+        return [ECBlock(ECChunk(np.zeros(self.blockSize, np.uint8)), False, True)
+                for _ in range(erasedIndexesSize * self.clayCodeUtil.getSubPacketSize())]
+
+    def getTestInputs(self, inputChunks, outputChunks, testErasedIndexes, blockId: str = "LP", write_dir=None):
+        """ClayCode.getTestInputs (:101-155), restated faithfully -- including the
+        reference's index quirk (SURVEY.md A.2 bug B1): the outer loop variable is
+        treated as the node although the flat index a*alpha+b is plane-major, so
+        the zeroed sub-chunks are not the erased node's for every e.  With
+        write_dir, also writes the per-sub-chunk files "<blockId> <node> <plane>"
+        (and "ORIGINAL ..." for erased nodes) as the reference does in its CWD."""
+        n = self.numDataUnits + self.numParityUnits
+        a = self.clayCodeUtil.getSubPacketSize()
+        erased = list(testErasedIndexes)
+        ib, ob = ECChunk.toBuffers(inputChunks), ECChunk.toBuffers(outputChunks)
+        test, k = [None] * (n * a), 0
+        for aa in range(n):
+            for b in range(a):
+                i = aa * a + b
+                if aa not in erased:
+                    if ib[i] is not None:
+                        buf = np.array(ib[i], np.uint8)
+                    else:
+                        buf = np.array(ob[k], np.uint8)
+                        k += 1
+                    test[i] = ECBlock(ECChunk(buf), False, True)
+                else:
+                    if ib[i] is None:
+                        k += 1
+                    test[i] = ECBlock(ECChunk(np.zeros(self.blockSize, np.uint8)), False, True)
+        if write_dir is not None:
+            k = 0
+            for i in range(a):
+                for j in range(n):
+                    idx = i * n + j
+                    data = ib[idx] if ib[idx] is not None else ob[k]
+                    if ib[idx] is None:
+                        k += 1
+                    write_subchunk(write_dir, blockId, j, i, data, original=j in erased)
+        return test
+
+
+class ClayCodeHelper:
+    """ClayCodeHelper.kt:11-76 -- coordinator-side single repair, one helper plane at a time
+    (doDecodeSingle overload 2)."""
+
+    def __init__(self, NUM_DATA_UNITS, NUM_PARITY_UNITS, SUBPACKET_SIZE, inputs):
+        self.k, self.m, self.alpha = NUM_DATA_UNITS, NUM_PARITY_UNITS, SUBPACKET_SIZE
+        self.n = NUM_DATA_UNITS + NUM_PARITY_UNITS
+        self.inputs = _buffers(inputs)
+
+    def getHelperPlanesAndDecode(self, util, blockId, outputs, erasedIndex, bufSize, isDirect=False):
+        """outputs: [alpha][|E|] arrays (|E| = 1)."""
+        step = ClayCodeErasureDecodingStep([erasedIndex], self.k, self.m)
+        hidx = util.getHelperPlanesIndexes(erasedIndex)
+        rows = [[self.inputs[z * self.n + j] for j in range(self.n)] for z in hidx]
+        flat_out = [outputs[z][0] for z in range(self.alpha)]
+        for i in range(len(hidx)):
+            step.doDecodeSingleHelper(rows, i, flat_out, erasedIndex, bufSize)
+
+
+# ---------------------------------------------------------------- per-sub-chunk files
+def _subchunk_path(directory, blockId, node, plane, original=False):
+    import os
+    return os.path.join(str(directory), f"{'ORIGINAL ' if original else ''}{blockId} {node} {plane}")
+
+
+def write_subchunk(directory, blockId: str, node: int, plane: int, data, original: bool = False) -> str:
+    """The reference's on-disk unit: one file "<blockId> <node> <plane>" holding exactly
+    B bytes (ClayCode.java:140-152, ClayCodeNode.kt:105,147,245,257)."""
+    path = _subchunk_path(directory, blockId, node, plane, original)
+    np.asarray(data, np.uint8).tofile(path)
+    return path
+
+
+def read_subchunk(directory, blockId: str, node: int, plane: int, blockSize: Optional[int] = None,
+                  original: bool = False) -> np.ndarray:
+    data = np.fromfile(_subchunk_path(directory, blockId, node, plane, original), dtype=np.uint8)
+    return data if blockSize is None else data[:blockSize].copy()
 
 
 # ---------------------------------------------------------------- LRC (lrc/)

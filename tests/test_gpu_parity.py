@@ -227,14 +227,55 @@ def test_clay_multi_nonnull_erased_inputs(ecx):
 
 
 def test_clay_getinputs_encode_digests(ecx, kats):
+    """ClayCodeRunner.main's encode half (ClayCodeRunner.java:20-28) through the facade."""
     d = kats["survey_digests"]
     cc = ecx.ClayCode(4, 2, 32768, [4, 5])
     inp = cc.getInputs()
-    assert bytes(inp[0][:8]).hex() == d["clay42_first_bytes"]
-    outs = cc.getOutputs()
-    cc.encode(inp, outs)
+    assert bytes(inp[0].getChunk().getBuffer()[:8]).hex() == d["clay42_first_bytes"]
+    ic, oc = cc.encode(inp, cc.getOutputs())
+    outs = ecx.ECChunk.toBuffers(oc)
     assert [h16(outs[z * 2]) for z in range(8)] == d["clay42_parity_node4"]
     assert [h16(outs[z * 2 + 1]) for z in range(8)] == d["clay42_parity_node5"]
+
+
+def test_clay_runner_flow_and_b1_quirk(ecx, tmp_path):
+    """ClayCodeRunner.main (ClayCodeRunner.java:6-39) end to end: encode, getTestInputs,
+    performCoding.  The reference's getTestInputs index quirk leaves
+    the erased node's data in place for e in {1,2,3} (repair correct) and zeroes the
+    wrong sub-chunks for e in {0,4,5} -- reproduced exactly, and checked vs the oracle."""
+    k, m, B = 4, 2, 2174
+    enc = ecx.ClayCode(k, m, B, [4, 5])
+    ic, oc = enc.encode(enc.getInputs(), enc.getOutputs())
+    ib, ob = ecx.ECChunk.toBuffers(ic), ecx.ECChunk.toBuffers(oc)
+    full = [ib[i] if ib[i] is not None else ob[(i // 6) * 2 + (i % 6) - 4] for i in range(48)]
+    for e in range(6):
+        cc = ecx.ClayCode(k, m, B, [e])
+        test = cc.getTestInputs(ic, oc, [e], write_dir=tmp_path if e == 1 else None)
+        outs = cc.getTestOutputs(1)
+        cc.performCoding(cc.getChunks(test), cc.getChunks(outs))
+        got = [o.getChunk().getBuffer() for o in outs]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(k, m, [e]).perform_coding([t.getChunk().getBuffer() for t in test], ref, B)
+        assert all((g == r).all() for g, r in zip(got, ref))
+        correct = all((got[z] == full[z * 6 + e]).all() for z in range(8))
+        assert correct == (e in (1, 2, 3)), e
+    assert (ecx.read_subchunk(tmp_path, "LP", 2, 5, B) == full[5 * 6 + 2]).all()
+    assert (ecx.read_subchunk(tmp_path, "LP", 1, 3, B, original=True) == full[3 * 6 + 1]).all()
+
+
+def test_clay_code_helper(ecx):
+    """ClayCodeHelper.getHelperPlanesAndDecode (ClayCodeHelper.kt:19-56), main()'s shape
+    (B = 2174, e = 1, ClayCodeHelper.kt:78-104)."""
+    k, m, B, e = 4, 2, 2174, 1
+    enc = ecx.ClayCode(k, m, B, [4, 5])
+    ic, oc = enc.encode(enc.getInputs(), enc.getOutputs())
+    ib, ob = ecx.ECChunk.toBuffers(ic), ecx.ECChunk.toBuffers(oc)
+    full = [ib[i] if ib[i] is not None else ob[(i // 6) * 2 + (i % 6) - 4] for i in range(48)]
+    blocks = [ecx.ECBlock(ecx.ECChunk(None if (i % 6) == e else full[i].copy())) for i in range(48)]
+    outs = [[np.zeros(B, np.uint8)] for _ in range(8)]
+    helper = ecx.ClayCodeHelper(k, m, 8, blocks)
+    helper.getHelperPlanesAndDecode(ecx.ClayCodeUtil([e], k, m), "LP", outs, e, B)
+    assert all((outs[z][0] == full[z * 6 + e]).all() for z in range(8))
 
 
 def test_clay_helper_overload(ecx):
