@@ -121,9 +121,33 @@ int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe
                         uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                         int64_t byte_count, void *stream);
 
+/* As ecx_map_apply_batch, but XOR-accumulates: out ^= M * in. */
+int ecx_map_accumulate_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
+                             int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride,
+                             int64_t nstripes, int64_t byte_count, void *stream);
+
 /* Maps of the codec entry points (owned by the codec; do not destroy). */
 int ecx_rs_encode_map(ecx_rs *rs, const ecx_map **out);              /* encodeParity, slots = shard index */
 int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **out); /* decodeMissing */
+
+/* ---------------------------------------------------------------- batched partial sums (repair pipelining) */
+/* Batched ReedSolomon.decodeMissingSingle (ReedSolomon.java:288-333) as used along the
+ * pipelined chain (ClayCodeNode.kt:182-186, :225-228): one helper's contribution to EVERY
+ * missing shard, over nstripes stripes: acc[s][o] (=, or ^= unless is_first)
+ * D[o][shard_index] * in[s], with o over the missing shards in ascending index order.
+ * Unlike the reference (bug B3) the rows include missing PARITY shards (the composed
+ * decodeMissing map), so a parity-node repair can be pipelined too.  A present shard that
+ * is not among the first k present contributes zero (the reference's first-k rule). */
+int ecx_rs_decode_partial_batch(ecx_rs *rs, const uint8_t *shard_present, int shard_index, const uint8_t *in,
+                                int64_t in_stripe_stride, uint8_t *acc, int64_t acc_stripe_stride,
+                                int64_t acc_row_stride, int64_t nstripes, int64_t byte_count, int is_first,
+                                void *stream);
+/* Batched ReedSolomon.encodeParitySingle (ReedSolomon.java:110-118; LRC chains,
+ * NodeHelper.kt:89): acc[s][p] (=, or ^= unless is_first) parityRows[p][input_index] * in[s]
+ * for every parity row p. */
+int ecx_rs_encode_partial_batch(ecx_rs *rs, int input_index, const uint8_t *in, int64_t in_stripe_stride,
+                                uint8_t *acc, int64_t acc_stripe_stride, int64_t acc_row_stride, int64_t nstripes,
+                                int64_t byte_count, int is_first, void *stream);
 
 /* ---------------------------------------------------------------- ClayCodeErasureDecodingStep.java */
 typedef struct ecx_clay ecx_clay;

@@ -273,6 +273,13 @@ class GfMap:
         check(lib().ecx_map_info(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return {"n_out": a.value, "n_in": b.value, "nnz": c.value}
 
+    def accumulate_batch(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride,
+                         nstripes, byte_count, stream=None):
+        """out ^= M * in (partial sums)."""
+        check(lib().ecx_map_accumulate_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_slot_stride,
+                                             _dev_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
+                                             byte_count, _stream(stream)))
+
     def matrix(self):
         """(dense matrix n_out x n_in, in_slot, out_slot) of the composed map."""
         inf = self.info()
@@ -359,6 +366,21 @@ class ReedSolomon:
                                                  byteCount, 1 if isFirst else 0))
 
     # batched, device-resident
+    def decodePartialBatch(self, shardPresent, shardIndex, inp, in_stripe_stride, acc, acc_stripe_stride,
+                           acc_row_stride, nstripes, byteCount, isFirst, stream=None):
+        """Batched decodeMissingSingle for every missing shard (data and parity)."""
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        check(lib().ecx_rs_decode_partial_batch(self._h, pres.ctypes.data, shardIndex, _dev_ptr(inp),
+                                                in_stripe_stride, _dev_ptr(acc), acc_stripe_stride, acc_row_stride,
+                                                nstripes, byteCount, 1 if isFirst else 0, _stream(stream)))
+
+    def encodePartialBatch(self, inputIndex, inp, in_stripe_stride, acc, acc_stripe_stride, acc_row_stride,
+                           nstripes, byteCount, isFirst, stream=None):
+        """Batched encodeParitySingle into every parity row."""
+        check(lib().ecx_rs_encode_partial_batch(self._h, inputIndex, _dev_ptr(inp), in_stripe_stride,
+                                                _dev_ptr(acc), acc_stripe_stride, acc_row_stride, nstripes,
+                                                byteCount, 1 if isFirst else 0, _stream(stream)))
+
     def encode_map(self) -> GfMap:
         h = ctypes.c_void_p()
         check(lib().ecx_rs_encode_map(self._h, ctypes.byref(h)))

@@ -81,8 +81,11 @@ SIGNATURES = {
     "ecx_map_info": (I, [P, PI, PI, PI]),
     "ecx_map_matrix": (I, [P, P, P, P]),
     "ecx_map_apply_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
+    "ecx_map_accumulate_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_rs_decode_map": (I, [P, P, ctypes.POINTER(P)]),
+    "ecx_rs_decode_partial_batch": (I, [P, P, I, P, I64, P, I64, I64, I64, I64, I, P]),
+    "ecx_rs_encode_partial_batch": (I, [P, I, P, I64, P, I64, I64, I64, I64, I, P]),
     "ecx_clay_create": (I, [I, I, P, I, ctypes.POINTER(P)]),
     "ecx_clay_create_shortened": (I, [I, I, I, P, I, ctypes.POINTER(P)]),
     "ecx_clay_destroy": (None, [P]),

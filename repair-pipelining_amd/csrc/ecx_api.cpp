@@ -20,7 +20,7 @@ struct ecx_rs {
     RsCode code;
     std::mutex mu;
     std::unique_ptr<ecx_map> enc, check;
-    std::map<std::string, std::unique_ptr<ecx_map>> dec;
+    std::map<std::string, std::unique_ptr<ecx_map>> dec, partial;  // plans live as long as the codec
 };
 
 struct ecx_clay {
@@ -444,6 +444,94 @@ int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe
         if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
         launch_apply(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
                      out_slot_stride, nstripes, byte_count, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+int ecx_map_accumulate_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                             uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                             int64_t byte_count, void *stream) {
+    return guarded([&]() -> int {
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
+        launch_apply(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
+                     out_slot_stride, nstripes, byte_count, (hipStream_t)stream, true);
+        return ECX_OK;
+    });
+}
+
+// ---------------------------------------------------------------- batched partial sums
+namespace {
+// One-input map: row o = coefficient of `column` in row o of `m` (0 if absent).
+ecx_map *single_input_map(const LinearMap &m, int column_slot, std::vector<int> out_slots) {
+    LinearMap lm;
+    lm.n_in = 1;
+    lm.in_slot.push_back(0);
+    lm.n_out = m.n_out;
+    lm.out_slot = std::move(out_slots);
+    int col = -1;
+    for (int j = 0; j < m.n_in; ++j)
+        if (m.in_slot[j] == column_slot) col = j;
+    for (int o = 0; o < m.n_out; ++o) lm.a.push_back(col < 0 ? 0 : m.at(o, col));
+    return new ecx_map(lm);
+}
+}  // namespace
+
+int ecx_rs_decode_partial_batch(ecx_rs *rs, const uint8_t *shard_present, int shard_index, const uint8_t *in,
+                                int64_t in_stripe_stride, uint8_t *acc, int64_t acc_stripe_stride,
+                                int64_t acc_row_stride, int64_t nstripes, int64_t byte_count, int is_first,
+                                void *stream) {
+    return guarded([&]() -> int {
+        const RsCode &c = rs->code;
+        if (shard_index < 0 || shard_index >= c.n()) throw Error(ECX_E_INDEX, "shard index");
+        std::vector<bool> present = present_vec(shard_present, c.n());
+        int np = 0;
+        for (bool b : present) np += b;
+        if (np < c.k()) throw Error(ECX_E_NOT_ENOUGH_SHARDS, "Not enough shards present");
+        if (np == c.n()) return ECX_OK;
+        ecx_map *full = rs_decode_map(rs, present);  // rows: the missing shards, data AND parity
+        ecx_map *part;
+        {
+            std::lock_guard<std::mutex> lk(rs->mu);
+            auto &slot = rs->partial[key_of(present, shard_index)];
+            if (!slot) {
+                std::vector<int> rows;
+                for (int o = 0; o < full->cm.map().n_out; ++o) rows.push_back(o);
+                slot.reset(single_input_map(full->cm.map(), shard_index, rows));
+            }
+            part = slot.get();
+        }
+        launch_apply(part->cm, in, in_stripe_stride, 0, acc, acc_stripe_stride, acc_row_stride, nstripes, byte_count,
+                     (hipStream_t)stream, !is_first);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_encode_partial_batch(ecx_rs *rs, int input_index, const uint8_t *in, int64_t in_stripe_stride,
+                                uint8_t *acc, int64_t acc_stripe_stride, int64_t acc_row_stride, int64_t nstripes,
+                                int64_t byte_count, int is_first, void *stream) {
+    return guarded([&]() -> int {
+        const RsCode &c = rs->code;
+        if (input_index < 0 || input_index >= c.k()) throw Error(ECX_E_INDEX, "data shard index");
+        ecx_map *part;
+        {
+            std::lock_guard<std::mutex> lk(rs->mu);
+            auto &slot = rs->partial[key_of({}, -1 - input_index)];
+            if (!slot) {
+                LinearMap lm;
+                lm.n_in = 1;
+                lm.in_slot.push_back(0);
+                lm.n_out = c.m();
+                for (int p = 0; p < c.m(); ++p) {
+                    lm.a.push_back(c.parity_row(p)[input_index]);
+                    lm.out_slot.push_back(p);
+                }
+                slot = std::make_unique<ecx_map>(lm);
+            }
+            part = slot.get();
+        }
+        launch_apply(part->cm, in, in_stripe_stride, 0, acc, acc_stripe_stride, acc_row_stride, nstripes, byte_count,
+                     (hipStream_t)stream, !is_first);
         return ECX_OK;
     });
 }

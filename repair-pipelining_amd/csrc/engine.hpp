@@ -74,6 +74,7 @@ struct ApplyArgs {
     int n_tiles;
     int items_per_block;  // k_gf_stream: consecutive chunks per workgroup
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
+    int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -90,7 +91,7 @@ Tuning &tuning();
 // Enqueue out = M * in over nstripes stripes (kernels.hip).
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
-                  hipStream_t stream);
+                  hipStream_t stream, bool accumulate = false);
 void launch_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, hipStream_t stream);
 void launch_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
                            int64_t row_bytes, uint64_t *d_count, hipStream_t stream);

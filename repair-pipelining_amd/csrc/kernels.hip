@@ -182,8 +182,10 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     for (int o = 0; o < kTileRows; ++o) {
         if (o < nrows) {
             uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
-            if (SAFE) store_partial(p, acc[o], valid);
-            else st16<NTS>(p, acc[o]);
+            u32x4 v = acc[o];
+            if (a.accumulate) v ^= SAFE ? load_partial(p, valid) : load16(p);  // wave-uniform branch
+            if (SAFE) store_partial(p, v, valid);
+            else st16<NTS>(p, v);
         }
     }
 }
@@ -260,7 +262,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_stream(ApplyArgs a) {
 
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
-                  hipStream_t stream) {
+                  hipStream_t stream, bool accumulate) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
     const DevicePlan &plan = cm.plan_for_current_device();
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
@@ -282,6 +284,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
     a.xcd_group = (tuning().xcd_group && a.n_tiles > 1) ? 1 : 0;
+    a.accumulate = accumulate ? 1 : 0;
     a.items_per_block = 0;
     a.total_items = 0;
 
@@ -289,7 +292,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
         a.n_chunks = n_chunks;
-        if (!safe && tu.items_per_block > 0) {
+        if (!safe && tu.items_per_block > 0 && !accumulate) {
             const int64_t ipb = tu.items_per_block;
             const int64_t max_items = ((int64_t)1 << 30) / a.n_tiles * ipb;
             const int64_t stripes_per_launch = std::max<int64_t>(1, max_items / n_chunks);

@@ -467,3 +467,33 @@ def test_clay104_shortened_batch_roundtrip(ecx, torch_dev):
     for z in range(0, a, 17):
         for j in range(m):
             assert (host[z * n + k + j] == ref[z * m + j]).all()
+
+
+def test_partial_sum_batches(ecx, torch_dev):
+    """Batched partial sums along a repair chain: summing the chain's
+    decodeMissingSingle contributions reproduces decodeMissing for data AND parity shards
+    (the reference can only do data, bug B3); per-stripe the oracle's decodeMissingSingle
+    chain matches the data rows; encode partials reproduce encodeParity."""
+    torch = torch_dev
+    k, m, L, S = 4, 2, 8192 + 32, 6
+    rs = ecx.ReedSolomon.create(k, m)
+    pool = torch.empty((S, 6, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 17)
+    rs.encode_map().apply_batch(pool, 6 * L, L, pool, 6 * L, L, S, L)
+    present = [True, False, True, True, True, False]  # missing data 1 and parity 5
+    chain = [0, 2, 3, 4]
+    acc = torch.empty((S, 2, L), dtype=torch.uint8, device="cuda")
+    for c, idx in enumerate(chain):
+        rs.decodePartialBatch(present, idx, pool[:, idx], 6 * L, acc, 2 * L, L, S, L, c == 0)
+    torch.cuda.synchronize()
+    assert torch.equal(acc[:, 0], pool[:, 1]) and torch.equal(acc[:, 1], pool[:, 5])
+    host = pool[0].cpu().numpy()
+    ref = [np.zeros(L, np.uint8)]
+    for c, idx in enumerate(chain):
+        O.ReedSolomon(k, m).decode_missing_single(host[idx].copy(), idx, c, present, ref, 0, L, c == 0)
+    assert (acc[0, 0].cpu().numpy() == ref[0]).all()
+    par = torch.empty((S, 2, L), dtype=torch.uint8, device="cuda")
+    for i in range(k):
+        rs.encodePartialBatch(i, pool[:, i], 6 * L, par, 2 * L, L, S, L, i == 0)
+    torch.cuda.synchronize()
+    assert torch.equal(par, pool[:, 4:6])
