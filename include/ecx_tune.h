@@ -3,8 +3,7 @@
  * Not part of the reference's coding interface (include/ecx.h is the boundary);
  * results are bit-identical for every setting, only speed changes.
  *
- *   "items_per_block"  consecutive 4 KiB chunks one workgroup streams through the
- *                      k_gf_stream kernel (default 0 = one chunk per workgroup, k_gf_apply)
+ *   "depth"            4 or 8: 16-B loads per lane in the kernel's load ring (default 4)
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        1 = multi-tile maps keep the tiles of one chunk on one XCD (default 0)

@@ -637,7 +637,10 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
 int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
     Tuning &t = tuning();
-    if (k == "items_per_block") t.items_per_block = value < 0 ? 0 : value;
+    if (k == "depth") {
+        if (value != 4 && value != 8) return ECX_E_ILLEGAL_ARGUMENT;
+        t.depth = value;
+    }
     else if (k == "nontemporal") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.nontemporal = value;

@@ -110,50 +110,73 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
             entries_.insert(entries_.end(), rec, rec + kEntryDwords);
             ++count;
         }
-        // Pad to a multiple of kDepth and add kDepth trailing dummies so the
-        // kernel's load ring never branches; dummies re-read the tile's first
-        // input slot (an L2 hit) and carry no coefficients.
-        const uint32_t first_slot = count ? entries_[(size_t)begin * kEntryDwords] : 0u;
-        const uint32_t padded = (count + kDepth - 1) / kDepth * kDepth;
-        for (uint32_t d = count; d < padded + kDepth; ++d) {
-            uint32_t rec[kEntryDwords] = {0};
-            rec[0] = first_slot;
-            entries_.insert(entries_.end(), rec, rec + kEntryDwords);
-        }
         uint32_t tile[kTileDwords] = {0};
         tile[0] = begin;
-        tile[1] = padded;
+        tile[1] = count;
         tile[2] = (uint32_t)rows;
         for (int r = 0; r < rows; ++r) tile[4 + r] = (uint32_t)map_.out_slot[order[r0 + r]];
         tiles_.insert(tiles_.end(), tile, tile + kTileDwords);
         ++n_tiles_;
     }
     if (tiles_.empty()) tiles_.assign(kTileDwords, 0);
+    if (entries_.empty()) entries_.assign(kEntryDwords, 0);
+}
+
+const uint8_t *zero_page_for_current_device() {
+    static std::mutex mu;
+    static std::map<int, uint8_t *> pages;
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(mu);
+    uint8_t *&p = pages[dev];
+    if (!p) {
+        check_hip(hipMalloc(&p, 4096), "hipMalloc(zero page)");
+        check_hip(hipMemset(p, 0, 4096), "hipMemset(zero page)");
+    }
+    return p;
 }
 
 CompiledMap::~CompiledMap() {
     for (auto &kv : dev_) {
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) continue;
-        (void)hipSetDevice(kv.first);
+        (void)hipSetDevice(kv.first.first);
         (void)hipFree(kv.second.entries);
         (void)hipFree(kv.second.tiles);
         (void)hipSetDevice(cur);
     }
 }
 
-const DevicePlan &CompiledMap::plan_for_current_device() {
+const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     int dev = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
     std::lock_guard<std::mutex> lk(mu_);
-    auto it = dev_.find(dev);
+    auto it = dev_.find({dev, depth});
     if (it != dev_.end()) return it->second;
+    // Pad each tile to a multiple of `depth` entries so the kernel's load ring
+    // runs branch-free (engine.hpp); padding entries load the zero page.
+    std::vector<uint32_t> ents, tiles = tiles_;
+    for (int t = 0; t < n_tiles_; ++t) {
+        uint32_t *tile = tiles.data() + (size_t)t * kTileDwords;
+        const uint32_t begin = tile[0], count = tile[1];
+        tile[0] = (uint32_t)(ents.size() / kEntryDwords);
+        ents.insert(ents.end(), entries_.begin() + (size_t)begin * kEntryDwords,
+                    entries_.begin() + (size_t)(begin + count) * kEntryDwords);
+        const uint32_t padded = count == 0 ? 0 : (count + depth - 1) / depth * depth;
+        for (uint32_t d = count; d < padded; ++d) {
+            uint32_t rec[kEntryDwords] = {0};
+            rec[0] = kDummySlot;
+            ents.insert(ents.end(), rec, rec + kEntryDwords);
+        }
+        tile[1] = padded;
+    }
+    if (ents.empty()) ents.assign(kEntryDwords, 0);
     DevicePlan p;
-    check_hip(hipMalloc(&p.entries, entries_.size() * 4), "hipMalloc(plan entries)");
-    check_hip(hipMalloc(&p.tiles, tiles_.size() * 4), "hipMalloc(plan tiles)");
-    check_hip(hipMemcpy(p.entries, entries_.data(), entries_.size() * 4, hipMemcpyHostToDevice), "plan upload");
-    check_hip(hipMemcpy(p.tiles, tiles_.data(), tiles_.size() * 4, hipMemcpyHostToDevice), "plan upload");
-    return dev_.emplace(dev, p).first->second;
+    check_hip(hipMalloc(&p.entries, ents.size() * 4), "hipMalloc(plan entries)");
+    check_hip(hipMalloc(&p.tiles, tiles.size() * 4), "hipMalloc(plan tiles)");
+    check_hip(hipMemcpy(p.entries, ents.data(), ents.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    check_hip(hipMemcpy(p.tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    return dev_.emplace(std::make_pair(dev, depth), p).first->second;
 }
 
 // ---------------------------------------------------------------- contexts

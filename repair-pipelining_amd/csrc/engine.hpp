@@ -12,9 +12,7 @@
 //        T2      = c*(v<<6) for v in 0..3   (top 2 bits)
 //     so that c*b = T0[b&7] ^ T1[(b>>3)&7] ^ T2[b>>6]; each lookup is one
 //     v_perm_b32 over four bytes at once (GF(2)-linearity of c*b).
-//   tile (kTileDwords u32): [0] first entry [1] entry count (a multiple of
-//     kDepth, zero-coefficient padding included; kDepth more dummies follow)
-//     [2] rows
+//   tile (kTileDwords u32): [0] first entry [1] entry count [2] rows
 //     [4..4+kTileRows) output slot of each row.
 #pragma once
 
@@ -35,14 +33,19 @@ constexpr int kEntryDwords = 48;
 constexpr int kTileDwords = 16;
 constexpr int kChunkBytes = 4096;  // one 256-thread workgroup x 16 bytes per lane
 constexpr int kBlockThreads = 256;
-constexpr int kDepth = 4;  // 16-B input loads in flight per lane (4 KiB per wave)
 
 void check_hip(hipError_t e, const char *what);
+
+constexpr uint32_t kDummySlot = 0xFFFFFFFFu;  // entry padding: loads the device's zero page
 
 struct DevicePlan {
     uint32_t *entries = nullptr;
     uint32_t *tiles = nullptr;
 };
+
+// 4 KiB of zeros per device, never written: the load target of padding entries
+// (always L2-resident, so padding costs no HBM traffic).
+const uint8_t *zero_page_for_current_device();
 
 // A LinearMap compiled to the kernel's table format, uploaded lazily per device.
 class CompiledMap {
@@ -53,14 +56,16 @@ public:
     int n_tiles() const { return n_tiles_; }
     int max_in_slot() const { return max_in_slot_; }
     int max_out_slot() const { return max_out_slot_; }
-    const DevicePlan &plan_for_current_device();
+    // The plan uploaded for the current device, each tile's entry list padded to a
+    // multiple of `depth` with zero-coefficient kDummySlot entries.
+    const DevicePlan &plan_for_current_device(int depth);
 
 private:
     LinearMap map_;
-    std::vector<uint32_t> entries_, tiles_;
+    std::vector<uint32_t> entries_, tiles_;  // unpadded
     int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1;
     std::mutex mu_;
-    std::map<int, DevicePlan> dev_;
+    std::map<std::pair<int, int>, DevicePlan> dev_;  // (device, depth)
 };
 
 struct ApplyArgs {
@@ -68,20 +73,18 @@ struct ApplyArgs {
     uint8_t *out;
     const uint32_t *entries;
     const uint32_t *tiles;
+    const uint8_t *zero_page;
     int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
     int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
-    int64_t total_items;  // k_gf_stream: (stripe, chunk) items in this launch
     int n_tiles;
-    int items_per_block;  // k_gf_stream: consecutive chunks per workgroup
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
 struct Tuning {
-    // Defaults are the fastest shape measured on MI355X (profiles/r01_kbench.txt):
-    // one 4 KiB chunk per workgroup with non-temporal loads/stores.
-    int items_per_block = 0;  // 0 = one chunk per workgroup (k_gf_apply); >0 = k_gf_stream
+    // Defaults are the fastest shape measured on MI355X (profiles/r01_kbench.txt).
+    int depth = 4;            // k_gf_apply load ring depth (4 or 8)
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
 };

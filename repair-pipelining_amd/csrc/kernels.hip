@@ -104,10 +104,15 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
             acc[o].w = gf_mac4(acc[o].w, t, i0.w, i1.w, i2.w);
         }
     }
-    if (mone) {
+    if (mone) {  // coefficient 1: acc ^= x & mask (one v_bitop3, table 0x78 = a ^ (b & c))
 #pragma unroll
-        for (int o = 0; o < kTileRows; ++o)
-            if (mone & (1u << o)) acc[o] ^= x;
+        for (int o = 0; o < kTileRows; ++o) {
+            const uint32_t m = (mone >> o) & 1u ? 0xFFFFFFFFu : 0u;
+            acc[o].x = __builtin_amdgcn_bitop3_b32(acc[o].x, x.x, m, 0x78);
+            acc[o].y = __builtin_amdgcn_bitop3_b32(acc[o].y, x.y, m, 0x78);
+            acc[o].z = __builtin_amdgcn_bitop3_b32(acc[o].z, x.z, m, 0x78);
+            acc[o].w = __builtin_amdgcn_bitop3_b32(acc[o].w, x.w, m, 0x78);
+        }
     }
 }
 
@@ -126,8 +131,8 @@ __device__ __forceinline__ uint32_t logical_block(bool xcd_group) {
 // NTL / NTS: non-temporal loads / stores.  Outputs are never re-read, so stores
 // are always streamed; loads are streamed only when the map has one tile (no
 // input is read twice), otherwise the re-reads of other tiles hit the caches.
-template <bool SAFE, bool NTL, bool NTS>
-__global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
+template <bool SAFE, bool NTL, bool NTS, int DEPTH>
+__global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
     constexpr int THREADS = kBlockThreads;
     const uint32_t w = logical_block(a.xcd_group != 0);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
@@ -148,8 +153,8 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
         const int64_t v = a.nbytes - off;
         valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
     }
-    auto load = [&](uint32_t slot) -> u32x4 {
-        const uint8_t *p = ib + (int64_t)slot * a.in_slot_stride;
+    auto load = [&](uint32_t slot) -> u32x4 {  // padding entries read the zero page
+        const uint8_t *p = slot == kDummySlot ? a.zero_page + threadIdx.x * 16 : ib + (int64_t)slot * a.in_slot_stride;
         return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
     };
 
@@ -158,25 +163,26 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
 
     cu32 *ent = plan_ptr(a.entries) + (int64_t)ebeg * kEntryDwords;
-    // The host pads every tile's entry list to a multiple of kDepth, so the
-    // ring refill inside the loop is unconditional and never copies a
-    // register whose load is still in flight; the last group is peeled and
-    // issues no refill (no loads past the tile's real entries).
+    // Load ring of DEPTH 16-B loads per lane.  Each tile's entry count is a
+    // multiple of DEPTH (padded on upload), so the refill inside the loop is
+    // unconditional: a slot is consumed, then refilled, keeping DEPTH-1 loads in
+    // flight during every entry's arithmetic, with compile-time vmcnt counts and
+    // no register copies.  The last group is peeled and issues no refill.
     if (ecnt > 0) {
-        u32x4 ring[kDepth];
+        u32x4 ring[DEPTH];
 #pragma unroll
-        for (int u = 0; u < kDepth; ++u) ring[u] = load(ent[u * kEntryDwords]);
-        const int last = ecnt - kDepth;
-        for (int e0 = 0; e0 < last; e0 += kDepth) {
+        for (int u = 0; u < DEPTH; ++u) ring[u] = load(ent[u * kEntryDwords]);
+        const int last = ecnt - DEPTH;
+        for (int e0 = 0; e0 < last; e0 += DEPTH) {
 #pragma unroll
-            for (int u = 0; u < kDepth; ++u) {
+            for (int u = 0; u < DEPTH; ++u) {
                 cu32 *r = ent + (int64_t)(e0 + u) * kEntryDwords;
-                apply_entry(r, ring[u], acc);              // consume the slot, then refill it:
-                ring[u] = load(r[kDepth * kEntryDwords]);  // kDepth-1 loads stay in flight
+                apply_entry(r, ring[u], acc);
+                ring[u] = load(r[DEPTH * kEntryDwords]);
             }
         }
 #pragma unroll
-        for (int u = 0; u < kDepth; ++u) apply_entry(ent + (int64_t)(last + u) * kEntryDwords, ring[u], acc);
+        for (int u = 0; u < DEPTH; ++u) apply_entry(ent + (int64_t)(last + u) * kEntryDwords, ring[u], acc);
     }
 #pragma unroll
     for (int o = 0; o < kTileRows; ++o) {
@@ -190,81 +196,12 @@ __global__ void __launch_bounds__(kBlockThreads) k_gf_apply(ApplyArgs a) {
     }
 }
 
-// Streaming form of k_gf_apply for aligned layouts: one workgroup walks
-// `items_per_block` consecutive 4 KiB chunks (same output tile) and the load
-// ring runs straight across chunk boundaries, so a wave keeps kDepth-1 loads
-// in flight from its first entry to its last store -- no fill/drain bubble
-// per chunk and no dummy prefetches inside the block.
-template <bool NT>
-__global__ void __launch_bounds__(kBlockThreads) k_gf_stream(ApplyArgs a) {
-    const uint32_t tl = blockIdx.x % (uint32_t)a.n_tiles;
-    const uint32_t grp = blockIdx.x / (uint32_t)a.n_tiles;
-    cu32 *tile = plan_ptr(a.tiles) + tl * kTileDwords;
-    const int ecnt = (int)tile[1];  // multiple of kDepth (host padding)
-    const int nrows = (int)tile[2];
-    cu32 *ent = plan_ptr(a.entries) + (int64_t)tile[0] * kEntryDwords;
-
-    const uint32_t item0 = grp * (uint32_t)a.items_per_block;
-    const int nit = (int)min((uint32_t)a.items_per_block, (uint32_t)a.total_items - item0);
-    const uint32_t nch = (uint32_t)a.n_chunks;
-    auto in_off = [&](int it) -> int64_t {
-        const uint32_t gi = item0 + (uint32_t)it;
-        return (a.stripe_begin + gi / nch) * a.in_stripe_stride + (a.chunk_begin + gi % nch) * kChunkBytes;
-    };
-    auto out_off = [&](int it) -> int64_t {
-        const uint32_t gi = item0 + (uint32_t)it;
-        return (a.stripe_begin + gi / nch) * a.out_stripe_stride + (a.chunk_begin + gi % nch) * kChunkBytes;
-    };
-    const int64_t lane = (int64_t)threadIdx.x * 16;
-    const uint8_t *ib = a.in + lane;
-    uint8_t *ob = a.out + lane;
-
-    u32x4 acc[kTileRows];
-#pragma unroll
-    for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
-
-    if (ecnt == 0) {  // all-zero rows
-        for (int it = 0; it < nit; ++it)
-            for (int o = 0; o < nrows; ++o) st16<NT>(ob + out_off(it) + (int64_t)tile[4 + o] * a.out_slot_stride, acc[0]);
-        return;
-    }
-
-    int64_t cur = in_off(0), nxt = in_off(nit > 1 ? 1 : 0);
-    u32x4 ring[kDepth];
-#pragma unroll
-    for (int u = 0; u < kDepth; ++u) ring[u] = ld16<NT>(ib + cur + (int64_t)ent[u * kEntryDwords] * a.in_slot_stride);
-    int item = 0, e = 0;
-    const int total = nit * ecnt;
-    for (int g = 0; g < total; g += kDepth) {
-#pragma unroll
-        for (int u = 0; u < kDepth; ++u) {
-            apply_entry(ent + (int64_t)(e + u) * kEntryDwords, ring[u], acc);
-            const int ep = e + u + kDepth;
-            const bool wrap = ep >= ecnt;  // wave-uniform
-            cu32 *rp = ent + (int64_t)(wrap ? ep - ecnt : ep) * kEntryDwords;
-            ring[u] = ld16<NT>(ib + (wrap ? nxt : cur) + (int64_t)rp[0] * a.in_slot_stride);
-        }
-        e += kDepth;
-        if (e == ecnt) {
-            const int64_t oo = out_off(item);
-#pragma unroll
-            for (int o = 0; o < kTileRows; ++o) {
-                if (o < nrows) st16<NT>(ob + oo + (int64_t)tile[4 + o] * a.out_slot_stride, acc[o]);
-                acc[o] = (u32x4){0u, 0u, 0u, 0u};
-            }
-            e = 0;
-            ++item;
-            cur = nxt;
-            nxt = in_off(item + 1 < nit ? item + 1 : nit - 1);
-        }
-    }
-}
-
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
-    const DevicePlan &plan = cm.plan_for_current_device();
+    const int depth = tuning().depth == 8 ? 8 : 4;
+    const DevicePlan &plan = cm.plan_for_current_device(depth);
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
     const Tuning &tu = tuning();
@@ -277,6 +214,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.out = out;
     a.entries = plan.entries;
     a.tiles = plan.tiles;
+    a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;
     a.in_slot_stride = in_slot_stride;
     a.out_stripe_stride = out_stripe_stride;
@@ -285,28 +223,11 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.n_tiles = cm.n_tiles();
     a.xcd_group = (tuning().xcd_group && a.n_tiles > 1) ? 1 : 0;
     a.accumulate = accumulate ? 1 : 0;
-    a.items_per_block = 0;
-    a.total_items = 0;
 
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
         a.n_chunks = n_chunks;
-        if (!safe && tu.items_per_block > 0 && !accumulate) {
-            const int64_t ipb = tu.items_per_block;
-            const int64_t max_items = ((int64_t)1 << 30) / a.n_tiles * ipb;
-            const int64_t stripes_per_launch = std::max<int64_t>(1, max_items / n_chunks);
-            for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
-                const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
-                a.stripe_begin = s0;
-                a.total_items = ns * n_chunks;
-                a.items_per_block = (int)ipb;
-                const dim3 grid((unsigned)(((a.total_items + ipb - 1) / ipb) * a.n_tiles));
-                if (tu.nontemporal) hipLaunchKernelGGL(k_gf_stream<true>, grid, dim3(kBlockThreads), 0, stream, a);
-                else hipLaunchKernelGGL(k_gf_stream<false>, grid, dim3(kBlockThreads), 0, stream, a);
-            }
-            return;
-        }
         const int64_t per_stripe = n_chunks * a.n_tiles;
         const int64_t max_blocks = (int64_t)1 << 30;
         const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / per_stripe);
@@ -315,10 +236,17 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             a.stripe_begin = s0;
             const dim3 grid((unsigned)(ns * per_stripe));
             const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (a.n_tiles == 1 ? 2 : 1) : 0);
-            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false>), grid, dim3(kBlockThreads), 0, stream, a);
-            else if (ntmode == 2) hipLaunchKernelGGL((k_gf_apply<false, true, true>), grid, dim3(kBlockThreads), 0, stream, a);
-            else if (ntmode == 1) hipLaunchKernelGGL((k_gf_apply<false, false, true>), grid, dim3(kBlockThreads), 0, stream, a);
-            else hipLaunchKernelGGL((k_gf_apply<false, false, false>), grid, dim3(kBlockThreads), 0, stream, a);
+            const dim3 blk(kBlockThreads);
+            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false, 4>), grid, blk, 0, stream, a);
+            else if (depth == 8) {
+                if (ntmode == 2) hipLaunchKernelGGL((k_gf_apply<false, true, true, 8>), grid, blk, 0, stream, a);
+                else if (ntmode == 1) hipLaunchKernelGGL((k_gf_apply<false, false, true, 8>), grid, blk, 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply<false, false, false, 8>), grid, blk, 0, stream, a);
+            } else {
+                if (ntmode == 2) hipLaunchKernelGGL((k_gf_apply<false, true, true, 4>), grid, blk, 0, stream, a);
+                else if (ntmode == 1) hipLaunchKernelGGL((k_gf_apply<false, false, true, 4>), grid, blk, 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply<false, false, false, 4>), grid, blk, 0, stream, a);
+            }
         }
     };
     run(false, 0, full);

@@ -26,17 +26,17 @@ def timed(fn, reps=10):
     return e0.elapsed_time(e1) / reps * 1e-3
 
 
-SWEEP = [(0, 1), (0, 0), (0, 2), (4, 1), (4, 0)]  # (items_per_block, nontemporal); first = default
+SWEEP = [(4, 1), (4, 0), (4, 2), (8, 1), (8, 0)]  # (load-ring depth, nontemporal); first = default
 
 
 def sweep(lib, name, unit_bytes, units, fn, reps=10, extra=None):
     """Time fn under each launch shape of SWEEP (results are bit-identical)."""
-    for ipb, nt in SWEEP:
-        lib.ecx_tune(b"items_per_block", ipb)
+    for depth, nt in SWEEP:
+        lib.ecx_tune(b"depth", depth)
         lib.ecx_tune(b"nontemporal", nt)
         t = timed(fn, reps)
-        report(name, unit_bytes, units, t, dict(extra or {}, items_per_block=ipb, nontemporal=nt))
-    lib.ecx_tune(b"items_per_block", 0)
+        report(name, unit_bytes, units, t, dict(extra or {}, depth=depth, nontemporal=nt))
+    lib.ecx_tune(b"depth", 4)
     lib.ecx_tune(b"nontemporal", 1)
 
 

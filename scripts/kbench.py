@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--pool", type=int, default=1 << 14)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0:0,0:1,0:2,4:1,8:1")
+    ap.add_argument("--variants", default="4:1,8:1,4:0,8:0,4:2")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
@@ -62,19 +62,19 @@ def main():
 
     variants = []
     for v in args.variants.split(","):
-        ipb, nt = map(int, v.split(":"))
-        variants.append((f"clay ipb={ipb} nt={nt}", clay, ipb, nt, P * ALGO))
-    variants.append(("xor-only ipb=0 nt=1", xor_only, 0, 1, P * ALGO))
-    variants.append(("probe read nt=0", probe(0, 0), 0, 0, PROBE))
-    variants.append(("probe read nt=1", probe(0, 1), 0, 0, PROBE))
-    variants.append(("probe copy nt=0", probe(1, 0), 0, 0, 2 * PROBE))
-    variants.append(("probe copy nt=1", probe(1, 1), 0, 0, 2 * PROBE))
-    variants.append(("d2d copy (torch)", copy, 0, 0, 2 * P * ALPHA * B))
+        depth, nt = map(int, v.split(":"))
+        variants.append((f"clay depth={depth} nt={nt}", clay, depth, nt, P * ALGO))
+    variants.append(("xor-only depth=4 nt=1", xor_only, 4, 1, P * ALGO))
+    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE))
+    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE))
+    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE))
+    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE))
+    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B))
 
     res = {name: [] for name, *_ in variants}
     for r in range(args.rounds):
-        for name, fn, ipb, nt, nbytes in variants:
-            lib.ecx_tune(b"items_per_block", ipb)
+        for name, fn, depth, nt, nbytes in variants:
+            lib.ecx_tune(b"depth", depth)
             lib.ecx_tune(b"nontemporal", nt)
             fn()
             torch.cuda.synchronize()
@@ -86,7 +86,7 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.launches
             res[name].append(nbytes / (ms * 1e-3) / 1e9)
-    lib.ecx_tune(b"items_per_block", 0)
+    lib.ecx_tune(b"depth", 4)
     lib.ecx_tune(b"nontemporal", 1)
     for name, *_ in variants:
         v = res[name]
