@@ -34,7 +34,7 @@ READ_BYTES = 20 * B                          # helper sub-chunks read by one rep
 WRITE_BYTES = ALPHA * B                      # repaired sub-chunks written
 ALGO_BYTES = READ_BYTES + WRITE_BYTES        # 917,504 B per stripe
 HBM_PEAK_GBS = 8000.0                        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL = "k_gf_apply<false,true,true>"  # dominant kernel (SAFE=false, NT loads, NT stores)
+KERNEL = "k_gf_apply<false,true,true,8>"  # dominant kernel (SAFE=false, NT loads, NT stores, depth 8)
 METRIC = "GiB/s repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU"
 
 

@@ -3,7 +3,8 @@
  * Not part of the reference's coding interface (include/ecx.h is the boundary);
  * results are bit-identical for every setting, only speed changes.
  *
- *   "depth"            4 or 8: 16-B loads per lane in the kernel's load ring (default 4)
+ *   "depth"            16-B loads per lane in the kernel's load ring: 0 = per map (default:
+ *                      8 when every tile has >= 16 entries, else 4), or force 4 / 8
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        1 = multi-tile maps keep the tiles of one chunk on one XCD (default 0)

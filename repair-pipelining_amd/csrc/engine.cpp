@@ -120,6 +120,12 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
     }
     if (tiles_.empty()) tiles_.assign(kTileDwords, 0);
     if (entries_.empty()) entries_.assign(kEntryDwords, 0);
+    int min_count = 1 << 30;
+    for (int t = 0; t < n_tiles_; ++t) {
+        const int c = (int)tiles_[(size_t)t * kTileDwords + 1];
+        if (c > 0) min_count = std::min(min_count, c);
+    }
+    preferred_depth_ = (min_count != (1 << 30) && min_count >= 16) ? 8 : 4;
 }
 
 const uint8_t *zero_page_for_current_device() {

@@ -56,6 +56,9 @@ public:
     int n_tiles() const { return n_tiles_; }
     int max_in_slot() const { return max_in_slot_; }
     int max_out_slot() const { return max_out_slot_; }
+    // Load-ring depth for this map: 8 when every non-empty tile has >= 16 entries
+    // (padding to a multiple of 8 then costs little), else 4 (profiles/r01_configs_depth.jsonl).
+    int preferred_depth() const { return preferred_depth_; }
     // The plan uploaded for the current device, each tile's entry list padded to a
     // multiple of `depth` with zero-coefficient kDummySlot entries.
     const DevicePlan &plan_for_current_device(int depth);
@@ -63,7 +66,7 @@ public:
 private:
     LinearMap map_;
     std::vector<uint32_t> entries_, tiles_;  // unpadded
-    int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1;
+    int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1, preferred_depth_ = 4;
     std::mutex mu_;
     std::map<std::pair<int, int>, DevicePlan> dev_;  // (device, depth)
 };
@@ -84,7 +87,7 @@ struct ApplyArgs {
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
 struct Tuning {
     // Defaults are the fastest shape measured on MI355X (profiles/r01_kbench.txt).
-    int depth = 4;            // k_gf_apply load ring depth (4 or 8)
+    int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or 4 / 8
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
 };

@@ -200,7 +200,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
-    const int depth = tuning().depth == 8 ? 8 : 4;
+    const int depth = tuning().depth == 8 ? 8 : (tuning().depth == 4 ? 4 : cm.preferred_depth());
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);

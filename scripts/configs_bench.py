@@ -26,7 +26,7 @@ def timed(fn, reps=10):
     return e0.elapsed_time(e1) / reps * 1e-3
 
 
-SWEEP = [(4, 1), (4, 0), (4, 2), (8, 1), (8, 0)]  # (load-ring depth, nontemporal); first = default
+SWEEP = [(0, 1), (4, 1), (8, 1), (0, 0)]  # (load-ring depth, nontemporal); first = default (0 = per map)
 
 
 def sweep(lib, name, unit_bytes, units, fn, reps=10, extra=None):
@@ -36,7 +36,7 @@ def sweep(lib, name, unit_bytes, units, fn, reps=10, extra=None):
         lib.ecx_tune(b"nontemporal", nt)
         t = timed(fn, reps)
         report(name, unit_bytes, units, t, dict(extra or {}, depth=depth, nontemporal=nt))
-    lib.ecx_tune(b"depth", 4)
+    lib.ecx_tune(b"depth", 0)
     lib.ecx_tune(b"nontemporal", 1)
 
 
