@@ -10,9 +10,10 @@ scaling); the only collectives are the timing barrier and the max-over-ranks.
 Metric: algorithmic bytes per stripe = 20 helper
 sub-chunks read + 8 repaired sub-chunks written = 917,504 B; GiB/s = bytes
 * stripes / time / 2^30, whole job.  ``roofline`` prices the dominant kernel
-(k_gf_apply<false,true,true>) against the MI355X HBM peak from per-launch HIP events;
+(k_gf_apply<false,true,true,8>) against the MI355X HBM peak from per-launch HIP events;
 ``cpu_baseline`` times the oracle (the C restatement of the reference's JVM
-path, stage by stage) on this host for a bounded sample.
+path, stage by stage) on this host for a bounded sample: one thread, then one
+thread per host core (oracle/orc_bench.c).
 """
 import argparse
 import json
@@ -51,38 +52,51 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
 def cpu_baseline(seconds: float, erased: int):
     """Oracle (C restatement of the reference JVM path: InputOutputByteTableCodingLoop
-    + the ClayCodeErasureDecodingStep.doDecodeSingle stage sequence, one thread)."""
+    + the ClayCodeErasureDecodingStep.doDecodeSingle stage sequence), timed by
+    oracle/orc_bench.c on one host thread and then on one thread per host core
+    (independent stripes per thread).  ``value`` is the
+    all-cores figure; the 1-thread figure rides along."""
     import numpy as np
     import oracle as O
 
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0)), 64))
+    per_thread = 2
     rng = np.random.default_rng(0)
-    stripes = []
-    for _ in range(4):
+
+    def stripe():
         data = [rng.integers(0, 256, B, dtype=np.uint8) if (i % N_NODES) < K else None
                 for i in range(N_NODES * ALPHA)]
         par = O.clay_encode(K, M, data, B)
         full = [data[i] if (i % N_NODES) < K else par[(i // N_NODES) * M + (i % N_NODES) - K]
                 for i in range(N_NODES * ALPHA)]
-        stripes.append([None if (i % N_NODES) == erased else full[i] for i in range(N_NODES * ALPHA)])
-    c = O.Clay(K, M, [erased])
-    outs = [np.zeros(B, np.uint8) for _ in range(ALPHA)]
-    c.perform_coding(stripes[0], outs, B)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        c.perform_coding(stripes[n % len(stripes)], outs, B)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+        return [None if (i % N_NODES) == erased else full[i] for i in range(N_NODES * ALPHA)]
+
+    stripes = [stripe() for _ in range(per_thread * threads)]
+    n1, el1 = O.bench_clay_repair(K, M, erased, B, stripes[:per_thread], 1, seconds / 2)
+    nn, eln = O.bench_clay_repair(K, M, erased, B, stripes, threads, seconds)
+    one = n1 * ALGO_BYTES / el1 / 2**30
     return {
-        "value": n * ALGO_BYTES / el / 2**30,
+        "value": round(nn * ALGO_BYTES / eln / 2**30, 3),
         "unit": "GiB/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{n} Clay(4,2) single repairs (e={erased}, B=32 KiB) of 4 host-resident valid stripes, "
-                  f"stage-by-stage C restatement of the reference JVM path, 1 thread, {el:.1f} s",
+        "single_thread_value": round(one, 3),
+        "sample": f"Clay(4,2) single repairs (e={erased}, B=32 KiB), stage-by-stage C restatement of the "
+                  f"reference JVM path (oracle/): {nn} repairs on {threads} threads x {per_thread} host-resident "
+                  f"valid stripes each in {eln:.1f} s; single thread {n1} repairs in {el1:.1f} s; {_cpu_model()}",
     }
 
 

@@ -105,6 +105,12 @@ int orc_clay_decode_single_helper(orc_clay *c, uint8_t *const *helper_coupled, i
 /* ClayCode.getInputs: flat n*alpha*B buffer, present[] flags (data sub-chunks only). */
 int orc_clay_get_inputs(int data_units, int parity_units, int block_size, uint8_t *flat, uint8_t *present);
 
+/* orc_bench.c -- timing harness (bench.py cpu_baseline): `threads` workers, each with its
+ * own Clay step object, repair `erased` on their own `per_thread` stripes for `seconds`.
+ * stripes: [threads*per_thread][n*alpha] sub-chunk pointers (NULL = absent). */
+int orc_bench_clay_repair(int data_units, int parity_units, int erased, int buf_size, uint8_t *const *stripes,
+                          int per_thread, int threads, double seconds, long long *repairs, double *elapsed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -94,6 +94,8 @@ def _load():
         "orc_clay_perform_coding": (I, [P, PP, PP, I]),
         "orc_clay_decode_single_helper": (I, [P, PP, I, PP, I, I]),
         "orc_clay_get_inputs": (I, [I, I, I, P, P]),
+        "orc_bench_clay_repair": (I, [I, I, I, I, PP, I, I, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -311,6 +313,17 @@ class Clay:
     def decode_single_helper(self, helper_coupled, helper_i, outputs, erased_index, buf_size):
         _check(lib().orc_clay_decode_single_helper(self._h, _ptrs(helper_coupled), helper_i, _ptrs(outputs),
                                                    erased_index, buf_size))
+
+
+def bench_clay_repair(data_units, parity_units, erased, block_size, stripes, threads, seconds):
+    """Timing harness (orc_bench.c): `stripes` is a list of threads*per_thread stripes, each a
+    list of n*alpha sub-chunk arrays (None = absent).  Returns (repairs, max elapsed seconds)."""
+    per = len(stripes) // threads
+    flat = [sc for st in stripes[:per * threads] for sc in st]
+    reps, el = ctypes.c_longlong(0), ctypes.c_double(0.0)
+    _check(lib().orc_bench_clay_repair(data_units, parity_units, erased, block_size, _ptrs(flat), per, threads,
+                                       float(seconds), ctypes.byref(reps), ctypes.byref(el)))
+    return int(reps.value), float(el.value)
 
 
 def clay_get_inputs(data_units: int, parity_units: int, block_size: int):

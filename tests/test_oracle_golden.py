@@ -240,3 +240,19 @@ def test_clay_unsupported_geometry():
     c = O.Clay(10, 4, [13])
     with pytest.raises(O.OracleError):
         c.helper_planes(13)
+
+
+def test_cpu_baseline_harness_runs_threads():
+    """orc_bench.c (bench.py's cpu_baseline) runs the oracle repair on several threads."""
+    import numpy as np
+    import oracle as O
+    rng = np.random.default_rng(3)
+    k, m, e, b = 4, 2, 1, 512
+    stripes = []
+    for _ in range(4):
+        data = [rng.integers(0, 256, b, dtype=np.uint8) if i % 6 < k else None for i in range(48)]
+        par = O.clay_encode(k, m, data, b)
+        full = [data[i] if i % 6 < k else par[(i // 6) * m + i % 6 - k] for i in range(48)]
+        stripes.append([None if i % 6 == e else full[i] for i in range(48)])
+    reps, el = O.bench_clay_repair(k, m, e, b, stripes, 2, 0.05)
+    assert reps >= 2 and el >= 0.05
