@@ -182,6 +182,28 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
                                   int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
                                   int64_t out_sub_stride, int64_t nstripes, int64_t buf_size, void *stream);
 
+/* ---------------------------------------------------------------- host-memory batches */
+/* The reference's repair starts and ends in host memory: helper sub-chunks arrive on
+ * sockets into ByteBuffers (ClayCoordinator.kt:372-395) and leave the same way
+ * (ClayCodeNode.kt:330-347).  A JNI shim hands over their addresses via
+ * GetDirectBufferAddress (ECChunk.toBuffers, ECChunk.java:81-95).
+ * These calls take the batch layouts above with HOST pointers.  Chunks of stripes are
+ * pipelined H2D -> kernel -> D2H on internal streams, and only the map's used input
+ * slots cross PCIe.  The calls are synchronous.  Pinned memory (ecx_host_alloc /
+ * ecx_host_register) runs at the PCIe rate.  Outputs may point into the input stripes
+ * (in-place decodeMissing) when no output slot is also an input slot. */
+int ecx_map_apply_batch_host(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
+                             int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride,
+                             int64_t out_slot_stride, int64_t nstripes, int64_t byte_count);
+int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
+                                       int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
+                                       int64_t out_sub_stride, int64_t nstripes, int64_t buf_size);
+/* Page-locked host memory for the calls above (e.g. backing direct ByteBuffers). */
+int ecx_host_alloc(int64_t nbytes, void **out);
+int ecx_host_free(void *ptr);
+int ecx_host_register(void *ptr, int64_t nbytes);
+int ecx_host_unregister(void *ptr);
+
 /* ---------------------------------------------------------------- synthetic data / verification (device) */
 /* Deterministic counter-based fill: byte i of the region = f(seed, i). */
 int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream);

@@ -8,6 +8,8 @@
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        1 = multi-tile maps keep the tiles of one chunk on one XCD (default 0)
+ *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
+ *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  */
 #ifndef ECX_TUNE_H
 #define ECX_TUNE_H

@@ -125,6 +125,51 @@ def _dev_ptr(x) -> int:
     raise TypeError("expected a device tensor or an integer pointer")
 
 
+def _host_ptr(x) -> int:
+    """Host address of a numpy array, a CPU torch tensor (pinned or not) or an int."""
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        return int(x.ctypes.data)
+    if hasattr(x, "data_ptr"):
+        if x.is_cuda:
+            raise TypeError("host batch APIs take host (CPU) buffers")
+        return int(x.data_ptr())
+    raise TypeError("expected a host array/tensor or an integer pointer")
+
+
+class HostBuffer:
+    """Page-locked host memory from ecx_host_alloc, viewed as a numpy uint8 array."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib().ecx_host_alloc(nbytes, ctypes.byref(p)))
+        self._p = p
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, nbytes)).from_address(p.value))[:nbytes]
+
+    def __del__(self):
+        if getattr(self, "_p", None) and lib is not None:
+            lib().ecx_host_free(self._p)
+            self._p = None
+
+
+def host_register(arr) -> None:
+    """Page-lock an existing host buffer (hipHostRegister) for PCIe-rate host batches."""
+    check(lib().ecx_host_register(_host_ptr(arr), int(arr.nbytes)))
+
+
+def host_unregister(arr) -> None:
+    check(lib().ecx_host_unregister(_host_ptr(arr)))
+
+
+def tune(key: str, value: int) -> None:
+    """Launch-shape knobs (include/ecx_tune.h); results are bit-identical for every setting."""
+    f = lib().ecx_tune
+    f.argtypes, f.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+    check(f(key.encode(), int(value)))
+
+
 def _stream(stream) -> Optional[int]:
     if stream is None:
         try:
@@ -293,6 +338,13 @@ class GfMap:
                     byte_count, stream=None):
         check(lib().ecx_map_apply_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_slot_stride, _dev_ptr(out),
                                         out_stripe_stride, out_slot_stride, nstripes, byte_count, _stream(stream)))
+
+    def apply_batch_host(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride,
+                         nstripes, byte_count):
+        """apply_batch over host buffers: pipelined H2D -> kernel -> D2H, synchronous."""
+        check(lib().ecx_map_apply_batch_host(self._h, _host_ptr(inp), in_stripe_stride, in_slot_stride,
+                                             _host_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
+                                             byte_count))
 
 
 # ---------------------------------------------------------------- ReedSolomon.java
@@ -500,6 +552,13 @@ class ClayCodeErasureDecodingStep:
         check(lib().ecx_clay_perform_coding_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_sub_stride,
                                                   _dev_ptr(out), out_stripe_stride, out_sub_stride, nstripes,
                                                   bufSize, _stream(stream)))
+
+    def performCodingBatchHost(self, inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
+                               nstripes, bufSize) -> None:
+        """performCodingBatch over host-memory stripes (ecx_clay_perform_coding_batch_host)."""
+        check(lib().ecx_clay_perform_coding_batch_host(self._h, _host_ptr(inp), in_stripe_stride, in_sub_stride,
+                                                       _host_ptr(out), out_stripe_stride, out_sub_stride, nstripes,
+                                                       bufSize))
 
 
 class JavaRandom:

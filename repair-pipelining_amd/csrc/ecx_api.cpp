@@ -633,6 +633,67 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
     });
 }
 
+// ---------------------------------------------------------------- host-memory batches (f1)
+int ecx_map_apply_batch_host(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                             uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                             int64_t byte_count) {
+    return guarded([&]() -> int {
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null host pointer");
+        run_host_batch(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
+                       out_slot_stride, nstripes, byte_count);
+        return ECX_OK;
+    });
+}
+
+int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
+                                       int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
+                                       int64_t out_sub_stride, int64_t nstripes, int64_t buf_size) {
+    return guarded([&]() -> int {
+        if (clay->pl.erased().empty()) return ECX_OK;
+        if (nstripes < 0 || buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null host pointer");
+        ecx_map *m = clay_standard_map(clay);
+        run_host_batch(m->cm, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
+                       buf_size);
+        return ECX_OK;
+    });
+}
+
+int ecx_host_alloc(int64_t nbytes, void **out) {
+    return guarded([&]() -> int {
+        if (!out) throw Error(ECX_E_NULL, "null out pointer");
+        if (nbytes < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative size");
+        *out = nullptr;
+        check_hip(hipHostMalloc(out, (size_t)std::max<int64_t>(nbytes, 1), hipHostMallocDefault), "hipHostMalloc");
+        return ECX_OK;
+    });
+}
+
+int ecx_host_free(void *ptr) {
+    return guarded([&]() -> int {
+        if (ptr) check_hip(hipHostFree(ptr), "hipHostFree");
+        return ECX_OK;
+    });
+}
+
+int ecx_host_register(void *ptr, int64_t nbytes) {
+    return guarded([&]() -> int {
+        if (!ptr) throw Error(ECX_E_NULL, "null pointer");
+        if (nbytes <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "non-positive size");
+        check_hip(hipHostRegister(ptr, (size_t)nbytes, hipHostRegisterDefault), "hipHostRegister");
+        return ECX_OK;
+    });
+}
+
+int ecx_host_unregister(void *ptr) {
+    return guarded([&]() -> int {
+        if (!ptr) throw Error(ECX_E_NULL, "null pointer");
+        check_hip(hipHostUnregister(ptr), "hipHostUnregister");
+        return ECX_OK;
+    });
+}
+
 // ---------------------------------------------------------------- tuning hook (include/ecx_tune.h)
 int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
@@ -646,6 +707,14 @@ int ecx_tune(const char *key, int value) {
         t.nontemporal = value;
     }
     else if (k == "xcd_group") t.xcd_group = value != 0;
+    else if (k == "host_chunk_kib") {
+        if (value < 1) return ECX_E_ILLEGAL_ARGUMENT;
+        t.host_chunk = (int64_t)value << 10;
+    }
+    else if (k == "host_buffers") {
+        if (value < 1 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
+        t.host_buffers = value;
+    }
     else return ECX_E_ILLEGAL_ARGUMENT;
     return ECX_OK;
 }

@@ -185,6 +185,40 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;
 }
 
+namespace {
+std::vector<int> sorted_unique(std::vector<int> v) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    return v;
+}
+int rank_of(const std::vector<int> &sorted, int slot) {
+    return (int)(std::lower_bound(sorted.begin(), sorted.end(), slot) - sorted.begin());
+}
+}  // namespace
+
+CompiledMap &CompiledMap::compact() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!compact_) {
+        used_in_ = sorted_unique(map_.in_slot);
+        used_out_ = sorted_unique(map_.out_slot);
+        LinearMap c = map_;
+        for (int &s : c.in_slot) s = rank_of(used_in_, s);
+        for (int &s : c.out_slot) s = rank_of(used_out_, s);
+        compact_ = std::make_unique<CompiledMap>(std::move(c));
+    }
+    return *compact_;
+}
+
+const std::vector<int> &CompiledMap::used_in_slots() {
+    compact();
+    return used_in_;
+}
+
+const std::vector<int> &CompiledMap::used_out_slots() {
+    compact();
+    return used_out_;
+}
+
 // ---------------------------------------------------------------- contexts
 DeviceContext &DeviceContext::current() {
     static std::mutex reg_mu;

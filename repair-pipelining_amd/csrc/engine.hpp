@@ -62,9 +62,17 @@ public:
     // The plan uploaded for the current device, each tile's entry list padded to a
     // multiple of `depth` with zero-coefficient kDummySlot entries.
     const DevicePlan &plan_for_current_device(int depth);
+    // The same map over densely renumbered slots: input column j reads compact slot
+    // rank(in_slot[j]) among used_in_slots() (sorted), likewise for outputs.  This is
+    // the device-side layout of the host-batch pipeline (host_pipe.cpp).
+    CompiledMap &compact();
+    const std::vector<int> &used_in_slots();
+    const std::vector<int> &used_out_slots();
 
 private:
     LinearMap map_;
+    std::unique_ptr<CompiledMap> compact_;
+    std::vector<int> used_in_, used_out_;
     std::vector<uint32_t> entries_, tiles_;  // unpadded
     int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1, preferred_depth_ = 4;
     std::mutex mu_;
@@ -90,6 +98,8 @@ struct Tuning {
     int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or 4 / 8
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
+    int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
+    int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();
@@ -127,5 +137,14 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
 // As run_host, but instead of copying outputs back, returns whether every
 // output byte is zero (used for checkSomeShards / isParityCorrect).
 bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count);
+
+// Host-memory batch over many stripes (host_pipe.cpp): the batch layout of
+// launch_apply, but `in`/`out` are host pointers.  Chunks of stripes are
+// pipelined H2D (copy stream) -> kernel (compute stream) -> D2H (copy stream)
+// through `host_buffers` device buffer sets; only the map's used slots cross
+// PCIe.  Synchronous.  Pinned host memory runs at the PCIe rate.
+void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                    uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                    int64_t nbytes);
 
 }  // namespace ecx

@@ -1,0 +1,165 @@
+// host_pipe.cpp -- pipelined host-memory batches.
+//
+// The reference's repair path starts and ends in host memory.  Helper
+// sub-chunks arrive on sockets into ByteBuffers (ClayCoordinator.kt:372-395),
+// and repaired sub-chunks leave the same way (ClayCodeNode.kt:330-347).
+// run_host_batch takes the device batch layout with host pointers.  It streams
+// chunks of stripes through a ring of device buffer sets on three streams, so
+// the PCIe transfers of chunk i+1 and i-1 overlap the kernel of chunk i:
+//
+//   h2d stream:  [in i] [in i+1] ...      (waits: the kernel that last read set k)
+//   cmp stream:         [map i]  ...      (waits: in i loaded, out i-NB drained)
+//   d2h stream:                [out i] ...(waits: map i)
+//
+// Only the map's used input slots cross PCIe; the Clay(4,2) e=1 repair, for
+// example, moves 20 of the 48 sub-chunks of a stripe.  Consecutive used slots
+// that are also consecutive in host memory are merged into one strided (2D)
+// copy per chunk.
+#include <algorithm>
+
+#include "engine.hpp"
+
+namespace ecx {
+namespace {
+
+struct Run {
+    int slot0;     // first host slot
+    int compact0;  // first compact (device) slot
+    int len;       // slots in the run
+};
+
+std::vector<Run> runs_of(const std::vector<int> &slots, int64_t slot_stride, int64_t nbytes) {
+    std::vector<Run> runs;
+    for (size_t i = 0; i < slots.size(); ++i) {
+        if (!runs.empty() && slot_stride == nbytes && slots[i] == runs.back().slot0 + runs.back().len) {
+            ++runs.back().len;
+            continue;
+        }
+        runs.push_back({slots[i], (int)i, 1});
+    }
+    return runs;
+}
+
+// Copy `rows` rows of `width` bytes between two pitched layouts.
+void copy_rows(uint8_t *dst, int64_t dpitch, const uint8_t *src, int64_t spitch, int64_t width, int64_t rows,
+               hipMemcpyKind kind, hipStream_t s) {
+    if (rows == 1 || (dpitch == width && spitch == width)) {
+        check_hip(hipMemcpyAsync(dst, src, (size_t)(width * rows), kind, s), "hipMemcpyAsync (host batch)");
+        return;
+    }
+    if (dpitch >= width && spitch >= width) {
+        check_hip(hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)rows, kind, s),
+                  "hipMemcpy2DAsync (host batch)");
+        return;
+    }
+    for (int64_t r = 0; r < rows; ++r)
+        check_hip(hipMemcpyAsync(dst + r * dpitch, src + r * spitch, (size_t)width, kind, s),
+                  "hipMemcpyAsync (host batch row)");
+}
+
+// Per-device streams, buffer sets and events of the host-batch pipeline.
+class HostPipe {
+public:
+    struct Set {
+        uint8_t *in = nullptr, *out = nullptr;
+        size_t in_cap = 0, out_cap = 0;
+        hipEvent_t loaded = nullptr, computed = nullptr, drained = nullptr;
+    };
+
+    static HostPipe &current() {
+        static std::mutex reg_mu;
+        static std::map<int, std::unique_ptr<HostPipe>> reg;
+        int dev = 0;
+        check_hip(hipGetDevice(&dev), "hipGetDevice");
+        std::lock_guard<std::mutex> lk(reg_mu);
+        auto &slot = reg[dev];
+        if (!slot) {
+            auto p = std::make_unique<HostPipe>();
+            for (hipStream_t *s : {&p->h2d, &p->cmp, &p->d2h})
+                check_hip(hipStreamCreateWithFlags(s, hipStreamNonBlocking), "hipStreamCreate (host batch)");
+            slot = std::move(p);
+        }
+        return *slot;
+    }
+
+    // Called with every stream idle (the previous call synchronised).
+    void ensure(int nb, size_t in_bytes, size_t out_bytes) {
+        while ((int)sets.size() < nb) {
+            Set s;
+            for (hipEvent_t *e : {&s.loaded, &s.computed, &s.drained})
+                check_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate (host batch)");
+            sets.push_back(s);
+        }
+        for (int k = 0; k < nb; ++k) {
+            Set &s = sets[k];
+            if (s.in_cap < in_bytes) {
+                if (s.in) check_hip(hipFree(s.in), "hipFree (host batch)");
+                s.in = nullptr;
+                s.in_cap = 0;
+                check_hip(hipMalloc(&s.in, in_bytes), "hipMalloc (host batch)");
+                s.in_cap = in_bytes;
+            }
+            if (s.out_cap < out_bytes) {
+                if (s.out) check_hip(hipFree(s.out), "hipFree (host batch)");
+                s.out = nullptr;
+                s.out_cap = 0;
+                check_hip(hipMalloc(&s.out, out_bytes), "hipMalloc (host batch)");
+                s.out_cap = out_bytes;
+            }
+        }
+    }
+
+    void drain() {
+        for (hipStream_t s : {h2d, cmp, d2h}) (void)hipStreamSynchronize(s);
+    }
+
+    std::mutex mu;
+    hipStream_t h2d = nullptr, cmp = nullptr, d2h = nullptr;
+    std::vector<Set> sets;
+};
+
+}  // namespace
+
+void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                    uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                    int64_t nbytes) {
+    if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
+    CompiledMap &cc = cm.compact();
+    const std::vector<int> &ins = cm.used_in_slots(), &outs = cm.used_out_slots();
+    const int64_t in_per = (int64_t)ins.size() * nbytes, out_per = (int64_t)outs.size() * nbytes;
+    const Tuning &t = tuning();
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, t.host_chunk / std::max<int64_t>(1, in_per)));
+    const int64_t nchunks = (nstripes + chunk - 1) / chunk;
+    const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
+    const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes), rout = runs_of(outs, out_slot_stride, nbytes);
+
+    HostPipe &p = HostPipe::current();
+    std::lock_guard<std::mutex> lk(p.mu);
+    try {
+        p.ensure(nb, (size_t)(chunk * in_per), (size_t)(chunk * out_per));
+        for (int64_t i = 0; i < nchunks; ++i) {
+            HostPipe::Set &b = p.sets[(size_t)(i % nb)];
+            const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
+            if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
+            for (const Run &r : rin)
+                copy_rows(b.in + r.compact0 * nbytes, in_per, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
+                          in_stripe_stride, r.len * nbytes, n, hipMemcpyHostToDevice, p.h2d);
+            check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
+            if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");
+            launch_apply(cc, b.in, in_per, nbytes, b.out, out_per, nbytes, n, nbytes, p.cmp);
+            check_hip(hipEventRecord(b.computed, p.cmp), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(p.d2h, b.computed, 0), "hipStreamWaitEvent");
+            for (const Run &r : rout)
+                copy_rows(out + lo * out_stripe_stride + r.slot0 * out_slot_stride, out_stripe_stride,
+                          b.out + r.compact0 * nbytes, out_per, r.len * nbytes, n, hipMemcpyDeviceToHost, p.d2h);
+            check_hip(hipEventRecord(b.drained, p.d2h), "hipEventRecord");
+        }
+        check_hip(hipStreamSynchronize(p.d2h), "hipStreamSynchronize (host batch)");
+    } catch (...) {
+        p.drain();
+        throw;
+    }
+}
+
+}  // namespace ecx

@@ -45,6 +45,15 @@ def test_no_gpu_fails_loudly(ecx):
     with pytest.raises(ecx.EcxError) as e:
         rs.encodeParity([np.zeros(16, np.uint8) for _ in range(6)], 0, 16)
     assert e.value.code == -10
+    # the host-memory batch path has no CPU fallback either
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    host_in, host_out = np.zeros((2, 48, 64), np.uint8), np.zeros((2, 8, 64), np.uint8)
+    with pytest.raises(ecx.EcxError) as e:
+        step.performCodingBatchHost(host_in, 48 * 64, 64, host_out, 8 * 64, 64, 2, 64)
+    assert e.value.code == -10
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.HostBuffer(4096)
+    assert e.value.code == -10
 
 
 def _has_device(ecx):

@@ -497,3 +497,77 @@ def test_partial_sum_batches(ecx, torch_dev):
         rs.encodePartialBatch(i, pool[:, i], 6 * L, par, 2 * L, L, S, L, i == 0)
     torch.cuda.synchronize()
     assert torch.equal(par, pool[:, 4:6])
+
+
+# ---------------------------------------------------------------- host-memory batches
+@pytest.fixture
+def small_host_chunks(ecx):
+    """Force many pipelined chunks and ring reuse; restore the defaults afterwards."""
+    ecx.tune("host_chunk_kib", 96)
+    ecx.tune("host_buffers", 3)
+    yield
+    ecx.tune("host_chunk_kib", 65536)
+    ecx.tune("host_buffers", 3)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_clay_host_batch_vs_oracle(ecx, small_host_chunks, pinned):
+    """performCodingBatchHost from the full 48-slot host layout (only the 20 helper
+    slots cross PCIe) equals the oracle's performCoding on every stripe."""
+    k, m, B, S, e = 4, 2, 2048 + 16, 23, 1
+    rng = np.random.default_rng(41)
+    if pinned:
+        hb = ecx.HostBuffer(S * 48 * B)
+        pool = hb.array.reshape(S, 48, B)
+        pool[:] = rng.integers(0, 256, (S, 48, B), dtype=np.uint8)
+    else:
+        pool = rng.integers(0, 256, (S, 48, B), dtype=np.uint8)
+    out = np.full((S, 8, B), 0xAB, np.uint8)
+    ecx.ClayCodeErasureDecodingStep([e], k, m).performCodingBatchHost(pool, 48 * B, B, out, 8 * B, B, S, B)
+    for s in range(S):
+        inputs = [None if (i % 6) == e else pool[s, i].copy() for i in range(48)]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
+        assert all((out[s, z] == ref[z]).all() for z in range(8)), s
+
+
+def test_rs_host_batch_in_place_unaligned(ecx, small_host_chunks):
+    """RS(12,4) decodeMissing over host stripes, in place, with a ragged shard length and a
+    padded shard stride (per-slot strided copies, byte-safe kernel)."""
+    k, m, L, S = 12, 4, 10001, 9
+    pitch = L + 37
+    rs = ecx.ReedSolomon.create(k, m)
+    rng = np.random.default_rng(8)
+    pool = np.zeros((S, 16, pitch), np.uint8)
+    pool[:, :k, :L] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    rs.encode_map().apply_batch_host(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+    for s in (0, S - 1):
+        b = [pool[s, i, :L].copy() for i in range(16)]
+        O.ReedSolomon(k, m).encode_parity(b, 0, L)
+        assert all((b[i] == pool[s, i, :L]).all() for i in range(k, 16))
+    orig = pool.copy()
+    present = [True] * 16
+    for i in (0, 5, 13):
+        present[i] = False
+        pool[:, i] = 0x5A
+    rs.decode_map(present).apply_batch_host(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+    assert (pool[:, :, :L] == orig[:, :, :L]).all()
+    assert (pool[:, (0, 5, 13), L:] == 0x5A).all()  # bytes past the shard untouched
+
+
+def test_lrc_host_batch_matches_device_batch(ecx, torch_dev):
+    """The same map over the same stripes: host and device batch paths agree byte for byte."""
+    torch = torch_dev
+    B, S = 65536, 40
+    mat = np.zeros((4, 12), np.uint8)
+    for g in range(4):
+        mat[g, 3 * g:3 * g + 3] = 1
+    gmap = ecx.GfMap.from_matrix(mat, in_slot=[g * 4 + r for g in range(4) for r in range(3)],
+                                 out_slot=[g * 4 + 3 for g in range(4)])
+    dev = torch.empty((S, 16, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(dev, dev.numel(), 23)
+    host = dev.cpu().numpy().copy()
+    gmap.apply_batch(dev, 16 * B, B, dev, 16 * B, B, S, B)
+    torch.cuda.synchronize()
+    gmap.apply_batch_host(host, 16 * B, B, host, 16 * B, B, S, B)
+    assert (dev.cpu().numpy() == host).all()
