@@ -7,7 +7,9 @@
  *                      8 when every tile has >= 16 entries, else 4), or force 4 / 8
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
- *   "xcd_group"        1 = multi-tile maps keep the tiles of one chunk on one XCD (default 0)
+ *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous
+ *                      eighth of the grid; 2 = each XCD runs whole (stripe, chunk) units, all
+ *                      tiles of a unit back to back (default: see engine.hpp Tuning)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  */

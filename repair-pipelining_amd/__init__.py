@@ -138,6 +138,37 @@ def _host_ptr(x) -> int:
     raise TypeError("expected a host array/tensor or an integer pointer")
 
 
+def _avail_bytes(x) -> Optional[int]:
+    """Bytes addressable from the buffer's first byte to the end of its allocation:
+    torch tensors use their storage, numpy arrays their outermost base array.
+    None for raw integer pointers (the caller vouches for those)."""
+    if isinstance(x, int):
+        return None
+    if isinstance(x, np.ndarray):
+        base = x
+        while isinstance(base.base, np.ndarray):
+            base = base.base
+        hi = base.ctypes.data + base.nbytes if base.flags.c_contiguous else None
+        return None if hi is None else hi - x.ctypes.data
+    if hasattr(x, "untyped_storage"):
+        st = x.untyped_storage()
+        return st.data_ptr() + st.nbytes() - x.data_ptr()
+    return None
+
+
+def _check_layout(buf, stripe_stride, slot_stride, max_slot, nstripes, nbytes, what):
+    """Fail loudly (ArrayIndexOutOfBoundsException, as a Java ByteBuffer would)
+    instead of letting a kernel address past the end of `buf`."""
+    if nstripes <= 0 or nbytes <= 0:
+        return
+    if stripe_stride < 0 or slot_stride < 0:
+        raise EcxError(-1, f"{what}: negative stride")
+    avail = _avail_bytes(buf)
+    need = (nstripes - 1) * stripe_stride + max(0, max_slot) * slot_stride + nbytes
+    if avail is not None and need > avail:
+        raise EcxError(-5, f"{what}: the batch layout addresses {need} bytes but the buffer holds {avail}")
+
+
 class HostBuffer:
     """Page-locked host memory from ecx_host_alloc, viewed as a numpy uint8 array."""
 
@@ -321,6 +352,8 @@ class GfMap:
     def accumulate_batch(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride,
                          nstripes, byte_count, stream=None):
         """out ^= M * in (partial sums)."""
+        self._check(inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                    byte_count)
         check(lib().ecx_map_accumulate_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_slot_stride,
                                              _dev_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
                                              byte_count, _stream(stream)))
@@ -334,14 +367,30 @@ class GfMap:
         check(lib().ecx_map_matrix(self._h, m.ctypes.data, ins.ctypes.data, outs.ctypes.data))
         return m, ins[:inf["n_in"]].copy(), outs[:inf["n_out"]].copy()
 
+    def max_slots(self):
+        """(largest input slot, largest output slot) of the map (cached)."""
+        if getattr(self, "_max_slots", None) is None:
+            _, ins, outs = self.matrix()
+            self._max_slots = (int(ins.max()) if len(ins) else 0, int(outs.max()) if len(outs) else 0)
+        return self._max_slots
+
+    def _check(self, inp, iss, isl, out, oss, osl, nstripes, nbytes):
+        mi, mo = self.max_slots()
+        _check_layout(inp, iss, isl, mi, nstripes, nbytes, "input")
+        _check_layout(out, oss, osl, mo, nstripes, nbytes, "output")
+
     def apply_batch(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
                     byte_count, stream=None):
+        self._check(inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                    byte_count)
         check(lib().ecx_map_apply_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_slot_stride, _dev_ptr(out),
                                         out_stripe_stride, out_slot_stride, nstripes, byte_count, _stream(stream)))
 
     def apply_batch_host(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride,
                          nstripes, byte_count):
         """apply_batch over host buffers: pipelined H2D -> kernel -> D2H, synchronous."""
+        self._check(inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                    byte_count)
         check(lib().ecx_map_apply_batch_host(self._h, _host_ptr(inp), in_stripe_stride, in_slot_stride,
                                              _host_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
                                              byte_count))
@@ -422,6 +471,8 @@ class ReedSolomon:
                            acc_row_stride, nstripes, byteCount, isFirst, stream=None):
         """Batched decodeMissingSingle for every missing shard (data and parity)."""
         pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        _check_layout(inp, in_stripe_stride, 0, 0, nstripes, byteCount, "input")
+        _check_layout(acc, acc_stripe_stride, acc_row_stride, int((pres == 0).sum()) - 1, nstripes, byteCount, "acc")
         check(lib().ecx_rs_decode_partial_batch(self._h, pres.ctypes.data, shardIndex, _dev_ptr(inp),
                                                 in_stripe_stride, _dev_ptr(acc), acc_stripe_stride, acc_row_stride,
                                                 nstripes, byteCount, 1 if isFirst else 0, _stream(stream)))
@@ -429,6 +480,8 @@ class ReedSolomon:
     def encodePartialBatch(self, inputIndex, inp, in_stripe_stride, acc, acc_stripe_stride, acc_row_stride,
                            nstripes, byteCount, isFirst, stream=None):
         """Batched encodeParitySingle into every parity row."""
+        _check_layout(inp, in_stripe_stride, 0, 0, nstripes, byteCount, "input")
+        _check_layout(acc, acc_stripe_stride, acc_row_stride, self.parityShardCount - 1, nstripes, byteCount, "acc")
         check(lib().ecx_rs_encode_partial_batch(self._h, inputIndex, _dev_ptr(inp), in_stripe_stride,
                                                 _dev_ptr(acc), acc_stripe_stride, acc_row_stride, nstripes,
                                                 byteCount, 1 if isFirst else 0, _stream(stream)))
@@ -547,8 +600,17 @@ class ClayCodeErasureDecodingStep:
         check(lib().ecx_clay_map(self._h, ctypes.byref(h)))
         return GfMap(h, owner=self)
 
+    def _check_batch(self, inp, iss, isl, out, oss, osl, nstripes, nbytes):
+        if not self.erasedIndexes:
+            return
+        if getattr(self, "_map", None) is None:
+            self._map = self.map()
+        self._map._check(inp, iss, isl, out, oss, osl, nstripes, nbytes)
+
     def performCodingBatch(self, inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
                            nstripes, bufSize, stream=None) -> None:
+        self._check_batch(inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
+                          bufSize)
         check(lib().ecx_clay_perform_coding_batch(self._h, _dev_ptr(inp), in_stripe_stride, in_sub_stride,
                                                   _dev_ptr(out), out_stripe_stride, out_sub_stride, nstripes,
                                                   bufSize, _stream(stream)))
@@ -556,6 +618,8 @@ class ClayCodeErasureDecodingStep:
     def performCodingBatchHost(self, inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
                                nstripes, bufSize) -> None:
         """performCodingBatch over host-memory stripes (ecx_clay_perform_coding_batch_host)."""
+        self._check_batch(inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
+                          bufSize)
         check(lib().ecx_clay_perform_coding_batch_host(self._h, _host_ptr(inp), in_stripe_stride, in_sub_stride,
                                                        _host_ptr(out), out_stripe_stride, out_sub_stride, nstripes,
                                                        bufSize))

@@ -116,16 +116,26 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
     }
 }
 
-// Logical work index of this workgroup.  Multi-tile maps re-read inputs across
-// the tiles of one (stripe, chunk); with `xcd_group` the tiles of a chunk are
-// given consecutive workgroups of ONE XCD (blocks b and b+8 share an XCD under
-// the observed round-robin dispatch; a speed choice only) so the re-reads are
-// served by that XCD's L2.  Bijective for any grid size.
-__device__ __forceinline__ uint32_t logical_block(bool xcd_group) {
+// Logical work index of this workgroup (blocks b and b+8 share an XCD under the
+// round-robin dispatch of MI355X; a speed choice only, every mapping is a bijection).
+// Multi-tile maps re-read inputs across the tiles of one (stripe, chunk) unit:
+//   xcd_group 0: identity -- the T tiles of a unit are spread over all 8 XCDs;
+//   xcd_group 1: XCD x runs the contiguous x-th eighth of the grid;
+//   xcd_group 2: XCD x runs whole units x, x+8, x+16, ..., each unit's T tiles
+//                back to back, so a unit's re-reads meet in one XCD's L2 while
+//                all XCDs stream neighbouring units.  Units past the last full
+//                group of 8 keep the identity mapping.
+__device__ __forceinline__ uint32_t logical_block(int xcd_group, uint32_t n_tiles) {
     const uint32_t b = blockIdx.x;
-    if (!xcd_group) return b;
-    const uint32_t g = gridDim.x, q = g / 8, r = g % 8, xcd = b % 8, j = b / 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    if (xcd_group == 0) return b;
+    const uint32_t g = gridDim.x, xcd = b % 8, j = b / 8;
+    if (xcd_group == 1) {
+        const uint32_t q = g / 8, r = g % 8;
+        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const uint32_t full = (g / (8 * n_tiles)) * (8 * n_tiles);
+    if (b >= full) return b;
+    return ((j / n_tiles) * 8 + xcd) * n_tiles + (j % n_tiles);
 }
 
 // NTL / NTS: non-temporal loads / stores.  Outputs are never re-read, so stores
@@ -134,7 +144,7 @@ __device__ __forceinline__ uint32_t logical_block(bool xcd_group) {
 template <bool SAFE, bool NTL, bool NTS, int DEPTH>
 __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
     constexpr int THREADS = kBlockThreads;
-    const uint32_t w = logical_block(a.xcd_group != 0);
+    const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
     const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
@@ -221,7 +231,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.out_slot_stride = out_slot_stride;
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
-    a.xcd_group = (tuning().xcd_group && a.n_tiles > 1) ? 1 : 0;
+    a.xcd_group = a.n_tiles > 1 ? tuning().xcd_group : 0;
     a.accumulate = accumulate ? 1 : 0;
 
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {

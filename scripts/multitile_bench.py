@@ -1,0 +1,80 @@
+"""Multi-tile maps (inputs re-read across the tiles of a (stripe, chunk) unit):
+block-order A/B over ecx_tune("xcd_group", 0|1|2), interleaved rounds in one
+process, median GB/s (algorithmic bytes).
+
+    python scripts/multitile_bench.py                 # all configs x all modes
+    python scripts/multitile_bench.py --only clay104 --xcd 2 --reps 20   # one shape (for --pmc runs)
+"""
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import rpamd  # noqa: E402
+
+
+def cases(ecx, torch, only):
+    out = []
+    if only in (None, "clay104"):
+        k, m, v, B, S = 10, 4, 2, 4096, 2048
+        n, a = 14, 256
+        pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(pool, pool.numel(), 3)
+        o = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
+        step = ecx.ClayCodeErasureDecodingStep([3], k, m, virtualUnits=v)
+        inf = step.map().info()
+        out.append(("clay104 repair e=3, 4 KiB sub-chunks", (inf["n_in"] + inf["n_out"]) * B * S,
+                    lambda pool=pool, o=o, step=step, n=n, a=a, B=B, S=S:
+                    step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B), (pool, o, step)))
+    if only in (None, "clay42enc"):
+        B, P = 32768, 1 << 13
+        pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(pool, pool.numel(), 1)
+        par = torch.empty((P, 16, B), dtype=torch.uint8, device="cuda")
+        enc = ecx.ClayCodeErasureDecodingStep([4, 5], 4, 2)
+        out.append(("clay42 encode, 32 KiB", 48 * B * P,
+                    lambda pool=pool, par=par, enc=enc, B=B, P=P:
+                    enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B), (pool, par, enc)))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--xcd", type=int, default=None)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    ecx = rpamd.load()
+    lib = ecx.lib()
+    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    modes = [args.xcd] if args.xcd is not None else [0, 1, 2]
+    cs = cases(ecx, torch, args.only)
+    res = {(c[0], x): [] for c in cs for x in modes}
+    for _ in range(args.rounds):
+        for name, nbytes, fn, _keep in cs:
+            for x in modes:
+                lib.ecx_tune(b"xcd_group", x)
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                res[(name, x)].append(nbytes / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
+    lib.ecx_tune(b"xcd_group", 0)
+    for (name, x), v in res.items():
+        med = statistics.median(v)
+        print(json.dumps({"case": name, "xcd_group": x, "GBps_median": round(med, 1),
+                          "frac": round(med / 8000, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

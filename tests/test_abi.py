@@ -89,3 +89,33 @@ def test_host_planner_errors(ecx):
     with pytest.raises(ecx.EcxError) as e:
         step.getHelperPlanesIndexes(13)
     assert e.value.code == -5
+
+
+def test_batch_layout_checked_before_any_device_work(ecx):
+    """A batch layout that addresses past the end of its buffer fails loudly
+    (ArrayIndexOutOfBoundsException) instead of reaching a kernel."""
+    import numpy as np
+    import torch
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    B, S = 512, 3
+    inp, out = np.zeros((S, 48, B), np.uint8), np.zeros((S, 8, B), np.uint8)
+    with pytest.raises(ecx.EcxError) as e:
+        step.performCodingBatchHost(inp, 48 * B, B, out, 8 * B, B, S + 1, B)  # one stripe too many
+    assert e.value.code == -5
+    with pytest.raises(ecx.EcxError) as e:
+        step.performCodingBatchHost(inp[1:], 48 * B, B, out, 8 * B, B, S, B)  # view: less room left
+    assert e.value.code == -5
+    with pytest.raises(ecx.EcxError) as e:
+        step.performCodingBatchHost(inp, 48 * B, B, out, 8 * B, 2 * B, S, B)  # output slot stride too wide
+    assert e.value.code == -5
+    t_in = torch.zeros((S, 48, B), dtype=torch.uint8)
+    mat, ins, outs = step.map().matrix()
+    gm = ecx.GfMap.from_matrix(mat, in_slot=ins, out_slot=outs)
+    assert gm.max_slots() == (int(ins.max()), int(outs.max()))
+    with pytest.raises(ecx.EcxError) as e:
+        gm.apply_batch_host(t_in[:, :40], 48 * B, B, out, 8 * B, B, S, B + 1)
+    assert e.value.code == -5
+    if not _has_device(ecx):  # a valid layout gets as far as the (absent) device
+        with pytest.raises(ecx.EcxError) as e:
+            gm.apply_batch_host(t_in, 48 * B, B, out, 8 * B, B, S, B)
+        assert e.value.code == -10
