@@ -10,6 +10,8 @@
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous
  *                      eighth of the grid; 2 = each XCD runs whole (stripe, chunk) units, all
  *                      tiles of a unit back to back (default: see engine.hpp Tuning)
+ *   "wave_groups"      multi-tile maps: 1 = one workgroup per group of tiles sharing inputs, one
+ *                      wave per tile, entry lists aligned (default); 0 = one workgroup per tile
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  */

@@ -83,24 +83,128 @@ std::vector<int> group_rows(const LinearMap &m) {
     return order;
 }
 
+// Group tiles that share inputs into workgroups of up to kWaveGroup tiles (one
+// wave each, k_gf_apply_waves): seed with the lowest unassigned tile, then add
+// the unassigned tile sharing the most inputs with the group (ties: lowest index).
+// Clay(10,4) repair: the 32 tiles form 4 groups of 8 in which every pair shares
+// 4 inputs -- each group reads its 208 distinct inputs, 832 in all.
+std::vector<std::vector<int>> group_tiles(const std::vector<std::vector<int>> &cols, int n_in) {
+    const int n = (int)cols.size();
+    std::vector<std::vector<int>> groups;
+    std::vector<char> used(n, 0), in_group(n_in, 0);
+    for (int seed = 0; seed < n; ++seed) {
+        if (used[seed]) continue;
+        std::vector<int> g = {seed};
+        used[seed] = 1;
+        std::fill(in_group.begin(), in_group.end(), 0);
+        for (int j : cols[seed]) in_group[j] = 1;
+        while ((int)g.size() < kWaveGroup) {
+            int best = -1, best_shared = -1;
+            for (int t = 0; t < n; ++t) {
+                if (used[t]) continue;
+                int shared = 0;
+                for (int j : cols[t]) shared += in_group[j];
+                if (shared > best_shared) {
+                    best = t;
+                    best_shared = shared;
+                }
+            }
+            if (best < 0 || best_shared == 0) break;
+            used[best] = 1;
+            g.push_back(best);
+            for (int j : cols[best]) in_group[j] = 1;
+        }
+        groups.push_back(g);
+    }
+    return groups;
+}
+
+// Order each tile's inputs so that an input shared by several tiles of a group
+// sits at the same position in all of them: the waves of a workgroup then load
+// it at about the same time, and the second load is served by the CU's L1 / the
+// XCD's L2 instead of HBM.  Greedy list scheduling: shared inputs first (most
+// sharers first), each into the earliest slot free in every tile that uses it;
+// private inputs fill the remaining holes.  Positions stay aligned wherever the
+// holes are filled exactly, which the regular Clay structure allows.
+void align_group(const std::vector<int> &group, std::vector<std::vector<int>> &cols) {
+    std::map<int, std::vector<int>> users;  // input column -> tiles of the group using it
+    for (int t : group)
+        for (int j : cols[t]) users[j].push_back(t);
+    std::vector<std::pair<int, int>> order;  // (-#users, column)
+    for (auto &kv : users) order.push_back({-(int)kv.second.size(), kv.first});
+    std::sort(order.begin(), order.end());
+    std::map<int, std::vector<char>> busy;  // tile -> slot occupancy
+    std::map<int, std::vector<std::pair<int, int>>> placed;  // tile -> (slot, column)
+    for (auto &oc : order) {
+        const int j = oc.second;
+        const std::vector<int> &ts = users[j];
+        for (int slot = 0;; ++slot) {
+            bool free = true;
+            for (int t : ts) {
+                std::vector<char> &b = busy[t];
+                if ((int)b.size() > slot && b[slot]) {
+                    free = false;
+                    break;
+                }
+            }
+            if (!free) continue;
+            for (int t : ts) {
+                std::vector<char> &b = busy[t];
+                if ((int)b.size() <= slot) b.resize(slot + 1, 0);
+                b[slot] = 1;
+                placed[t].push_back({slot, j});
+            }
+            break;
+        }
+    }
+    for (int t : group) {
+        std::vector<std::pair<int, int>> &p = placed[t];
+        std::sort(p.begin(), p.end());
+        cols[t].clear();
+        for (auto &sj : p) cols[t].push_back(sj.second);
+    }
+}
+
 }  // namespace
 
 CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
     for (int s : map_.in_slot) max_in_slot_ = std::max(max_in_slot_, s);
     for (int s : map_.out_slot) max_out_slot_ = std::max(max_out_slot_, s);
     const std::vector<int> order = group_rows(map_);
+    // Tiles of kTileRows output rows and the input columns each one reads.
+    std::vector<std::vector<int>> cols;
     for (int r0 = 0; r0 < map_.n_out; r0 += kTileRows) {
         const int rows = std::min(kTileRows, map_.n_out - r0);
-        const uint32_t begin = (uint32_t)(entries_.size() / kEntryDwords);
-        uint32_t count = 0;
+        std::vector<int> c;
         for (int j = 0; j < map_.n_in; ++j) {
+            bool any = false;
+            for (int r = 0; r < rows; ++r) any |= map_.at(order[r0 + r], j) != 0;
+            if (any) c.push_back(j);
+        }
+        cols.push_back(c);
+    }
+    n_tiles_ = (int)cols.size();
+    if (n_tiles_ > 1) {
+        for (const std::vector<int> &g : group_tiles(cols, map_.n_in)) {
+            align_group(g, cols);
+            uint32_t rec[kWaveGroup];
+            for (int w = 0; w < kWaveGroup; ++w) rec[w] = w < (int)g.size() ? (uint32_t)g[w] : kNoTile;
+            groups_.insert(groups_.end(), rec, rec + kWaveGroup);
+            group_size_ = std::max(group_size_, (int)g.size());
+            ++n_groups_;
+        }
+    }
+    for (int t = 0; t < n_tiles_; ++t) {
+        const int r0 = t * kTileRows;
+        const int rows = std::min(kTileRows, map_.n_out - r0);
+        const uint32_t begin = (uint32_t)(entries_.size() / kEntryDwords);
+        for (int j : cols[t]) {
             uint32_t mmul = 0, mone = 0;
             for (int r = 0; r < rows; ++r) {
                 const uint8_t c = map_.at(order[r0 + r], j);
                 if (c == 1) mone |= 1u << r;
                 else if (c) mmul |= 1u << r;
             }
-            if (!(mmul | mone)) continue;
             uint32_t rec[kEntryDwords] = {0};
             rec[0] = (uint32_t)map_.in_slot[j];
             rec[1] = mmul;
@@ -108,18 +212,17 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
             for (int r = 0; r < rows; ++r)
                 if (mmul & (1u << r)) split_tables(map_.at(order[r0 + r], j), rec + 4 + 5 * r);
             entries_.insert(entries_.end(), rec, rec + kEntryDwords);
-            ++count;
         }
         uint32_t tile[kTileDwords] = {0};
         tile[0] = begin;
-        tile[1] = count;
+        tile[1] = (uint32_t)cols[t].size();
         tile[2] = (uint32_t)rows;
         for (int r = 0; r < rows; ++r) tile[4 + r] = (uint32_t)map_.out_slot[order[r0 + r]];
         tiles_.insert(tiles_.end(), tile, tile + kTileDwords);
-        ++n_tiles_;
     }
     if (tiles_.empty()) tiles_.assign(kTileDwords, 0);
     if (entries_.empty()) entries_.assign(kEntryDwords, 0);
+    if (groups_.empty()) groups_.assign(kWaveGroup, kNoTile);
     int min_count = 1 << 30;
     for (int t = 0; t < n_tiles_; ++t) {
         const int c = (int)tiles_[(size_t)t * kTileDwords + 1];
@@ -149,6 +252,7 @@ CompiledMap::~CompiledMap() {
         (void)hipSetDevice(kv.first.first);
         (void)hipFree(kv.second.entries);
         (void)hipFree(kv.second.tiles);
+        (void)hipFree(kv.second.groups);
         (void)hipSetDevice(cur);
     }
 }
@@ -180,6 +284,8 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     DevicePlan p;
     check_hip(hipMalloc(&p.entries, ents.size() * 4), "hipMalloc(plan entries)");
     check_hip(hipMalloc(&p.tiles, tiles.size() * 4), "hipMalloc(plan tiles)");
+    check_hip(hipMalloc(&p.groups, groups_.size() * 4), "hipMalloc(plan groups)");
+    check_hip(hipMemcpy(p.groups, groups_.data(), groups_.size() * 4, hipMemcpyHostToDevice), "plan upload");
     check_hip(hipMemcpy(p.entries, ents.data(), ents.size() * 4, hipMemcpyHostToDevice), "plan upload");
     check_hip(hipMemcpy(p.tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice), "plan upload");
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;

@@ -138,33 +138,30 @@ __device__ __forceinline__ uint32_t logical_block(int xcd_group, uint32_t n_tile
     return ((j / n_tiles) * 8 + xcd) * n_tiles + (j % n_tiles);
 }
 
+// One output tile over the workgroup's (or wave's) lanes x 16 bytes of one stripe.
+// `ib` / `ob` point at this lane's 16 bytes of slot 0; `zoff` is this lane's offset
+// into the zero page (recomputed at each padding load rather than kept live).
 // NTL / NTS: non-temporal loads / stores.  Outputs are never re-read, so stores
 // are always streamed; loads are streamed only when the map has one tile (no
 // input is read twice), otherwise the re-reads of other tiles hit the caches.
-template <bool SAFE, bool NTL, bool NTS, int DEPTH>
-__global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
-    constexpr int THREADS = kBlockThreads;
-    const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
-    const uint32_t tl = w % (uint32_t)a.n_tiles;
-    const uint32_t rest = w / (uint32_t)a.n_tiles;
-    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
-    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+// Wave-uniform 64-bit value into SGPRs (the block-index arithmetic goes through
+// VALU division; keeping the bases scalar frees VGPRs for the load ring).
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 
-    cu32 *tile = plan_ptr(a.tiles) + tl * kTileDwords;
+template <bool SAFE, bool NTL, bool NTS, int DEPTH>
+__device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint64_t in_base, uint64_t out_base,
+                                           uint32_t lane16, int valid) {
+    const uint8_t *ib = reinterpret_cast<const uint8_t *>(in_base) + lane16;
+    const uint32_t zoff = lane16;
     const int ebeg = (int)tile[0];
     const int ecnt = (int)tile[1];
     const int nrows = (int)tile[2];
-
-    const int64_t off = c * (THREADS * 16) + (int64_t)threadIdx.x * 16;
-    const uint8_t *ib = a.in + s * a.in_stripe_stride + off;
-    uint8_t *ob = a.out + s * a.out_stripe_stride + off;
-    int valid = 16;
-    if (SAFE) {
-        const int64_t v = a.nbytes - off;
-        valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
-    }
     auto load = [&](uint32_t slot) -> u32x4 {  // padding entries read the zero page
-        const uint8_t *p = slot == kDummySlot ? a.zero_page + threadIdx.x * 16 : ib + (int64_t)slot * a.in_slot_stride;
+        const uint8_t *p = slot == kDummySlot ? a.zero_page + zoff : ib + (int64_t)slot * a.in_slot_stride;
         return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
     };
 
@@ -197,13 +194,61 @@ __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(
 #pragma unroll
     for (int o = 0; o < kTileRows; ++o) {
         if (o < nrows) {
-            uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
+            uint8_t *p = reinterpret_cast<uint8_t *>(out_base) + lane16 + (int64_t)tile[4 + o] * a.out_slot_stride;
             u32x4 v = acc[o];
             if (a.accumulate) v ^= SAFE ? load_partial(p, valid) : load16(p);  // wave-uniform branch
             if (SAFE) store_partial(p, v, valid);
             else st16<NTS>(p, v);
         }
     }
+}
+
+// One workgroup = one (stripe, 4 KiB chunk, output tile); single-tile maps.
+template <bool SAFE, bool NTL, bool NTS, int DEPTH>
+__global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
+    constexpr int THREADS = kBlockThreads;
+    const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
+    const uint32_t tl = w % (uint32_t)a.n_tiles;
+    const uint32_t rest = w / (uint32_t)a.n_tiles;
+    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
+    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+    const int64_t cbase = c * (THREADS * 16);
+    int valid = 16;
+    if (SAFE) {
+        const int64_t v = a.nbytes - cbase - (int64_t)threadIdx.x * 16;
+        valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
+    }
+    apply_tile<SAFE, NTL, NTS, DEPTH>(a, plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords,
+                                      uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
+                                      uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)),
+                                      threadIdx.x * 16, valid);
+}
+
+// Multi-tile maps: one workgroup = one (stripe, 1 KiB chunk, tile GROUP), one
+// wave per tile of the group.  The group's tiles share inputs and their entry
+// lists are aligned (engine.cpp align_group), so the waves of one CU load a
+// shared input at about the same time and HBM serves it once.
+template <bool SAFE, int DEPTH>
+__global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_apply_waves(ApplyArgs a) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t b = blockIdx.x;
+    const uint32_t g = b % (uint32_t)a.n_groups;
+    const uint32_t rest = b / (uint32_t)a.n_groups;
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(plan_ptr(a.groups)[g * kWaveGroup + wave]);
+    if (tl == kNoTile) return;  // wave-uniform: an idle wave of a smaller group
+    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
+    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+    const int64_t cbase = c * kWaveChunkBytes;
+    int valid = 16;
+    if (SAFE) {
+        const int64_t v = a.nbytes - cbase - (int64_t)lane * 16;
+        valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
+    }
+    apply_tile<SAFE, false, true, DEPTH>(a, plan_ptr(a.tiles) + tl * kTileDwords,
+                                         uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
+                                         uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)), lane * 16,
+                                         valid);
 }
 
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
@@ -215,15 +260,20 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
     const Tuning &tu = tuning();
-    const int64_t chunk = kChunkBytes;
-    const int64_t full = aligned ? nbytes / chunk : 0;  // in units of `chunk`
-    const int64_t tail_chunks = (nbytes - full * chunk + kChunkBytes - 1) / kChunkBytes;  // 4 KiB units
+    // Multi-tile maps run as tile groups (one wave per tile, 1 KiB chunks); single-tile
+    // maps as one 256-lane workgroup per 4 KiB chunk.
+    const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
+    const int64_t chunk = waves ? kWaveChunkBytes : kChunkBytes;
+    const int64_t full = aligned ? nbytes / chunk : 0;               // in units of `chunk`
+    const int64_t tail_chunks = (nbytes - full * chunk + chunk - 1) / chunk;
 
     ApplyArgs a;
     a.in = in;
     a.out = out;
     a.entries = plan.entries;
     a.tiles = plan.tiles;
+    a.groups = plan.groups;
+    a.n_groups = cm.n_groups();
     a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;
     a.in_slot_stride = in_slot_stride;
@@ -238,13 +288,20 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
         a.n_chunks = n_chunks;
-        const int64_t per_stripe = n_chunks * a.n_tiles;
+        const int64_t per_stripe = n_chunks * (waves ? a.n_groups : a.n_tiles);
         const int64_t max_blocks = (int64_t)1 << 30;
         const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / per_stripe);
         for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
             const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
             a.stripe_begin = s0;
             const dim3 grid((unsigned)(ns * per_stripe));
+            if (waves) {
+                const dim3 blk(64 * cm.group_size());
+                if (safe) hipLaunchKernelGGL((k_gf_apply_waves<true, 4>), grid, blk, 0, stream, a);
+                else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_waves<false, 8>), grid, blk, 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply_waves<false, 4>), grid, blk, 0, stream, a);
+                continue;
+            }
             const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (a.n_tiles == 1 ? 2 : 1) : 0);
             const dim3 blk(kBlockThreads);
             if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false, 4>), grid, blk, 0, stream, a);

@@ -1,9 +1,12 @@
 """Multi-tile maps (inputs re-read across the tiles of a (stripe, chunk) unit):
-block-order A/B over ecx_tune("xcd_group", 0|1|2), interleaved rounds in one
-process, median GB/s (algorithmic bytes).
+launch-shape A/B, interleaved rounds in one process, median GB/s (algorithmic
+bytes).  Modes:
+    waves   -- k_gf_apply_waves: one workgroup per group of tiles sharing inputs (default)
+    tiles   -- k_gf_apply: one workgroup per tile, identity block order
+    tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
-    python scripts/multitile_bench.py                 # all configs x all modes
-    python scripts/multitile_bench.py --only clay104 --xcd 2 --reps 20   # one shape (for --pmc runs)
+    python scripts/multitile_bench.py                          # all configs x all modes
+    python scripts/multitile_bench.py --only clay104 --mode tiles --reps 2 --rounds 1   # one shape (PMC runs)
 """
 import argparse
 import ctypes
@@ -42,10 +45,15 @@ def cases(ecx, torch, only):
     return out
 
 
+MODES = {"waves": {"wave_groups": 1, "xcd_group": 0},
+         "tiles": {"wave_groups": 0, "xcd_group": 0},
+         "tiles2": {"wave_groups": 0, "xcd_group": 2}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
-    ap.add_argument("--xcd", type=int, default=None)
+    ap.add_argument("--mode", default=None, choices=list(MODES))
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
@@ -53,13 +61,14 @@ def main():
     ecx = rpamd.load()
     lib = ecx.lib()
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
-    modes = [args.xcd] if args.xcd is not None else [0, 1, 2]
+    modes = [args.mode] if args.mode else list(MODES)
     cs = cases(ecx, torch, args.only)
     res = {(c[0], x): [] for c in cs for x in modes}
     for _ in range(args.rounds):
         for name, nbytes, fn, _keep in cs:
             for x in modes:
-                lib.ecx_tune(b"xcd_group", x)
+                for key, val in MODES[x].items():
+                    lib.ecx_tune(key.encode(), val)
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,10 +78,11 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[(name, x)].append(nbytes / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
-    lib.ecx_tune(b"xcd_group", 0)
+    for key, val in MODES["waves"].items():
+        lib.ecx_tune(key.encode(), val)
     for (name, x), v in res.items():
         med = statistics.median(v)
-        print(json.dumps({"case": name, "xcd_group": x, "GBps_median": round(med, 1),
+        print(json.dumps({"case": name, "mode": x, "GBps_median": round(med, 1),
                           "frac": round(med / 8000, 4)}), flush=True)
 
 

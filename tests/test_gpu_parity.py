@@ -571,3 +571,32 @@ def test_lrc_host_batch_matches_device_batch(ecx, torch_dev):
     torch.cuda.synchronize()
     gmap.apply_batch_host(host, 16 * B, B, host, 16 * B, B, S, B)
     assert (dev.cpu().numpy() == host).all()
+
+
+@pytest.mark.parametrize("k,m,v,erased,B", [(4, 2, 0, [0, 3], 4096 * 2 + 1000), (4, 2, 0, [4, 5], 3 * 1024),
+                                            (10, 4, 2, [3], 4096), (6, 3, 0, [1, 7], 1024 + 16)])
+def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
+    """Multi-tile maps: the tile-group kernel (k_gf_apply_waves, aligned entry lists,
+    1 KiB chunks + byte-safe tail) and the one-workgroup-per-tile kernel give the same
+    bytes, and both match the oracle on a sampled stripe."""
+    torch = torch_dev
+    step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
+    n, a = k + m, step.subPacketSize
+    S = 5
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 31)
+    outs = []
+    for wg in (1, 0):
+        ecx.tune("wave_groups", wg)
+        o = torch.full((S, len(erased) * a, B), 7, dtype=torch.uint8, device="cuda")
+        step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
+        torch.cuda.synchronize()
+        outs.append(o.cpu().numpy())
+    ecx.tune("wave_groups", 1)
+    assert (outs[0] == outs[1]).all()
+    if v == 0:
+        host = pool[S - 1].cpu().numpy()
+        inputs = [None if (i % n) in erased else host[i].copy() for i in range(n * a)]
+        ref = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
+        O.Clay(k, m, erased).perform_coding(inputs, ref, B)
+        assert all((outs[0][S - 1, j] == ref[j]).all() for j in range(len(ref)))
