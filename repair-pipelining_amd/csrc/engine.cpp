@@ -84,7 +84,7 @@ std::vector<int> group_rows(const LinearMap &m) {
 }
 
 // Group tiles that share inputs into workgroups of up to kWaveGroup tiles (one
-// wave each, k_gf_apply_waves): seed with the lowest unassigned tile, then add
+// wave each, k_gf_apply_lds): seed with the lowest unassigned tile, then add
 // the unassigned tile sharing the most inputs with the group (ties: lowest index).
 // Clay(10,4) repair: the 32 tiles form 4 groups of 8 in which every pair shares
 // 4 inputs -- each group reads its 208 distinct inputs, 832 in all.
@@ -119,14 +119,14 @@ std::vector<std::vector<int>> group_tiles(const std::vector<std::vector<int>> &c
     return groups;
 }
 
-// Order each tile's inputs so that an input shared by several tiles of a group
-// sits at the same position in all of them: the waves of a workgroup then load
-// it at about the same time, and the second load is served by the CU's L1 / the
-// XCD's L2 instead of HBM.  Greedy list scheduling: shared inputs first (most
-// sharers first), each into the earliest slot free in every tile that uses it;
-// private inputs fill the remaining holes.  Positions stay aligned wherever the
-// holes are filled exactly, which the regular Clay structure allows.
-void align_group(const std::vector<int> &group, std::vector<std::vector<int>> &cols) {
+// Schedule a group's inputs so that every stage of k_gf_apply_lds (one input per
+// wave, staged through LDS) gives each tile about the same amount of work: greedy
+// list scheduling, shared inputs first (most sharers first), each into the
+// earliest slot free in every tile that uses it; private inputs fill the holes.
+// Returns the group's union of inputs in schedule order (slot, then column): the
+// order in which k_gf_apply_lds stages them through LDS.  Every tile's list is
+// increasing in that order.
+std::vector<int> align_group(const std::vector<int> &group, std::vector<std::vector<int>> &cols) {
     std::map<int, std::vector<int>> users;  // input column -> tiles of the group using it
     for (int t : group)
         for (int j : cols[t]) users[j].push_back(t);
@@ -157,12 +157,22 @@ void align_group(const std::vector<int> &group, std::vector<std::vector<int>> &c
             break;
         }
     }
+    std::map<int, int> slot_of;
     for (int t : group) {
         std::vector<std::pair<int, int>> &p = placed[t];
         std::sort(p.begin(), p.end());
         cols[t].clear();
-        for (auto &sj : p) cols[t].push_back(sj.second);
+        for (auto &sj : p) {
+            cols[t].push_back(sj.second);
+            slot_of[sj.second] = sj.first;
+        }
     }
+    std::vector<std::pair<int, int>> u;
+    for (auto &kv : slot_of) u.push_back({kv.second, kv.first});
+    std::sort(u.begin(), u.end());
+    std::vector<int> uni;
+    for (auto &sj : u) uni.push_back(sj.second);
+    return uni;
 }
 
 }  // namespace
@@ -184,12 +194,20 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         cols.push_back(c);
     }
     n_tiles_ = (int)cols.size();
+    std::vector<int> upos(map_.n_in, 0);  // column -> position in its group's union
     if (n_tiles_ > 1) {
         for (const std::vector<int> &g : group_tiles(cols, map_.n_in)) {
-            align_group(g, cols);
-            uint32_t rec[kWaveGroup];
+            const std::vector<int> uni = align_group(g, cols);
+            uint32_t rec[kGroupDwords];
+            std::fill(rec, rec + kGroupDwords, 0u);
             for (int w = 0; w < kWaveGroup; ++w) rec[w] = w < (int)g.size() ? (uint32_t)g[w] : kNoTile;
-            groups_.insert(groups_.end(), rec, rec + kWaveGroup);
+            rec[8] = (uint32_t)unions_.size();
+            rec[9] = (uint32_t)uni.size();
+            for (size_t u = 0; u < uni.size(); ++u) {
+                upos[uni[u]] = (int)u;
+                unions_.push_back((uint32_t)map_.in_slot[uni[u]]);
+            }
+            groups_.insert(groups_.end(), rec, rec + kGroupDwords);
             group_size_ = std::max(group_size_, (int)g.size());
             ++n_groups_;
         }
@@ -209,6 +227,7 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
             rec[0] = (uint32_t)map_.in_slot[j];
             rec[1] = mmul;
             rec[2] = mone;
+            rec[3] = (uint32_t)upos[j];
             for (int r = 0; r < rows; ++r)
                 if (mmul & (1u << r)) split_tables(map_.at(order[r0 + r], j), rec + 4 + 5 * r);
             entries_.insert(entries_.end(), rec, rec + kEntryDwords);
@@ -217,12 +236,16 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         tile[0] = begin;
         tile[1] = (uint32_t)cols[t].size();
         tile[2] = (uint32_t)rows;
+        tile[3] = (uint32_t)cols[t].size();  // unpadded count (k_gf_apply_lds)
         for (int r = 0; r < rows; ++r) tile[4 + r] = (uint32_t)map_.out_slot[order[r0 + r]];
         tiles_.insert(tiles_.end(), tile, tile + kTileDwords);
     }
     if (tiles_.empty()) tiles_.assign(kTileDwords, 0);
     if (entries_.empty()) entries_.assign(kEntryDwords, 0);
-    if (groups_.empty()) groups_.assign(kWaveGroup, kNoTile);
+    if (groups_.empty()) {
+        groups_.assign(kGroupDwords, 0u);
+        std::fill(groups_.begin(), groups_.begin() + kWaveGroup, kNoTile);
+    }
     int min_count = 1 << 30;
     for (int t = 0; t < n_tiles_; ++t) {
         const int c = (int)tiles_[(size_t)t * kTileDwords + 1];
@@ -253,6 +276,7 @@ CompiledMap::~CompiledMap() {
         (void)hipFree(kv.second.entries);
         (void)hipFree(kv.second.tiles);
         (void)hipFree(kv.second.groups);
+        (void)hipFree(kv.second.unions);
         (void)hipSetDevice(cur);
     }
 }
@@ -284,8 +308,25 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     DevicePlan p;
     check_hip(hipMalloc(&p.entries, ents.size() * 4), "hipMalloc(plan entries)");
     check_hip(hipMalloc(&p.tiles, tiles.size() * 4), "hipMalloc(plan tiles)");
-    check_hip(hipMalloc(&p.groups, groups_.size() * 4), "hipMalloc(plan groups)");
-    check_hip(hipMemcpy(p.groups, groups_.data(), groups_.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    // Unions: each group's list padded with zero-page entries to a multiple of
+    // group_size * depth, i.e. whole stages of the LDS kernel's load ring.
+    std::vector<uint32_t> groups = groups_, unions;
+    const int gsz = std::max(1, group_size_);
+    for (int g = 0; g < n_groups_; ++g) {
+        uint32_t *rec = groups.data() + (size_t)g * kGroupDwords;
+        const uint32_t begin = rec[8], count = rec[9];
+        rec[8] = (uint32_t)unions.size();
+        unions.insert(unions.end(), unions_.begin() + begin, unions_.begin() + begin + count);
+        const uint32_t quantum = (uint32_t)(gsz * depth);
+        const uint32_t padded = (count + quantum - 1) / quantum * quantum;
+        unions.resize(unions.size() + (padded - count), kDummySlot);
+        rec[9] = padded;
+    }
+    if (unions.empty()) unions.assign(1, kDummySlot);
+    check_hip(hipMalloc(&p.groups, groups.size() * 4), "hipMalloc(plan groups)");
+    check_hip(hipMemcpy(p.groups, groups.data(), groups.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    check_hip(hipMalloc(&p.unions, unions.size() * 4), "hipMalloc(plan unions)");
+    check_hip(hipMemcpy(p.unions, unions.data(), unions.size() * 4, hipMemcpyHostToDevice), "plan upload");
     check_hip(hipMemcpy(p.entries, ents.data(), ents.size() * 4, hipMemcpyHostToDevice), "plan upload");
     check_hip(hipMemcpy(p.tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice), "plan upload");
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;

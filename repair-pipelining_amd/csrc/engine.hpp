@@ -33,8 +33,9 @@ constexpr int kEntryDwords = 48;
 constexpr int kTileDwords = 16;
 constexpr int kChunkBytes = 4096;  // one 256-thread workgroup x 16 bytes per lane
 constexpr int kBlockThreads = 256;
-constexpr int kWaveGroup = 8;       // k_gf_apply_waves: up to 8 tiles (one wave each) per workgroup
-constexpr int kWaveChunkBytes = 1024;  // k_gf_apply_waves: 64 lanes x 16 bytes per wave
+constexpr int kWaveGroup = 8;       // k_gf_apply_lds: up to 8 tiles (one wave each) per workgroup
+constexpr int kGroupDwords = 16;    // group: [0..7] tiles (kNoTile = none), [8] union begin, [9] union count
+constexpr int kWaveChunkBytes = 1024;  // k_gf_apply_lds: 64 lanes x 16 bytes per wave
 constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 
 void check_hip(hipError_t e, const char *what);
@@ -44,7 +45,8 @@ constexpr uint32_t kDummySlot = 0xFFFFFFFFu;  // entry padding: loads the device
 struct DevicePlan {
     uint32_t *entries = nullptr;
     uint32_t *tiles = nullptr;
-    uint32_t *groups = nullptr;  // n_groups x kWaveGroup tile ids (kNoTile = idle wave)
+    uint32_t *groups = nullptr;  // n_groups x kGroupDwords
+    uint32_t *unions = nullptr;  // per group: input slots in staging order, padded (kDummySlot)
 };
 
 // 4 KiB of zeros per device, never written: the load target of padding entries
@@ -82,7 +84,7 @@ private:
     std::unique_ptr<CompiledMap> compact_;
     std::vector<int> used_in_, used_out_;
     std::vector<uint32_t> entries_, tiles_;  // unpadded
-    std::vector<uint32_t> groups_;
+    std::vector<uint32_t> groups_, unions_;  // unpadded unions
     int n_groups_ = 0, group_size_ = 0;
     int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1, preferred_depth_ = 4;
     std::mutex mu_;
@@ -95,11 +97,12 @@ struct ApplyArgs {
     const uint32_t *entries;
     const uint32_t *tiles;
     const uint32_t *groups;
+    const uint32_t *unions;
     const uint8_t *zero_page;
     int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
     int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
     int n_tiles;
-    int n_groups;         // k_gf_apply_waves: tile groups (workgroups per chunk)
+    int n_groups;         // k_gf_apply_lds: tile groups (workgroups per chunk)
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
 };
@@ -110,7 +113,7 @@ struct Tuning {
     int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or 4 / 8
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
-    int wave_groups = 1;      // multi-tile maps: 1 = k_gf_apply_waves (tile groups per workgroup)
+    int wave_groups = 1;      // multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS)
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
 };

@@ -32,26 +32,33 @@ __device__ __forceinline__ cu32 *plan_ptr(const uint32_t *p) { return (cu32 *)p;
 
 __host__ __device__ __forceinline__ bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
-__device__ __forceinline__ u32x4 load16(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+// Global-memory accesses go through address_space(1) pointers so they compile to
+// global_load / global_store: a flat access also counts in lgkmcnt and may alias
+// LDS, which would force full waits at every scalar-load or LDS wait.
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+typedef __attribute__((address_space(1))) uint8_t gu8;
 
-__device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+__device__ __forceinline__ u32x4 load16(const uint8_t *p) { return *(const gu32x4 *)p; }
+
+__device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { *(gu32x4 *)p = v; }
 
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
-    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-    return *reinterpret_cast<const u32x4 *>(p);
+    if (NT) return __builtin_nontemporal_load((const gu32x4 *)p);
+    return *(const gu32x4 *)p;
 }
 
 template <bool NT>
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
-    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
-    else *reinterpret_cast<u32x4 *>(p) = v;
+    if (NT) __builtin_nontemporal_store(v, (gu32x4 *)p);
+    else *(gu32x4 *)p = v;
 }
 
 // Byte-granular versions for the ragged tail / unaligned layouts.
 __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, int valid) {
+    const gu8 *q = (const gu8 *)p;
     uint32_t w[4] = {0, 0, 0, 0};
-    for (int b = 0; b < valid; ++b) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
+    for (int b = 0; b < valid; ++b) w[b >> 2] |= (uint32_t)q[b] << (8 * (b & 3));
     u32x4 r;
     r.x = w[0];
     r.y = w[1];
@@ -61,8 +68,9 @@ __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, int valid) {
 }
 
 __device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, int valid) {
+    gu8 *q = (gu8 *)p;
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    for (int b = 0; b < valid; ++b) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+    for (int b = 0; b < valid; ++b) q[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
 }
 
 // c*b for four packed bytes: three 8-entry lookups (v_perm_b32 selects bytes
@@ -225,30 +233,101 @@ __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(
 }
 
 // Multi-tile maps: one workgroup = one (stripe, 1 KiB chunk, tile GROUP), one
-// wave per tile of the group.  The group's tiles share inputs and their entry
-// lists are aligned (engine.cpp align_group), so the waves of one CU load a
-// shared input at about the same time and HBM serves it once.
+// wave per tile.  The tiles of a group share inputs (Clay(10,4): 8 tiles read
+// 208 distinct inputs 320 times), so instead of each wave loading its own
+// inputs, the group's union of inputs streams through LDS exactly once:
+//
+//   stage k: wave w stores union[k*G + w] (held in its load ring) to LDS buffer
+//            k&1 and refills the ring DEPTH stages ahead; barrier; every wave
+//            applies the entries of its tile whose union position falls in
+//            stage k, reading the 1 KiB rows from LDS.
+//
+// Two LDS buffers make one barrier per stage enough: buffer k&1 is rewritten at
+// stage k+2, after every wave has passed the barrier of stage k+1.  HBM reads
+// are the algorithmic bytes (1.0x instead of the re-read factor); the union is
+// padded with zero-page entries to whole ring groups so refills are branch-free.
 template <bool SAFE, int DEPTH>
-__global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_apply_waves(ApplyArgs a) {
+__global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_apply_lds(ApplyArgs a) {
+    __shared__ u32x4 stage[2][kWaveGroup][64];  // 16 KiB
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t G = blockDim.x >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t g = b % (uint32_t)a.n_groups;
     const uint32_t rest = b / (uint32_t)a.n_groups;
-    const uint32_t tl = __builtin_amdgcn_readfirstlane(plan_ptr(a.groups)[g * kWaveGroup + wave]);
-    if (tl == kNoTile) return;  // wave-uniform: an idle wave of a smaller group
+    cu32 *grp = plan_ptr(a.groups) + g * kGroupDwords;
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(grp[wave]);
+    const int nst = (int)(grp[9] / G);  // stages; a multiple of DEPTH
+    cu32 *uni = plan_ptr(a.unions) + grp[8];
     const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
     const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
     const int64_t cbase = c * kWaveChunkBytes;
+    const uint32_t lane16 = lane * 16;
     int valid = 16;
     if (SAFE) {
-        const int64_t v = a.nbytes - cbase - (int64_t)lane * 16;
+        const int64_t v = a.nbytes - cbase - (int64_t)lane16;
         valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
     }
-    apply_tile<SAFE, false, true, DEPTH>(a, plan_ptr(a.tiles) + tl * kTileDwords,
-                                         uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
-                                         uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)), lane * 16,
-                                         valid);
+    const uint8_t *ib = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase))) + lane16;
+    auto load = [&](uint32_t slot) -> u32x4 {
+        const uint8_t *p = slot == kDummySlot ? a.zero_page + lane16 : ib + (int64_t)slot * a.in_slot_stride;
+        return SAFE ? load_partial(p, valid) : ld16<true>(p);  // each union input is read once: stream it
+    };
+
+    const bool active = tl != kNoTile;
+    cu32 *tile = plan_ptr(a.tiles) + (active ? tl : 0u) * kTileDwords;
+    const int ecnt = active ? (int)tile[3] : 0;
+    cu32 *ent = plan_ptr(a.entries) + (int64_t)tile[0] * kEntryDwords;
+    int e = 0;
+    uint32_t next_pos = ecnt > 0 ? ent[3] : 0xFFFFFFFFu;
+
+    u32x4 acc[kTileRows];
+#pragma unroll
+    for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
+
+    auto consume = [&](int k, int buf) {  // entries of this tile staged at stage k
+        const uint32_t hi = (uint32_t)(k + 1) * G;
+        while (next_pos < hi) {
+            cu32 *r = ent + (int64_t)e * kEntryDwords;
+            apply_entry(r, stage[buf][next_pos - (uint32_t)k * G][lane], acc);
+            ++e;
+            next_pos = e < ecnt ? r[kEntryDwords + 3] : 0xFFFFFFFFu;
+        }
+    };
+
+    u32x4 ring[DEPTH];
+#pragma unroll
+    for (int u = 0; u < DEPTH; ++u) ring[u] = load(uni[u * G + wave]);
+    const int last = nst - DEPTH;
+    for (int k0 = 0; k0 < last; k0 += DEPTH) {
+#pragma unroll
+        for (int u = 0; u < DEPTH; ++u) {
+            const int k = k0 + u;
+            stage[u & 1][wave][lane] = ring[u];  // DEPTH is even: k & 1 == u & 1
+            ring[u] = load(uni[(k + DEPTH) * G + wave]);
+            __syncthreads();
+            consume(k, u & 1);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < DEPTH; ++u) {
+        stage[u & 1][wave][lane] = ring[u];
+        __syncthreads();
+        consume(last + u, u & 1);
+    }
+    if (!active) return;
+    uint8_t *ob = reinterpret_cast<uint8_t *>(uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase))) + lane16;
+    const int nrows = (int)tile[2];
+#pragma unroll
+    for (int o = 0; o < kTileRows; ++o) {
+        if (o < nrows) {
+            uint8_t *p = ob + (int64_t)tile[4 + o] * a.out_slot_stride;
+            u32x4 v = acc[o];
+            if (a.accumulate) v ^= SAFE ? load_partial(p, valid) : load16(p);
+            if (SAFE) store_partial(p, v, valid);
+            else st16<true>(p, v);
+        }
+    }
 }
 
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
@@ -273,6 +352,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.entries = plan.entries;
     a.tiles = plan.tiles;
     a.groups = plan.groups;
+    a.unions = plan.unions;
     a.n_groups = cm.n_groups();
     a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;
@@ -297,9 +377,9 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             const dim3 grid((unsigned)(ns * per_stripe));
             if (waves) {
                 const dim3 blk(64 * cm.group_size());
-                if (safe) hipLaunchKernelGGL((k_gf_apply_waves<true, 4>), grid, blk, 0, stream, a);
-                else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_waves<false, 8>), grid, blk, 0, stream, a);
-                else hipLaunchKernelGGL((k_gf_apply_waves<false, 4>), grid, blk, 0, stream, a);
+                if (safe) hipLaunchKernelGGL((k_gf_apply_lds<true, 4>), grid, blk, 0, stream, a);
+                else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_lds<false, 8>), grid, blk, 0, stream, a);
+                else hipLaunchKernelGGL((k_gf_apply_lds<false, 4>), grid, blk, 0, stream, a);
                 continue;
             }
             const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (a.n_tiles == 1 ? 2 : 1) : 0);
