@@ -11,7 +11,8 @@
  *                      eighth of the grid; 2 = each XCD runs whole (stripe, chunk) units, all
  *                      tiles of a unit back to back (default: see engine.hpp Tuning)
  *   "wave_groups"      multi-tile maps: 1 = one workgroup per group of tiles sharing inputs, one
- *                      wave per tile, entry lists aligned (default); 0 = one workgroup per tile
+ *                      wave per tile, the group's input union staged once through LDS;
+ *                      0 = one workgroup per tile (default; faster on every measured map)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  */
@@ -25,6 +26,14 @@ int ecx_tune(const char *key, int value); /* 0, or ECX_E_ILLEGAL_ARGUMENT for an
 /* Pure-bandwidth probes over nbytes (multiple of 16 KiB) of device memory:
  * kind 0 = read-only stream, kind 1 = copy src -> dst.  Enqueued on `stream`. */
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream);
+/* Host-only plan self-test: interprets the compiled plan of `map` (entry tables,
+ * tiles, tile groups and their LDS unions) on pseudo-random bytes and compares
+ * with the dense GF(256) map.  0 = consistent, else ECX_E_ILLEGAL_ARGUMENT. */
+struct ecx_map;
+int ecx_map_selftest(const struct ecx_map *map, uint64_t seed);
+/* Plan shape: row tiles, tile entries (= input loads of the one-workgroup-per-tile
+ * kernel), tile groups, and the summed group unions (= input loads of the LDS kernel). */
+int ecx_map_plan_stats(const struct ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total);
 #ifdef __cplusplus
 }
 #endif

@@ -374,6 +374,21 @@ class GfMap:
             self._max_slots = (int(ins.max()) if len(ins) else 0, int(outs.max()) if len(outs) else 0)
         return self._max_slots
 
+    def selftest(self, seed: int = 1) -> None:
+        """Host-only check that the compiled plan (tables, tiles, tile-group unions)
+        reproduces the dense map (ecx_map_selftest, include/ecx_tune.h)."""
+        f = lib().ecx_map_selftest
+        f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_uint64], ctypes.c_int
+        check(f(self._h, seed))
+
+    def plan_stats(self) -> dict:
+        """Shape of the compiled plan (ecx_map_plan_stats, include/ecx_tune.h)."""
+        f = lib().ecx_map_plan_stats
+        f.argtypes, f.restype = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 4, ctypes.c_int
+        v = [ctypes.c_int() for _ in range(4)]
+        check(f(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(["tiles", "entries", "groups", "union_total"], [x.value for x in v]))
+
     def _check(self, inp, iss, isl, out, oss, osl, nstripes, nbytes):
         mi, mo = self.max_slots()
         _check_layout(inp, iss, isl, mi, nstripes, nbytes, "input")

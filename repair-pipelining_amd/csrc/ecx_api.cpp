@@ -730,6 +730,52 @@ int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbyt
     });
 }
 
+int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total) {
+    return guarded([&]() -> int {
+        const CompiledMap &cm = map->cm;
+        if (n_tiles) *n_tiles = cm.n_tiles();
+        if (n_entries) *n_entries = cm.n_tiles() ? cm.n_entries() : 0;
+        if (n_groups) *n_groups = cm.n_groups();
+        if (union_total) *union_total = cm.union_total();
+        return ECX_OK;
+    });
+}
+
+int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
+    return guarded([&]() -> int {
+        const CompiledMap &cm = map->cm;
+        const LinearMap &m = cm.map();
+        const int64_t len = 97;  // ragged on purpose
+        const int nin = cm.max_in_slot() + 1, nout = cm.max_out_slot() + 1;
+        std::vector<uint8_t> in((size_t)std::max(1, nin) * len), ref((size_t)std::max(1, nout) * len, 0);
+        uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
+        for (uint8_t &b : in) {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            b = (uint8_t)x;
+        }
+        const Field &f = Field::get();
+        for (int o = 0; o < m.n_out; ++o)
+            for (int j = 0; j < m.n_in; ++j) {
+                const uint8_t c = m.at(o, j);
+                if (!c) continue;
+                for (int64_t i = 0; i < len; ++i)
+                    ref[(size_t)m.out_slot[o] * len + i] ^= f.mul(c, in[(size_t)m.in_slot[j] * len + i]);
+            }
+        for (bool via_unions : {false, true}) {
+            std::vector<uint8_t> got(ref.size(), 0);
+            cm.emulate(in.data(), got.data(), len, via_unions);
+            for (int o = 0; o < m.n_out; ++o)
+                if (!std::equal(got.begin() + (size_t)m.out_slot[o] * len, got.begin() + (size_t)(m.out_slot[o] + 1) * len,
+                                ref.begin() + (size_t)m.out_slot[o] * len))
+                    throw Error(ECX_E_ILLEGAL_ARGUMENT, via_unions ? "plan (union view) differs from the map"
+                                                                   : "plan (slot view) differs from the map");
+        }
+        return ECX_OK;
+    });
+}
+
 // ---------------------------------------------------------------- synthetic data / verification
 int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream) {
     return guarded([&]() -> int {

@@ -194,19 +194,21 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         cols.push_back(c);
     }
     n_tiles_ = (int)cols.size();
-    std::vector<int> upos(map_.n_in, 0);  // column -> position in its group's union
+    // (tile, column) -> position in the tile's group union; a column read by
+    // several groups has a different position in each.
+    std::vector<std::map<int, int>> upos(n_tiles_);
     if (n_tiles_ > 1) {
         for (const std::vector<int> &g : group_tiles(cols, map_.n_in)) {
             const std::vector<int> uni = align_group(g, cols);
+            std::map<int, int> pos;
+            for (size_t u = 0; u < uni.size(); ++u) pos[uni[u]] = (int)u;
+            for (int t : g) upos[t] = pos;
             uint32_t rec[kGroupDwords];
             std::fill(rec, rec + kGroupDwords, 0u);
             for (int w = 0; w < kWaveGroup; ++w) rec[w] = w < (int)g.size() ? (uint32_t)g[w] : kNoTile;
             rec[8] = (uint32_t)unions_.size();
             rec[9] = (uint32_t)uni.size();
-            for (size_t u = 0; u < uni.size(); ++u) {
-                upos[uni[u]] = (int)u;
-                unions_.push_back((uint32_t)map_.in_slot[uni[u]]);
-            }
+            for (size_t u = 0; u < uni.size(); ++u) unions_.push_back((uint32_t)map_.in_slot[uni[u]]);
             groups_.insert(groups_.end(), rec, rec + kGroupDwords);
             group_size_ = std::max(group_size_, (int)g.size());
             ++n_groups_;
@@ -227,7 +229,7 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
             rec[0] = (uint32_t)map_.in_slot[j];
             rec[1] = mmul;
             rec[2] = mone;
-            rec[3] = (uint32_t)upos[j];
+            rec[3] = n_tiles_ > 1 ? (uint32_t)upos[t].at(j) : 0u;
             for (int r = 0; r < rows; ++r)
                 if (mmul & (1u << r)) split_tables(map_.at(order[r0 + r], j), rec + 4 + 5 * r);
             entries_.insert(entries_.end(), rec, rec + kEntryDwords);
@@ -252,6 +254,47 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         if (c > 0) min_count = std::min(min_count, c);
     }
     preferred_depth_ = (min_count != (1 << 30) && min_count >= 16) ? 8 : 4;
+}
+
+void CompiledMap::emulate(const uint8_t *in, uint8_t *out, int64_t len, bool via_unions) const {
+    auto table_byte = [](const uint32_t *t, int idx) { return (uint8_t)(t[idx >> 2] >> (8 * (idx & 3))); };
+    std::vector<int> group_of(n_tiles_, -1);
+    for (int g = 0; g < n_groups_; ++g)
+        for (int w = 0; w < kWaveGroup; ++w)
+            if (groups_[(size_t)g * kGroupDwords + w] != kNoTile) group_of[groups_[(size_t)g * kGroupDwords + w]] = g;
+    std::vector<uint8_t> acc((size_t)kTileRows * len);
+    for (int t = 0; t < n_tiles_; ++t) {
+        const uint32_t *tile = tiles_.data() + (size_t)t * kTileDwords;
+        std::fill(acc.begin(), acc.end(), 0);
+        uint32_t prev = 0;
+        for (uint32_t e = 0; e < tile[1]; ++e) {
+            const uint32_t *rec = entries_.data() + (size_t)(tile[0] + e) * kEntryDwords;
+            uint32_t slot = rec[0];
+            if (via_unions && n_tiles_ > 1) {
+                const int g = group_of[t];
+                if (g < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "tile without a group");
+                const uint32_t *grp = groups_.data() + (size_t)g * kGroupDwords;
+                if (rec[3] >= grp[9] || (e > 0 && rec[3] <= prev))
+                    throw Error(ECX_E_ILLEGAL_ARGUMENT, "union positions not increasing within a tile");
+                prev = rec[3];
+                slot = unions_[grp[8] + rec[3]];
+                if (slot != rec[0]) throw Error(ECX_E_ILLEGAL_ARGUMENT, "union position names another input");
+            }
+            const uint8_t *x = in + (int64_t)slot * len;
+            for (int r = 0; r < (int)tile[2]; ++r) {
+                uint8_t *a = acc.data() + (size_t)r * len;
+                if (rec[2] & (1u << r))
+                    for (int64_t i = 0; i < len; ++i) a[i] ^= x[i];
+                if (rec[1] & (1u << r)) {
+                    const uint32_t *tb = rec + 4 + 5 * r;
+                    for (int64_t i = 0; i < len; ++i)
+                        a[i] ^= table_byte(tb, x[i] & 7) ^ table_byte(tb + 2, (x[i] >> 3) & 7) ^ table_byte(tb + 4, x[i] >> 6);
+                }
+            }
+        }
+        for (int r = 0; r < (int)tile[2]; ++r)
+            std::copy(acc.begin() + (size_t)r * len, acc.begin() + (size_t)(r + 1) * len, out + (int64_t)tile[4 + r] * len);
+    }
 }
 
 const uint8_t *zero_page_for_current_device() {

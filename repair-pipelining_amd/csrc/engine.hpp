@@ -64,6 +64,8 @@ public:
     // (engine.cpp group_tiles / align_group).
     int n_groups() const { return n_groups_; }
     int group_size() const { return group_size_; }
+    int n_entries() const { return (int)(entries_.size() / kEntryDwords); }  // unpadded (1 if empty)
+    int union_total() const { return (int)unions_.size(); }                   // unpadded
     int max_in_slot() const { return max_in_slot_; }
     int max_out_slot() const { return max_out_slot_; }
     // Load-ring depth for this map: 8 when every non-empty tile has >= 16 entries
@@ -75,6 +77,12 @@ public:
     // The same map over densely renumbered slots: input column j reads compact slot
     // rank(in_slot[j]) among used_in_slots() (sorted), likewise for outputs.  This is
     // the device-side layout of the host-batch pipeline (host_pipe.cpp).
+    // Host interpretation of the compiled plan (diagnostics, ecx_map_selftest):
+    // applies the entry tables exactly as the kernels read them -- by input slot
+    // (k_gf_apply) or through the group unions (k_gf_apply_lds) -- to `in`
+    // ([max_in_slot+1][len]) and writes `out` ([max_out_slot+1][len]).  Throws
+    // if the union bookkeeping is inconsistent.
+    void emulate(const uint8_t *in, uint8_t *out, int64_t len, bool via_unions) const;
     CompiledMap &compact();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
@@ -113,7 +121,10 @@ struct Tuning {
     int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or 4 / 8
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
-    int wave_groups = 1;      // multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS)
+    // Multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS).  Off by
+    // default: Clay(10,4)'s 64-row groups still need 1.23x the unique inputs and the
+    // per-stage barriers cost more than the saved traffic (profiles/r01_multitile.jsonl).
+    int wave_groups = 0;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
 };

@@ -1,8 +1,8 @@
 """Multi-tile maps (inputs re-read across the tiles of a (stripe, chunk) unit):
 launch-shape A/B, interleaved rounds in one process, median GB/s (algorithmic
 bytes).  Modes:
-    waves   -- k_gf_apply_waves: one workgroup per group of tiles sharing inputs (default)
-    tiles   -- k_gf_apply: one workgroup per tile, identity block order
+    waves   -- k_gf_apply_lds: one workgroup per group of tiles, input union staged via LDS
+    tiles   -- k_gf_apply: one workgroup per tile, identity block order (default)
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -78,7 +78,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[(name, x)].append(nbytes / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
-    for key, val in MODES["waves"].items():
+    for key, val in MODES["tiles"].items():
         lib.ecx_tune(key.encode(), val)
     for (name, x), v in res.items():
         med = statistics.median(v)

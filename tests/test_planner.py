@@ -160,3 +160,29 @@ def test_clay104_shortened_shape(ecx):
     """BASELINE config 4: Clay(10,4) repair reads 13 real helper nodes x 64 planes."""
     inf = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2).map().info()
     assert inf["n_out"] == 256 and inf["n_in"] == 13 * 64
+
+
+@pytest.mark.parametrize("k,m,v,erased", [(4, 2, 0, [1]), (4, 2, 0, [4, 5]), (4, 2, 0, [0, 3]), (6, 3, 0, [6, 7, 8]),
+                                          (6, 3, 0, [1, 7]), (10, 4, 2, [3]), (10, 4, 2, [10, 11, 12, 13]),
+                                          (12, 4, 0, [2, 9])])
+def test_compiled_plan_selftest_clay(ecx, k, m, v, erased):
+    """The compiled plan -- split tables, row tiles, tile groups and the LDS unions of
+    k_gf_apply_lds -- interpreted on the host reproduces the composed map."""
+    step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
+    step.map().selftest(seed=len(erased) + k)
+
+
+def test_compiled_plan_selftest_rs_lrc(ecx):
+    import numpy as np
+    rs = ecx.ReedSolomon.create(12, 4)
+    rs.encode_map().selftest()
+    rs.decode_map([False, True, True, False] + [True] * 11 + [False]).selftest()
+    m = np.zeros((4, 12), np.uint8)
+    for g in range(4):
+        m[g, 3 * g:3 * g + 3] = 1
+    ecx.GfMap.from_matrix(m, in_slot=[g * 4 + r for g in range(4) for r in range(3)],
+                          out_slot=[g * 4 + 3 for g in range(4)]).selftest()
+    rng = np.random.default_rng(0)
+    big = rng.integers(0, 256, (40, 30), dtype=np.uint8)
+    big[big < 100] = 0
+    ecx.GfMap.from_matrix(big).selftest(7)  # 5 tiles with arbitrary sharing
