@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--erased", type=int, default=1, help="erased node (README: '1 LP 1 pipeline')")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample; 0 = skip")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-probes", action="store_true", help="skip the in-run memory ceiling probes")
     return ap.parse_args()
 
 
@@ -62,14 +63,24 @@ def _cpu_model() -> str:
     return "unknown CPU"
 
 
-def cpu_baseline(seconds: float, erased: int):
+def cpu_baseline(seconds: float, erased: int, sample=None):
     """Oracle (C restatement of the reference JVM path: InputOutputByteTableCodingLoop
     + the ClayCodeErasureDecodingStep.doDecodeSingle stage sequence), timed by
     oracle/orc_bench.c on one host thread and then on one thread per host core
     (independent stripes per thread).  ``value`` is the
-    all-cores figure; the 1-thread figure rides along."""
+    all-cores figure; the 1-thread figure rides along.  `sample` = (stripe, GPU repair
+    output) of one pool stripe: the oracle repairs it too, and ``oracle_check`` says
+    whether the bytes agree (the sampled byte-compare of SURVEY.md 8(d))."""
     import numpy as np
     import oracle as O
+
+    oracle_check = None
+    if sample is not None:
+        stripe, got = sample
+        inputs = [None if (i % N_NODES) == erased else stripe[i].copy() for i in range(N_NODES * ALPHA)]
+        ref = [np.zeros(B, np.uint8) for _ in range(ALPHA)]
+        O.Clay(K, M, [erased]).perform_coding(inputs, ref, B)
+        oracle_check = all(bool((got[z] == ref[z]).all()) for z in range(ALPHA))
 
     threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     threads = max(1, min(threads, len(os.sched_getaffinity(0)), 64))
@@ -94,6 +105,7 @@ def cpu_baseline(seconds: float, erased: int):
         "cores": threads,
         "kind": "port",
         "single_thread_value": round(one, 3),
+        "oracle_check": oracle_check,
         "sample": f"Clay(4,2) single repairs (e={erased}, B=32 KiB), stage-by-stage C restatement of the "
                   f"reference JVM path (oracle/): {nn} repairs on {threads} threads x {per_thread} host-resident "
                   f"valid stripes each in {eln:.1f} s; single thread {n1} repairs in {el1:.1f} s; {_cpu_model()}",
@@ -112,6 +124,35 @@ def pmc_traffic(pool: int):
     except Exception:
         return None
     return None
+
+
+def memory_probes(ecx, torch, pool, reps: int = 5):
+    """In-run memory ceilings on this GPU: NT read stream, NT copy
+    kernel, hipMemcpyDtoD (torch copy_), each the best of `reps` over 8 GiB regions of
+    the (already verified and timed) pool.  The mix model prices this workload's
+    20-read : 8-write bytes from the read and copy probes."""
+    flat = pool.view(-1)
+    n = min(8 << 30, flat.numel() // 2) // 16384 * 16384
+    src, dst = flat[:n], flat[n:2 * n]
+
+    def best(fn, nbytes):
+        out = 0.0
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            out = max(out, nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+        return out
+
+    rd = best(lambda: ecx.probe_bandwidth(0, src, dst, n, True), n)
+    cp = best(lambda: ecx.probe_bandwidth(1, src, dst, n, True), 2 * n)
+    dd = best(lambda: dst.copy_(src), 2 * n)
+    w = 1.0 / (2.0 / cp - 1.0 / rd)  # write-equivalent rate implied by the copy probe
+    mix = (20 + 8) / (20 / rd + 8 / w)
+    return {"read_probe_GBps": round(rd, 1), "copy_probe_GBps": round(cp, 1), "dtod_copy_GBps": round(dd, 1),
+            "mix_model_GBps": round(mix, 1)}
 
 
 def main():
@@ -200,9 +241,14 @@ def main():
     value = total_stripes * ALGO_BYTES / el / 2**30
     traffic = pmc_traffic(P)
 
+    sample = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:  # one repaired stripe for the oracle check
+        sample = (pool[P // 2].cpu().numpy(), out[P // 2].cpu().numpy())
+    probes = memory_probes(ecx, torch, pool) if not args.no_probes else None
+
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args.cpu_seconds, args.erased)
+    if sample is not None:
+        cpu = cpu_baseline(args.cpu_seconds, args.erased, sample)
 
     if rank == 0:
         line = {
@@ -235,6 +281,8 @@ def main():
                 "kernel": KERNEL,
                 "avg_launch_ms": round(launch_ms, 4),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
+                "measured_ceilings": probes,
+                "frac_of_mix_model": round(achieved / probes["mix_model_GBps"], 4) if probes else None,
             },
             "cpu_baseline": cpu,
             "verified": verified,

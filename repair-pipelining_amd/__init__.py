@@ -201,6 +201,15 @@ def tune(key: str, value: int) -> None:
     check(f(key.encode(), int(value)))
 
 
+def probe_bandwidth(kind: int, src, dst, nbytes: int, nontemporal: bool = True, stream=None) -> None:
+    """Pure-bandwidth probe kernels (include/ecx_tune.h): kind 0 = read-only stream of
+    `src`, kind 1 = copy src -> dst; nbytes a multiple of 16 KiB.  Diagnostics only."""
+    f = lib().ecx_probe_bandwidth
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    check(f(kind, _dev_ptr(src), _dev_ptr(dst), nbytes, 1 if nontemporal else 0, _stream(stream)))
+
+
 def _stream(stream) -> Optional[int]:
     if stream is None:
         try:
