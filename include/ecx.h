@@ -182,6 +182,23 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
                                   int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
                                   int64_t out_sub_stride, int64_t nstripes, int64_t buf_size, void *stream);
 
+/* ---------------------------------------------------------------- LRC (device batch, in place) */
+/* LRCErasureCode.kt:5-9 / LRCErasureUtil.kt:3-6: K=12 data blocks in local groups of
+ * R=3, one RS(3,1) parity each (parity row [1,1,1], i.e. XOR), N=16 blocks in the
+ * LRCErasureCodeExample.kt:48 order (group g = blocks 4g..4g+3, parity 4g+3).
+ * Block b of stripe s is at stripes + s*stripe_stride + b*block_stride. */
+/* The composed map: block_present == NULL -> encode, else decode (owned by the library). */
+int ecx_lrc_map(const uint8_t *block_present /* 16 flags or NULL */, const ecx_map **out);
+/* encode / encodeUsingSingle (LRCErasureCodeExample.kt:30-98): writes the 4 group parities. */
+int ecx_lrc_encode_batch(uint8_t *stripes, int64_t stripe_stride, int64_t block_stride, int64_t nstripes,
+                         int64_t block_size, void *stream);
+/* decode (LRCErasureCodeExample.kt:100-131): rebuilds every non-present block from
+ * its group (decodeMissing per group).  Two blocks missing in one group ->
+ * ECX_E_NOT_ENOUGH_SHARDS, as RS(3,1).decodeMissing throws. */
+int ecx_lrc_decode_batch(uint8_t *stripes, int64_t stripe_stride, int64_t block_stride,
+                         const uint8_t *block_present /* 16 flags */, int64_t nstripes, int64_t block_size,
+                         void *stream);
+
 /* ---------------------------------------------------------------- host-memory batches */
 /* The reference's repair starts and ends in host memory: helper sub-chunks arrive on
  * sockets into ByteBuffers (ClayCoordinator.kt:372-395) and leave the same way

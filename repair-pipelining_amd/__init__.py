@@ -822,6 +822,33 @@ class LRCErasureCode:
     def encodeParitySingle(self, shard, output, index, blockSize):
         self.rs.encodeParitySingle(shard, output, index, 0, 0, blockSize)
 
+    @staticmethod
+    def map(blockPresent=None) -> GfMap:
+        """The composed LRC map over the 16 blocks: encode (None) or decode (ecx_lrc_map)."""
+        h = ctypes.c_void_p()
+        pres = None if blockPresent is None else np.array([1 if p else 0 for p in blockPresent], np.uint8)
+        check(lib().ecx_lrc_map(None if pres is None else pres.ctypes.data, ctypes.byref(h)))
+        return GfMap(h)
+
+    @staticmethod
+    def encodeBatch(stripes, stripe_stride, block_stride, nstripes, blockSize, stream=None) -> None:
+        """All group parities of device-resident [S][16][B] stripes, in place (ecx_lrc_encode_batch)."""
+        LRCErasureCode.map()._check(stripes, stripe_stride, block_stride, stripes, stripe_stride, block_stride,
+                                    nstripes, blockSize)
+        check(lib().ecx_lrc_encode_batch(_dev_ptr(stripes), stripe_stride, block_stride, nstripes, blockSize,
+                                         _stream(stream)))
+
+    @staticmethod
+    def decodeBatch(stripes, stripe_stride, block_stride, blockPresent, nstripes, blockSize, stream=None) -> None:
+        """Rebuild the non-present blocks of device-resident stripes in place (ecx_lrc_decode_batch)."""
+        pres = np.array([1 if p else 0 for p in blockPresent], np.uint8)
+        if pres.all():
+            return
+        LRCErasureCode.map(blockPresent)._check(stripes, stripe_stride, block_stride, stripes, stripe_stride,
+                                                block_stride, nstripes, blockSize)
+        check(lib().ecx_lrc_decode_batch(_dev_ptr(stripes), stripe_stride, block_stride, pres.ctypes.data, nstripes,
+                                         blockSize, _stream(stream)))
+
 
 def lrc_encode(data: np.ndarray):
     """LRCErasureCodeExample.encode (:30-57): K blocks -> N blocks (group g: 3 data + parity)."""

@@ -95,6 +95,9 @@ SIGNATURES = {
     "ecx_clay_decode_single_helper": (I, [P, PP, I, PP, I, I]),
     "ecx_clay_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_clay_perform_coding_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
+    "ecx_lrc_map": (I, [P, ctypes.POINTER(P)]),
+    "ecx_lrc_encode_batch": (I, [P, I64, I64, I64, I64, P]),
+    "ecx_lrc_decode_batch": (I, [P, I64, I64, P, I64, I64, P]),
     "ecx_map_apply_batch_host": (I, [P, P, I64, I64, P, I64, I64, I64, I64]),
     "ecx_clay_perform_coding_batch_host": (I, [P, P, I64, I64, P, I64, I64, I64, I64]),
     "ecx_host_alloc": (I, [I64, ctypes.POINTER(P)]),

@@ -132,6 +132,46 @@ LinearMap RsCode::decode_map(const std::vector<bool> &present) const {
     return mp.pruned();
 }
 
+// ---------------------------------------------------------------- LrcCode
+namespace {
+// Stack per-group maps (over group-local slots 0..R) into one map over the N blocks.
+LinearMap stack_groups(const std::vector<std::pair<int, LinearMap>> &parts) {
+    LinearMap mp;
+    mp.n_in = LrcCode::kN;
+    for (int i = 0; i < LrcCode::kN; ++i) mp.in_slot.push_back(i);
+    for (const auto &gp : parts) {
+        const int base = gp.first * (LrcCode::kR + 1);
+        const LinearMap &g = gp.second;
+        for (int o = 0; o < g.n_out; ++o) {
+            std::vector<uint8_t> row(LrcCode::kN, 0);
+            for (int j = 0; j < g.n_in; ++j) row[base + g.in_slot[j]] = g.at(o, j);
+            mp.a.insert(mp.a.end(), row.begin(), row.end());
+            mp.out_slot.push_back(base + g.out_slot[o]);
+        }
+    }
+    mp.n_out = (int)mp.out_slot.size();
+    return mp.pruned();
+}
+}  // namespace
+
+LinearMap LrcCode::encode_map() const {
+    std::vector<std::pair<int, LinearMap>> parts;
+    for (int g = 0; g < kGroups; ++g) parts.push_back({g, group_.encode_map()});
+    return stack_groups(parts);
+}
+
+LinearMap LrcCode::decode_map(const std::vector<bool> &present) const {
+    if ((int)present.size() != kN) throw Error(ECX_E_ILLEGAL_ARGUMENT, "wrong number of blocks");
+    std::vector<std::pair<int, LinearMap>> parts;
+    for (int g = 0; g < kGroups; ++g) {
+        std::vector<bool> p(present.begin() + g * (kR + 1), present.begin() + (g + 1) * (kR + 1));
+        bool all = true;
+        for (bool b : p) all &= b;
+        if (!all) parts.push_back({g, group_.decode_map(p)});  // throws "Not enough shards present"
+    }
+    return stack_groups(parts);
+}
+
 // ---------------------------------------------------------------- ClayPlanner
 namespace {
 int ipow(int b, int e) {

@@ -59,6 +59,23 @@ private:
     Matrix gen_;
 };
 
+// LRC (LRCErasureCode.kt:5-9, LRCErasureUtil.kt:3-6): K = 12 data blocks in local
+// groups of R = 3, each with one parity from RS(R, 1) (parity row [1,1,1]: XOR).
+// Block order of LRCErasureCodeExample.kt:48: group g = blocks 4g..4g+3, parity 4g+3.
+class LrcCode {
+public:
+    static constexpr int kK = 12, kR = 3, kGroups = kK / kR, kN = kK + kGroups;
+    LrcCode() : group_(kR, 1) {}
+    // encode / encodeUsingSingle (LRCErasureCodeExample.kt:30-98): every group parity.
+    LinearMap encode_map() const;
+    // decode (:100-131): per group, decodeMissing of the group's non-present blocks;
+    // more than one missing block in a group -> ECX_E_NOT_ENOUGH_SHARDS.
+    LinearMap decode_map(const std::vector<bool> &present) const;
+
+private:
+    RsCode group_;
+};
+
 // ClayCodeErasureDecodingStep.java + ClayCodeUtil (:676-944), symbolically.
 //
 // virtual_units > 0 builds a SHORTENED code: Clay(k + v, m) whose data nodes

@@ -633,6 +633,63 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
     });
 }
 
+// ---------------------------------------------------------------- LRC
+namespace {
+struct LrcCache {
+    std::mutex mu;
+    LrcCode code;
+    std::unique_ptr<ecx_map> enc;
+    std::map<uint32_t, std::unique_ptr<ecx_map>> dec;  // present mask -> map
+};
+LrcCache *lrc_cache() {
+    static LrcCache c;
+    return &c;
+}
+}  // namespace
+
+int ecx_lrc_map(const uint8_t *block_present, const ecx_map **out) {
+    return guarded([&]() -> int {
+        if (!out) throw Error(ECX_E_NULL, "null out pointer");
+        LrcCache &c = *lrc_cache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        if (!block_present) {
+            if (!c.enc) c.enc = std::make_unique<ecx_map>(c.code.encode_map());
+            *out = c.enc.get();
+            return ECX_OK;
+        }
+        uint32_t mask = 0;
+        std::vector<bool> present(LrcCode::kN);
+        for (int i = 0; i < LrcCode::kN; ++i) {
+            present[i] = block_present[i] != 0;
+            mask |= present[i] ? (1u << i) : 0u;
+        }
+        auto &slot = c.dec[mask];
+        if (!slot) slot = std::make_unique<ecx_map>(c.code.decode_map(present));
+        *out = slot.get();
+        return ECX_OK;
+    });
+}
+
+int ecx_lrc_encode_batch(uint8_t *stripes, int64_t stripe_stride, int64_t block_stride, int64_t nstripes,
+                         int64_t block_size, void *stream) {
+    const ecx_map *m = nullptr;
+    int st = ecx_lrc_map(nullptr, &m);
+    if (st) return st;
+    return ecx_map_apply_batch(m, stripes, stripe_stride, block_stride, stripes, stripe_stride, block_stride, nstripes,
+                               block_size, stream);
+}
+
+int ecx_lrc_decode_batch(uint8_t *stripes, int64_t stripe_stride, int64_t block_stride, const uint8_t *block_present,
+                         int64_t nstripes, int64_t block_size, void *stream) {
+    if (!block_present) return ECX_E_NULL;
+    const ecx_map *m = nullptr;
+    int st = ecx_lrc_map(block_present, &m);
+    if (st) return st;
+    if (m->cm.map().n_out == 0) return ECX_OK;  // nothing missing
+    return ecx_map_apply_batch(m, stripes, stripe_stride, block_stride, stripes, stripe_stride, block_stride, nstripes,
+                               block_size, stream);
+}
+
 // ---------------------------------------------------------------- host-memory batches (f1)
 int ecx_map_apply_batch_host(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                              uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,

@@ -600,3 +600,28 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
         ref = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
         O.Clay(k, m, erased).perform_coding(inputs, ref, B)
         assert all((outs[0][S - 1, j] == ref[j]).all() for j in range(len(ref)))
+
+
+def test_lrc_batch_abi_encode_and_decode(ecx, torch_dev):
+    """ecx_lrc_encode_batch / ecx_lrc_decode_batch on BASELINE config 3 shapes (64 KiB
+    blocks): parities equal the oracle's RS(3,1) encodeParity; erasing one block in each
+    of three groups and decoding in place restores every block."""
+    torch = torch_dev
+    B, S = 65536, 24
+    pool = torch.empty((S, 16, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 71)
+    ecx.LRCErasureCode.encodeBatch(pool, 16 * B, B, S, B)
+    torch.cuda.synchronize()
+    host = pool[S - 1].cpu().numpy()
+    for g in range(4):
+        b = [host[4 * g + j].copy() for j in range(4)]
+        O.ReedSolomon(3, 1).encode_parity(b, 0, B)
+        assert (b[3] == host[4 * g + 3]).all()
+    orig = pool.clone()
+    present = [True] * 16
+    for i in (1, 7, 14):
+        present[i] = False
+        pool[:, i] = 0
+    ecx.LRCErasureCode.decodeBatch(pool, 16 * B, B, present, S, B)
+    torch.cuda.synchronize()
+    assert torch.equal(pool, orig)

@@ -186,3 +186,31 @@ def test_compiled_plan_selftest_rs_lrc(ecx):
     big = rng.integers(0, 256, (40, 30), dtype=np.uint8)
     big[big < 100] = 0
     ecx.GfMap.from_matrix(big).selftest(7)  # 5 tiles with arbitrary sharing
+
+
+def test_lrc_maps_match_reference_groups(ecx):
+    """LRC maps (ecx_lrc_map): encode = XOR of each group's 3 data blocks into its parity
+    (RS(3,1), LRCErasureCode.kt); decode rebuilds one block per group from the other 3
+    and refuses two missing blocks in a group (RS(3,1).decodeMissing's exception)."""
+    import numpy as np
+    m, ins, outs = ecx.LRCErasureCode.map().matrix()
+    assert list(outs) == [3, 7, 11, 15] and list(ins) == [g * 4 + r for g in range(4) for r in range(3)]
+    assert (m == np.kron(np.eye(4, dtype=np.uint8), np.ones((1, 3), np.uint8))).all()
+    pres = [True] * 16
+    pres[2] = pres[7] = pres[12] = False
+    dm = ecx.LRCErasureCode.map(pres)
+    dm.selftest()
+    m, ins, outs = dm.matrix()
+    assert list(outs) == [2, 7, 12]
+    rng = np.random.default_rng(4)
+    blocks = [rng.integers(0, 256, 64, dtype=np.uint8) for _ in range(16)]
+    for g in range(4):
+        blocks[4 * g + 3] = blocks[4 * g] ^ blocks[4 * g + 1] ^ blocks[4 * g + 2]
+    from conftest import gf_apply_numpy
+    got = gf_apply_numpy(m, [blocks[s] for s in ins])
+    for o, slot in enumerate(outs):
+        assert (got[o] == blocks[slot]).all()
+    pres[13] = False
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.LRCErasureCode.map(pres)
+    assert e.value.code == -2
