@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--stripes-per-step", type=int, default=1 << 20)
-    ap.add_argument("--pool", type=int, default=1 << 14, help="resident stripes per GPU (24 GiB at 2^14)")
+    ap.add_argument("--pool", type=int, default=1 << 15, help="resident stripes per GPU (48 GiB at 2^15)")
     ap.add_argument("--erased", type=int, default=1, help="erased node (README: '1 LP 1 pipeline')")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample; 0 = skip")
     ap.add_argument("--no-verify", action="store_true")

@@ -15,7 +15,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 KERNEL = "k_gf_apply<false, true, true, 8>"
-POOL, B = 1 << 14, 32768
+POOL, B = 1 << 15, 32768
 GRID = POOL * 8 * 256  # threads of one pool launch (8 chunks x 256 lanes per stripe)
 
 
