@@ -15,6 +15,9 @@
  *                      0 = one workgroup per tile (default; faster on every measured map)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
+ *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered
+ *                      through pinned staging (one H2D / one D2H); 0 = always per-slot copies
+ *                      (default 256)
  */
 #ifndef ECX_TUNE_H
 #define ECX_TUNE_H

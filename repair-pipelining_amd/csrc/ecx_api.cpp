@@ -772,6 +772,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 1) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_chunk = (int64_t)value << 10;
     }
+    else if (k == "host_gather_kib") {
+        if (value < 0) return ECX_E_ILLEGAL_ARGUMENT;
+        t.host_gather_max = (int64_t)value << 10;
+    }
     else if (k == "host_buffers") {
         if (value < 1 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_buffers = value;

@@ -437,6 +437,17 @@ uint8_t *DeviceContext::ensure(size_t bytes) {
     return staging_;
 }
 
+uint8_t *DeviceContext::ensure_pinned(size_t bytes) {
+    if (bytes <= pinned_size_) return pinned_;
+    if (pinned_) check_hip(hipHostFree(pinned_), "hipHostFree(staging)");
+    pinned_ = nullptr;
+    pinned_size_ = 0;
+    size_t sz = std::max<size_t>(bytes, 1 << 20);
+    check_hip(hipHostMalloc(reinterpret_cast<void **>(&pinned_), sz, hipHostMallocDefault), "hipHostMalloc(staging)");
+    pinned_size_ = sz;
+    return pinned_;
+}
+
 uint64_t *DeviceContext::counter() {
     if (!counter_) check_hip(hipMalloc(&counter_, sizeof(uint64_t)), "hipMalloc(counter)");
     return counter_;
@@ -470,11 +481,50 @@ Staged stage_inputs(DeviceContext &ctx, CompiledMap &cm, const uint8_t *const *i
 
 }  // namespace
 
+namespace {
+// Gather path: used input slots -> pinned [U][pitch] -> HBM; compact map; rows -> pinned [V][pitch].
+// Returns the pinned output rows (valid after the stream synchronises).
+const uint8_t *run_gathered(DeviceContext &ctx, CompiledMap &cm, const uint8_t *const *inputs, int64_t offset,
+                            int64_t byte_count, uint8_t **dev_out, int64_t *pitch_out) {
+    CompiledMap &cc = cm.compact();
+    const std::vector<int> &ins = cm.used_in_slots(), &outs = cm.used_out_slots();
+    const int64_t pitch = (byte_count + 255) / 256 * 256;
+    const int64_t nin = (int64_t)ins.size(), nout = (int64_t)outs.size();
+    uint8_t *host = ctx.ensure_pinned((size_t)(pitch * (nin + nout)));
+    uint8_t *dev = ctx.ensure((size_t)(pitch * (nin + nout)));
+    for (int64_t u = 0; u < nin; ++u) {
+        const uint8_t *src = inputs[ins[u]];
+        if (!src) throw Error(ECX_E_NULL, "input buffer is null");
+        std::memcpy(host + u * pitch, src + offset, (size_t)byte_count);
+    }
+    check_hip(hipMemcpyAsync(dev, host, (size_t)(pitch * nin), hipMemcpyHostToDevice, ctx.stream), "hipMemcpyAsync H2D");
+    launch_apply(cc, dev, 0, pitch, dev + pitch * nin, 0, pitch, 1, byte_count, ctx.stream);
+    *dev_out = dev + pitch * nin;
+    *pitch_out = pitch;
+    return host + pitch * nin;
+}
+}  // namespace
+
 void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
               int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return;
     DeviceContext &ctx = DeviceContext::current();
     std::lock_guard<std::mutex> lk(ctx.mu);
+    if (byte_count <= tuning().host_gather_max) {
+        const std::vector<int> &outs = cm.used_out_slots();
+        for (int slot : outs)
+            if (!outputs[slot]) throw Error(ECX_E_NULL, "output buffer is null");
+        uint8_t *dev_rows = nullptr;
+        int64_t pitch = 0;
+        const uint8_t *host_rows = run_gathered(ctx, cm, inputs, offset, byte_count, &dev_rows, &pitch);
+        check_hip(hipMemcpyAsync(const_cast<uint8_t *>(host_rows), dev_rows, (size_t)(pitch * (int64_t)outs.size()),
+                                 hipMemcpyDeviceToHost, ctx.stream),
+                  "hipMemcpyAsync D2H");
+        check_hip(hipStreamSynchronize(ctx.stream), "hipStreamSynchronize");
+        for (size_t v = 0; v < outs.size(); ++v)
+            std::memcpy(outputs[outs[v]] + offset, host_rows + (int64_t)v * pitch, (size_t)byte_count);
+        return;
+    }
     Staged st = stage_inputs(ctx, cm, inputs, offset, byte_count);
     launch_apply(cm, st.in, 0, st.pitch, st.out, 0, st.pitch, 1, byte_count, ctx.stream);
     const LinearMap &m = cm.map();
@@ -492,13 +542,21 @@ bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t of
     if (byte_count <= 0 || cm.map().n_out == 0) return true;
     DeviceContext &ctx = DeviceContext::current();
     std::lock_guard<std::mutex> lk(ctx.mu);
-    Staged st = stage_inputs(ctx, cm, inputs, offset, byte_count);
-    launch_apply(cm, st.in, 0, st.pitch, st.out, 0, st.pitch, 1, byte_count, ctx.stream);
     uint64_t *cnt = ctx.counter();
     check_hip(hipMemsetAsync(cnt, 0, sizeof(uint64_t), ctx.stream), "hipMemsetAsync");
-    const LinearMap &m = cm.map();
-    for (int o = 0; o < m.n_out; ++o)
-        launch_count_mismatch(st.out + st.pitch * m.out_slot[o], 0, nullptr, 0, 1, byte_count, cnt, ctx.stream);
+    if (byte_count <= tuning().host_gather_max) {
+        uint8_t *dev_rows = nullptr;
+        int64_t pitch = 0;
+        (void)run_gathered(ctx, cm, inputs, offset, byte_count, &dev_rows, &pitch);
+        launch_count_mismatch(dev_rows, pitch, nullptr, 0, (int64_t)cm.used_out_slots().size(), byte_count, cnt,
+                              ctx.stream);
+    } else {
+        Staged st = stage_inputs(ctx, cm, inputs, offset, byte_count);
+        launch_apply(cm, st.in, 0, st.pitch, st.out, 0, st.pitch, 1, byte_count, ctx.stream);
+        const LinearMap &m = cm.map();
+        for (int o = 0; o < m.n_out; ++o)
+            launch_count_mismatch(st.out + st.pitch * m.out_slot[o], 0, nullptr, 0, 1, byte_count, cnt, ctx.stream);
+    }
     uint64_t host = 0;
     check_hip(hipMemcpyAsync(&host, cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, ctx.stream), "hipMemcpyAsync D2H");
     check_hip(hipStreamSynchronize(ctx.stream), "hipStreamSynchronize");

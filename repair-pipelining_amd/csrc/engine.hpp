@@ -127,6 +127,8 @@ struct Tuning {
     int wave_groups = 0;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
+    int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the
+                                          // used slots into pinned staging (one H2D / one D2H)
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();
@@ -148,17 +150,23 @@ public:
     hipStream_t stream = nullptr;
     int device = 0;
     uint8_t *ensure(size_t bytes);
+    uint8_t *ensure_pinned(size_t bytes);  // page-locked host staging
     uint64_t *counter();
 
 private:
     uint8_t *staging_ = nullptr;
     size_t staging_size_ = 0;
+    uint8_t *pinned_ = nullptr;
+    size_t pinned_size_ = 0;
     uint64_t *counter_ = nullptr;
 };
 
-// Host-pointer execution of a compiled map: gathers each used input slot
+// Host-pointer execution of a compiled map: moves each used input slot
 // (`inputs[slot] + offset`, byte_count bytes) into HBM, applies the map and
-// copies each output row back to `outputs[slot] + offset`.  Synchronous.
+// copies each output row back to `outputs[slot] + offset`.  Synchronous.  Up to
+// Tuning::host_gather_max bytes the used slots are gathered into pinned staging
+// (one H2D, the compact map, one D2H, scatter): per-call latency is then a few
+// copies, not one pageable transfer per slot.
 void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
               int64_t byte_count);
 // As run_host, but instead of copying outputs back, returns whether every

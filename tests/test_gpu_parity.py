@@ -625,3 +625,31 @@ def test_lrc_batch_abi_encode_and_decode(ecx, torch_dev):
     ecx.LRCErasureCode.decodeBatch(pool, 16 * B, B, present, S, B)
     torch.cuda.synchronize()
     assert torch.equal(pool, orig)
+
+
+@pytest.mark.parametrize("L", [1, 4097, 300000])
+def test_per_call_paths_agree(ecx, L):
+    """Per-call host entry points: the pinned gather path (one H2D / one D2H) and the
+    per-slot copy path give the oracle's bytes for encode, check and decodeMissing."""
+    rng = np.random.default_rng(L)
+    base = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(6)]
+    ref = [b.copy() for b in base]
+    O.ReedSolomon(4, 2).encode_parity(ref, 0, L)
+    rs = ecx.ReedSolomon.create(4, 2)
+    try:
+        for gather_kib in (0, 1 << 20):
+            ecx.tune("host_gather_kib", gather_kib)
+            sh = [b.copy() for b in base]
+            rs.encodeParity(sh, 0, L)
+            assert all((sh[i] == ref[i]).all() for i in range(6))
+            assert rs.isParityCorrect(sh, 0, L)
+            sh[5][L // 2] ^= 0x40
+            assert not rs.isParityCorrect(sh, 0, L)
+            sh[5][L // 2] ^= 0x40
+            present = [True, False, True, False, True, True]
+            sh[1][:] = 0
+            sh[3][:] = 0
+            rs.decodeMissing(sh, present, 0, L)
+            assert all((sh[i] == ref[i]).all() for i in range(6))
+    finally:
+        ecx.tune("host_gather_kib", 256)
