@@ -1,4 +1,4 @@
-"""In-process A/B of k_gf_apply / k_gf_stream launch shapes on the headline
+"""In-process A/B of k_gf_apply launch shapes (load-ring depth, non-temporal policy) on the headline
 workload (Clay(4,2) repair, B = 32 KiB, resident pool), interleaved rounds
 (cdna_hip_programming.md 5.4 rule 24), plus two ceilings for this access
 pattern: an XOR-only map with the identical 20-read / 8-write layout, and a
