@@ -284,6 +284,7 @@ def main():
                 "measured_ceilings": probes,
                 "frac_of_mix_model": round(achieved / probes["mix_model_GBps"], 4) if probes else None,
             },
+            "repaired_output_GiBps": round(total_stripes * WRITE_BYTES / el / 2**30, 3),
             "cpu_baseline": cpu,
             "verified": verified,
         }
