@@ -13,6 +13,9 @@
  *   "wave_groups"      multi-tile maps: 1 = one workgroup per group of tiles sharing inputs, one
  *                      wave per tile, the group's input union staged once through LDS;
  *                      0 = one workgroup per tile (default; faster on every measured map)
+ *   "lds_tables"       0 = all split-table dwords read as scalars (one v_mov per 8-entry table
+ *                      and row); 1 = the low dword of each 8-entry table staged per workgroup
+ *                      in LDS, for multi-tile maps (default); 2 = for every map
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

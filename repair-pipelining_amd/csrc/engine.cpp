@@ -320,6 +320,7 @@ CompiledMap::~CompiledMap() {
         (void)hipFree(kv.second.tiles);
         (void)hipFree(kv.second.groups);
         (void)hipFree(kv.second.unions);
+        (void)hipFree(kv.second.atab);
         (void)hipSetDevice(cur);
     }
 }
@@ -349,6 +350,15 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     }
     if (ents.empty()) ents.assign(kEntryDwords, 0);
     DevicePlan p;
+    std::vector<uint32_t> atab;
+    for (size_t e = 0; e < ents.size() / kEntryDwords; ++e)
+        for (int r = 0; r < kTileRows; ++r) {
+            atab.push_back(ents[e * kEntryDwords + 4 + 5 * r]);      // T0a
+            atab.push_back(ents[e * kEntryDwords + 4 + 5 * r + 2]);  // T1a
+        }
+    for (int t = 0; t < n_tiles_; ++t) p.max_tile_entries = std::max(p.max_tile_entries, (int)tiles[(size_t)t * kTileDwords + 1]);
+    check_hip(hipMalloc(&p.atab, atab.size() * 4), "hipMalloc(plan atab)");
+    check_hip(hipMemcpy(p.atab, atab.data(), atab.size() * 4, hipMemcpyHostToDevice), "plan upload");
     check_hip(hipMalloc(&p.entries, ents.size() * 4), "hipMalloc(plan entries)");
     check_hip(hipMalloc(&p.tiles, tiles.size() * 4), "hipMalloc(plan tiles)");
     // Unions: each group's list padded with zero-page entries to a multiple of

@@ -47,7 +47,13 @@ struct DevicePlan {
     uint32_t *tiles = nullptr;
     uint32_t *groups = nullptr;  // n_groups x kGroupDwords
     uint32_t *unions = nullptr;  // per group: input slots in staging order, padded (kDummySlot)
+    // Per padded entry, kTileRows x {T0a, T1a}: the low table dwords of every row,
+    // staged per workgroup into LDS by k_gf_apply<..., TLDS=true> (kernels.hip).
+    uint32_t *atab = nullptr;
+    int max_tile_entries = 0;  // padded
 };
+constexpr int kAtabDwords = 2 * kTileRows;
+constexpr int kMaxLdsTileEntries = 512;  // 32 KiB of LDS per workgroup at most
 
 // 4 KiB of zeros per device, never written: the load target of padding entries
 // (always L2-resident, so padding costs no HBM traffic).
@@ -106,6 +112,7 @@ struct ApplyArgs {
     const uint32_t *tiles;
     const uint32_t *groups;
     const uint32_t *unions;
+    const uint32_t *atab;
     const uint8_t *zero_page;
     int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
     int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
@@ -113,6 +120,7 @@ struct ApplyArgs {
     int n_groups;         // k_gf_apply_lds: tile groups (workgroups per chunk)
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
+    int lane_zero;        // always 0 (keeps k_gf_apply's LDS table base in a VGPR)
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -125,6 +133,10 @@ struct Tuning {
     // default: Clay(10,4)'s 64-row groups still need 1.23x the unique inputs and the
     // per-stage barriers cost more than the saved traffic (profiles/r01_multitile.jsonl).
     int wave_groups = 0;
+    // k_gf_apply: 0 = every table dword from the plan in SGPRs (a v_mov per 8-entry table
+    // and row); 1 = the low table dwords staged once per workgroup in LDS and read as
+    // VGPRs, for multi-tile maps; 2 = for every map.
+    int lds_tables = 1;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -80,10 +80,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-__device__ __forceinline__ uint32_t gf_mac4(uint32_t acc, const uint32_t *tb, uint32_t i0, uint32_t i1, uint32_t i2) {
-    const uint32_t p0 = __builtin_amdgcn_perm(tb[1], tb[0], i0);
-    const uint32_t p1 = __builtin_amdgcn_perm(tb[3], tb[2], i1);
-    const uint32_t p2 = __builtin_amdgcn_perm(tb[4], tb[4], i2);
+__device__ __forceinline__ uint32_t gf_mac4(uint32_t acc, uint32_t t0a, uint32_t t0b, uint32_t t1a, uint32_t t1b,
+                                            uint32_t t2, uint32_t i0, uint32_t i1, uint32_t i2) {
+    const uint32_t p0 = __builtin_amdgcn_perm(t0b, t0a, i0);
+    const uint32_t p1 = __builtin_amdgcn_perm(t1b, t1a, i1);
+    const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, i2);
     return xor3(acc, p0, xor3(p1, p2, 0u));
 }
 
@@ -91,7 +92,13 @@ __device__ __forceinline__ uint32_t gf_mac4(uint32_t acc, const uint32_t *tb, ui
 // dwords are fetched as five 8-dword scalar loads that straddle the per-row
 // groups, so they are issued once per entry (not sunk into the per-row
 // branches); rows without a coefficient are skipped by scalar branches.
-__device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)[kTileRows]) {
+//
+// A v_perm_b32 reads at most one SGPR, so an 8-entry table (two dwords) needs one
+// of its dwords in a VGPR.  With TLDS the low dwords of both 8-entry tables of
+// every row come from the workgroup's LDS copy of the plan (`lt`, one broadcast
+// ds_read_b64 per row); otherwise each is copied from its SGPR with a v_mov.
+template <bool TLDS>
+__device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)[kTileRows], const uint2 *lt) {
     const uint32_t mmul = r[1], mone = r[2];
     cu32x8 *tv = (cu32x8 *)(r + 4);
     const u32x8 v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3], v4 = tv[4];
@@ -106,10 +113,16 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
     for (int o = 0; o < kTileRows; ++o) {
         if (mmul & (1u << o)) {
             const uint32_t *t = tb + 5 * o;
-            acc[o].x = gf_mac4(acc[o].x, t, i0.x, i1.x, i2.x);
-            acc[o].y = gf_mac4(acc[o].y, t, i0.y, i1.y, i2.y);
-            acc[o].z = gf_mac4(acc[o].z, t, i0.z, i1.z, i2.z);
-            acc[o].w = gf_mac4(acc[o].w, t, i0.w, i1.w, i2.w);
+            uint32_t t0a = t[0], t1a = t[2];
+            if (TLDS) {
+                const uint2 la = lt[o];
+                t0a = la.x;
+                t1a = la.y;
+            }
+            acc[o].x = gf_mac4(acc[o].x, t0a, t[1], t1a, t[3], t[4], i0.x, i1.x, i2.x);
+            acc[o].y = gf_mac4(acc[o].y, t0a, t[1], t1a, t[3], t[4], i0.y, i1.y, i2.y);
+            acc[o].z = gf_mac4(acc[o].z, t0a, t[1], t1a, t[3], t[4], i0.z, i1.z, i2.z);
+            acc[o].w = gf_mac4(acc[o].w, t0a, t[1], t1a, t[3], t[4], i0.w, i1.w, i2.w);
         }
     }
     if (mone) {  // coefficient 1: acc ^= x & mask (one v_bitop3, table 0x78 = a ^ (b & c))
@@ -160,9 +173,9 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool SAFE, bool NTL, bool NTS, int DEPTH>
+template <bool SAFE, bool NTL, bool NTS, int DEPTH, bool TLDS>
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint64_t in_base, uint64_t out_base,
-                                           uint32_t lane16, int valid) {
+                                           uint32_t lane16, int valid, uint2 *lds_tab) {
     const uint8_t *ib = reinterpret_cast<const uint8_t *>(in_base) + lane16;
     const uint32_t zoff = lane16;
     const int ebeg = (int)tile[0];
@@ -178,6 +191,18 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
     for (int r = 0; r < kTileRows; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
 
     cu32 *ent = plan_ptr(a.entries) + (int64_t)ebeg * kEntryDwords;
+    // TLDS: the tile's {T0a, T1a} table dwords (kAtabDwords per entry) go to LDS.
+    // Their global loads are issued before the load ring so that waiting for them
+    // does not wait for the ring; the ring loads overlap the LDS store and barrier.
+    const int n16 = TLDS ? ecnt * (kAtabDwords / 4) : 0;  // 16-B pieces
+    const gu32x4 *asrc = (const gu32x4 *)(a.atab + (int64_t)ebeg * kAtabDwords);
+    u32x4 apiece = (u32x4){0u, 0u, 0u, 0u};
+    // LDS addresses are VGPRs.  A base the compiler sees as uniform lives in an SGPR
+    // and is copied by a v_mov before every row's ds_read; adding threadIdx.x times
+    // a run-time zero (ApplyArgs::lane_zero) keeps it in a VGPR, so each read is the
+    // base plus an immediate offset.
+    uint2 *ltab = lds_tab + threadIdx.x * (uint32_t)a.lane_zero;
+    if (TLDS && (int)threadIdx.x < n16) apiece = asrc[threadIdx.x];
     // Load ring of DEPTH 16-B loads per lane.  Each tile's entry count is a
     // multiple of DEPTH (padded on upload), so the refill inside the loop is
     // unconditional: a slot is consumed, then refilled, keeping DEPTH-1 loads in
@@ -187,17 +212,24 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
         u32x4 ring[DEPTH];
 #pragma unroll
         for (int u = 0; u < DEPTH; ++u) ring[u] = load(ent[u * kEntryDwords]);
+        if (TLDS) {
+            u32x4 *dst = (u32x4 *)lds_tab;
+            if ((int)threadIdx.x < n16) dst[threadIdx.x] = apiece;
+            for (int i = threadIdx.x + kBlockThreads; i < n16; i += kBlockThreads) dst[i] = asrc[i];  // > 64 entries
+            __syncthreads();
+        }
         const int last = ecnt - DEPTH;
         for (int e0 = 0; e0 < last; e0 += DEPTH) {
 #pragma unroll
             for (int u = 0; u < DEPTH; ++u) {
                 cu32 *r = ent + (int64_t)(e0 + u) * kEntryDwords;
-                apply_entry(r, ring[u], acc);
+                apply_entry<TLDS>(r, ring[u], acc, ltab + (e0 + u) * kTileRows);
                 ring[u] = load(r[DEPTH * kEntryDwords]);
             }
         }
 #pragma unroll
-        for (int u = 0; u < DEPTH; ++u) apply_entry(ent + (int64_t)(last + u) * kEntryDwords, ring[u], acc);
+        for (int u = 0; u < DEPTH; ++u)
+            apply_entry<TLDS>(ent + (int64_t)(last + u) * kEntryDwords, ring[u], acc, ltab + (last + u) * kTileRows);
     }
 #pragma unroll
     for (int o = 0; o < kTileRows; ++o) {
@@ -211,9 +243,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
     }
 }
 
-// One workgroup = one (stripe, 4 KiB chunk, output tile); single-tile maps.
-template <bool SAFE, bool NTL, bool NTS, int DEPTH>
+// One workgroup = one (stripe, 4 KiB chunk, output tile).  TLDS: dynamic LDS holds
+// the tile's low table dwords (launch_apply sizes it to the longest padded tile).
+template <bool SAFE, bool NTL, bool NTS, int DEPTH, bool TLDS>
 __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
+    extern __shared__ uint2 lds_tab[];
     constexpr int THREADS = kBlockThreads;
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
@@ -226,10 +260,10 @@ __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(
         const int64_t v = a.nbytes - cbase - (int64_t)threadIdx.x * 16;
         valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
     }
-    apply_tile<SAFE, NTL, NTS, DEPTH>(a, plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords,
-                                      uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
-                                      uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)),
-                                      threadIdx.x * 16, valid);
+    apply_tile<SAFE, NTL, NTS, DEPTH, TLDS>(a, plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords,
+                                            uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
+                                            uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)),
+                                            threadIdx.x * 16, valid, lds_tab);
 }
 
 // Multi-tile maps: one workgroup = one (stripe, 1 KiB chunk, tile GROUP), one
@@ -289,7 +323,7 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
         const uint32_t hi = (uint32_t)(k + 1) * G;
         while (next_pos < hi) {
             cu32 *r = ent + (int64_t)e * kEntryDwords;
-            apply_entry(r, stage[buf][next_pos - (uint32_t)k * G][lane], acc);
+            apply_entry<false>(r, stage[buf][next_pos - (uint32_t)k * G][lane], acc, nullptr);
             ++e;
             next_pos = e < ecnt ? r[kEntryDwords + 3] : 0xFFFFFFFFu;
         }
@@ -353,6 +387,8 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.tiles = plan.tiles;
     a.groups = plan.groups;
     a.unions = plan.unions;
+    a.atab = plan.atab;
+    a.lane_zero = 0;
     a.n_groups = cm.n_groups();
     a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;
@@ -384,16 +420,25 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             }
             const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (a.n_tiles == 1 ? 2 : 1) : 0);
             const dim3 blk(kBlockThreads);
-            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false, 4>), grid, blk, 0, stream, a);
+            const bool tlds = !safe && plan.max_tile_entries > 0 && plan.max_tile_entries <= kMaxLdsTileEntries &&
+                              (tu.lds_tables == 2 || (tu.lds_tables == 1 && a.n_tiles > 1));
+            const size_t lds = tlds ? (size_t)plan.max_tile_entries * kAtabDwords * 4 : 0;
+#define ECX_LAUNCH(NTL, NTS, D)                                                                          \
+    do {                                                                                                 \
+        if (tlds) hipLaunchKernelGGL((k_gf_apply<false, NTL, NTS, D, true>), grid, blk, lds, stream, a); \
+        else hipLaunchKernelGGL((k_gf_apply<false, NTL, NTS, D, false>), grid, blk, 0, stream, a);       \
+    } while (0)
+            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false, 4, false>), grid, blk, 0, stream, a);
             else if (depth == 8) {
-                if (ntmode == 2) hipLaunchKernelGGL((k_gf_apply<false, true, true, 8>), grid, blk, 0, stream, a);
-                else if (ntmode == 1) hipLaunchKernelGGL((k_gf_apply<false, false, true, 8>), grid, blk, 0, stream, a);
-                else hipLaunchKernelGGL((k_gf_apply<false, false, false, 8>), grid, blk, 0, stream, a);
+                if (ntmode == 2) ECX_LAUNCH(true, true, 8);
+                else if (ntmode == 1) ECX_LAUNCH(false, true, 8);
+                else ECX_LAUNCH(false, false, 8);
             } else {
-                if (ntmode == 2) hipLaunchKernelGGL((k_gf_apply<false, true, true, 4>), grid, blk, 0, stream, a);
-                else if (ntmode == 1) hipLaunchKernelGGL((k_gf_apply<false, false, true, 4>), grid, blk, 0, stream, a);
-                else hipLaunchKernelGGL((k_gf_apply<false, false, false, 4>), grid, blk, 0, stream, a);
+                if (ntmode == 2) ECX_LAUNCH(true, true, 4);
+                else if (ntmode == 1) ECX_LAUNCH(false, true, 4);
+                else ECX_LAUNCH(false, false, 4);
             }
+#undef ECX_LAUNCH
         }
     };
     run(false, 0, full);

@@ -3,6 +3,8 @@ launch-shape A/B, interleaved rounds in one process, median GB/s (algorithmic
 bytes).  Modes:
     waves   -- k_gf_apply_lds: one workgroup per group of tiles, input union staged via LDS
     tiles   -- k_gf_apply: one workgroup per tile, identity block order (default)
+    tiles_sgpr    -- as tiles, every split-table dword from SGPRs (lds_tables 0)
+    tiles_lds_all -- as tiles, low table dwords from LDS for single-tile maps too (lds_tables 2)
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -42,12 +44,23 @@ def cases(ecx, torch, only):
         out.append(("clay42 encode, 32 KiB", 48 * B * P,
                     lambda pool=pool, par=par, enc=enc, B=B, P=P:
                     enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B), (pool, par, enc)))
+    if only in (None, "clay42rep"):
+        B, P = 32768, 1 << 13
+        pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(pool, pool.numel(), 4)
+        o = torch.empty((P, 8, B), dtype=torch.uint8, device="cuda")
+        rep = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+        out.append(("clay42 repair e=1, 32 KiB (single tile)", 28 * B * P,
+                    lambda pool=pool, o=o, rep=rep, B=B, P=P:
+                    rep.performCodingBatch(pool, 48 * B, B, o, 8 * B, B, P, B), (pool, o, rep)))
     return out
 
 
-MODES = {"waves": {"wave_groups": 1, "xcd_group": 0},
-         "tiles": {"wave_groups": 0, "xcd_group": 0},
-         "tiles2": {"wave_groups": 0, "xcd_group": 2}}
+MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1},
+         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1},
+         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0},
+         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2},
+         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1}}
 
 
 def main():

@@ -574,11 +574,14 @@ def test_lrc_host_batch_matches_device_batch(ecx, torch_dev):
 
 
 @pytest.mark.parametrize("k,m,v,erased,B", [(4, 2, 0, [0, 3], 4096 * 2 + 1000), (4, 2, 0, [4, 5], 3 * 1024),
-                                            (10, 4, 2, [3], 4096), (6, 3, 0, [1, 7], 1024 + 16)])
+                                            (10, 4, 2, [3], 4096), (6, 3, 0, [1, 7], 1024 + 16),
+                                            (4, 2, 0, [1], 4096 * 3)])
 def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
-    """Multi-tile maps: the LDS tile-group kernel (k_gf_apply_lds, 1 KiB chunks +
-    byte-safe tail) and the one-workgroup-per-tile kernel give the same bytes, and
-    both match the oracle on a sampled stripe."""
+    """Every launch shape gives the same bytes: the LDS tile-group kernel
+    (k_gf_apply_lds, 1 KiB chunks + byte-safe tail) and the one-workgroup-per-tile
+    kernel with its split tables read from SGPRs only or partly from LDS
+    (lds_tables 0 / 1 / 2); all match the oracle on a sampled stripe.  The last
+    case is a single-tile map (Clay(4,2) repair)."""
     torch = torch_dev
     step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
     n, a = k + m, step.subPacketSize
@@ -586,14 +589,17 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 31)
     outs = []
-    for wg in (1, 0):
+    for wg, lt in ((1, 1), (0, 0), (0, 1), (0, 2)):
         ecx.tune("wave_groups", wg)
+        ecx.tune("lds_tables", lt)
         o = torch.full((S, len(erased) * a, B), 7, dtype=torch.uint8, device="cuda")
         step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
-    ecx.tune("wave_groups", 0)  # the default
-    assert (outs[0] == outs[1]).all()
+    ecx.tune("wave_groups", 0)  # the defaults
+    ecx.tune("lds_tables", 1)
+    for o in outs[1:]:
+        assert (o == outs[0]).all()
     if v == 0:
         host = pool[S - 1].cpu().numpy()
         inputs = [None if (i % n) in erased else host[i].copy() for i in range(n * a)]
