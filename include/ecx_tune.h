@@ -4,7 +4,7 @@
  * results are bit-identical for every setting, only speed changes.
  *
  *   "depth"            16-B loads per lane in the kernel's load ring: 0 = per map (default:
- *                      8 when every tile has >= 16 entries, else 4), or force 4 / 8
+ *                      8 when every tile has >= 12 entries, else 4), or force 4 / 8
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous
@@ -16,6 +16,8 @@
  *   "lds_tables"       0 = all split-table dwords read as scalars (one v_mov per 8-entry table
  *                      and row); 1 = the low dword of each 8-entry table staged per workgroup
  *                      in LDS, for multi-tile maps (default); 2 = for every map
+ *   "store_scope"      0 = non-temporal output stores (`nt`, default); 1 = `nt sc0 sc1`
+ *                      (system scope: written through, dropped from L2)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -768,6 +768,7 @@ int ecx_tune(const char *key, int value) {
         t.xcd_group = value;
     }
     else if (k == "wave_groups") t.wave_groups = value != 0;
+    else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "lds_tables") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.lds_tables = value;

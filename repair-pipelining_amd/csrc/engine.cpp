@@ -253,7 +253,7 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         const int c = (int)tiles_[(size_t)t * kTileDwords + 1];
         if (c > 0) min_count = std::min(min_count, c);
     }
-    preferred_depth_ = (min_count != (1 << 30) && min_count >= 16) ? 8 : 4;
+    preferred_depth_ = (min_count != (1 << 30) && min_count >= 12) ? 8 : 4;
 }
 
 void CompiledMap::emulate(const uint8_t *in, uint8_t *out, int64_t len, bool via_unions) const {

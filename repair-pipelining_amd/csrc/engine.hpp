@@ -74,8 +74,8 @@ public:
     int union_total() const { return (int)unions_.size(); }                   // unpadded
     int max_in_slot() const { return max_in_slot_; }
     int max_out_slot() const { return max_out_slot_; }
-    // Load-ring depth for this map: 8 when every non-empty tile has >= 16 entries
-    // (padding to a multiple of 8 then costs little), else 4 (profiles/r01_configs_depth.jsonl).
+    // Load-ring depth for this map: 8 when every non-empty tile has >= 12 entries
+    // (padding to a multiple of 8 then costs little), else 4 (profiles/r01_configs_depth.jsonl, r01_configs_sweep2.jsonl).
     int preferred_depth() const { return preferred_depth_; }
     // The plan uploaded for the current device, each tile's entry list padded to a
     // multiple of `depth` with zero-coefficient kDummySlot entries.
@@ -137,6 +137,9 @@ struct Tuning {
     // and row); 1 = the low table dwords staged once per workgroup in LDS and read as
     // VGPRs, for multi-tile maps; 2 = for every map.
     int lds_tables = 1;
+    // Non-temporal output stores: 0 = `nt`; 1 = `nt sc0 sc1` (written through, dropped
+    // from L2; scripts/copy_probe.hip).
+    int store_scope = 0;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

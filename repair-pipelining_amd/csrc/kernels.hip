@@ -48,9 +48,14 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
     return *(const gu32x4 *)p;
 }
 
-template <bool NT>
+// Store policy: 0 plain, 1 non-temporal, 2 non-temporal + sc0 sc1 (system scope:
+// the line is written through and dropped from L2; inline asm, as no builtin sets
+// the scope bits on a store).  Stores are the last vector-memory operations of a
+// tile, so the asm store's vmcnt entry is never waited on by compiler-counted loads.
+template <int NT>
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
-    if (NT) __builtin_nontemporal_store(v, (gu32x4 *)p);
+    if constexpr (NT == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (NT == 1) __builtin_nontemporal_store(v, (gu32x4 *)p);
     else *(gu32x4 *)p = v;
 }
 
@@ -106,6 +111,9 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
                              v1[2], v1[3], v1[4], v1[5], v1[6], v1[7], v2[0], v2[1], v2[2], v2[3],
                              v2[4], v2[5], v2[6], v2[7], v3[0], v3[1], v3[2], v3[3], v3[4], v3[5],
                              v3[6], v3[7], v4[0], v4[1], v4[2], v4[3], v4[4], v4[5], v4[6], v4[7]};
+    // The byte split is computed before the mask is known (issuing it ahead of the
+    // scalar branch hides the plan's s_load latency; wrapping it in `if (mmul)` cost
+    // 20-25 % on the Clay maps).
     const u32x4 i0 = x & 0x07070707u;
     const u32x4 i1 = (x >> 3) & 0x07070707u;
     const u32x4 i2 = (x >> 6) & 0x03030303u;
@@ -125,15 +133,14 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
             acc[o].w = gf_mac4(acc[o].w, t0a, t[1], t1a, t[3], t[4], i0.w, i1.w, i2.w);
         }
     }
-    if (mone) {  // coefficient 1: acc ^= x & mask (one v_bitop3, table 0x78 = a ^ (b & c))
+    // Coefficient 1 (LRC parity, Clay dot nodes): a bare v_xor_b32 per dword for each
+    // such row, behind scalar branches.  (A masked v_bitop3 over all rows would read
+    // the mask from an SGPR, and gfx950 issues a VALU op with an SGPR operand at half
+    // rate: profiles/r01_valu_probe_operands.jsonl.)
+    if (mone) {
 #pragma unroll
-        for (int o = 0; o < kTileRows; ++o) {
-            const uint32_t m = (mone >> o) & 1u ? 0xFFFFFFFFu : 0u;
-            acc[o].x = __builtin_amdgcn_bitop3_b32(acc[o].x, x.x, m, 0x78);
-            acc[o].y = __builtin_amdgcn_bitop3_b32(acc[o].y, x.y, m, 0x78);
-            acc[o].z = __builtin_amdgcn_bitop3_b32(acc[o].z, x.z, m, 0x78);
-            acc[o].w = __builtin_amdgcn_bitop3_b32(acc[o].w, x.w, m, 0x78);
-        }
+        for (int o = 0; o < kTileRows; ++o)
+            if (mone & (1u << o)) acc[o] ^= x;
     }
 }
 
@@ -173,7 +180,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool SAFE, bool NTL, bool NTS, int DEPTH, bool TLDS>
+template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS>
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint64_t in_base, uint64_t out_base,
                                            uint32_t lane16, int valid, uint2 *lds_tab) {
     const uint8_t *ib = reinterpret_cast<const uint8_t *>(in_base) + lane16;
@@ -245,7 +252,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
 
 // One workgroup = one (stripe, 4 KiB chunk, output tile).  TLDS: dynamic LDS holds
 // the tile's low table dwords (launch_apply sizes it to the longest padded tile).
-template <bool SAFE, bool NTL, bool NTS, int DEPTH, bool TLDS>
+template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS>
 __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
     extern __shared__ uint2 lds_tab[];
     constexpr int THREADS = kBlockThreads;
@@ -428,15 +435,24 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         if (tlds) hipLaunchKernelGGL((k_gf_apply<false, NTL, NTS, D, true>), grid, blk, lds, stream, a); \
         else hipLaunchKernelGGL((k_gf_apply<false, NTL, NTS, D, false>), grid, blk, 0, stream, a);       \
     } while (0)
-            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, false, 4, false>), grid, blk, 0, stream, a);
+            const int sts = tu.store_scope ? 2 : 1;  // non-temporal stores: plain nt, or nt sc0 sc1
+            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, 0, 4, false>), grid, blk, 0, stream, a);
             else if (depth == 8) {
-                if (ntmode == 2) ECX_LAUNCH(true, true, 8);
-                else if (ntmode == 1) ECX_LAUNCH(false, true, 8);
-                else ECX_LAUNCH(false, false, 8);
+                if (ntmode == 2) {
+                    if (sts == 2) ECX_LAUNCH(true, 2, 8);
+                    else ECX_LAUNCH(true, 1, 8);
+                } else if (ntmode == 1) {
+                    if (sts == 2) ECX_LAUNCH(false, 2, 8);
+                    else ECX_LAUNCH(false, 1, 8);
+                } else ECX_LAUNCH(false, 0, 8);
             } else {
-                if (ntmode == 2) ECX_LAUNCH(true, true, 4);
-                else if (ntmode == 1) ECX_LAUNCH(false, true, 4);
-                else ECX_LAUNCH(false, false, 4);
+                if (ntmode == 2) {
+                    if (sts == 2) ECX_LAUNCH(true, 2, 4);
+                    else ECX_LAUNCH(true, 1, 4);
+                } else if (ntmode == 1) {
+                    if (sts == 2) ECX_LAUNCH(false, 2, 4);
+                    else ECX_LAUNCH(false, 1, 4);
+                } else ECX_LAUNCH(false, 0, 4);
             }
 #undef ECX_LAUNCH
         }

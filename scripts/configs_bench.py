@@ -1,102 +1,120 @@
 """Secondary measurements: every BASELINE.json config on one MI355X, device
 resident, as achieved algorithmic GB/s of the dominant kernel against the
 8 TB/s HBM peak (BASELINE.md section 3 bytes per unit).  One JSON line per
-config; recorded in DESIGN.md (the bench.py headline is config 2)."""
+config and launch shape; recorded in DESIGN.md (the bench.py headline is config 2).
+
+All configs are set up first (about 100 GB of HBM), then timed in interleaved
+rounds (each round: every config, `--reps` launches after one warm-up launch);
+the reported time is the median round, so clock and thermal drift hit every
+config alike.
+
+    python scripts/configs_bench.py [--rounds 3] [--reps 5] [--sweep]
+"""
+import argparse
+import ctypes
 import json
+import statistics
 import sys
 from pathlib import Path
+
+import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import rpamd  # noqa: E402
 
 PEAK = 8000.0
-
-
-def timed(fn, reps=10):
-    import torch
-    fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e-3
-
-
 SWEEP = [(0, 1), (4, 1), (8, 1), (0, 0)]  # (load-ring depth, nontemporal); first = default (0 = per map)
 
 
-def sweep(lib, name, unit_bytes, units, fn, reps=10, extra=None):
-    """Time fn under each launch shape of SWEEP (results are bit-identical)."""
-    for depth, nt in SWEEP:
-        lib.ecx_tune(b"depth", depth)
-        lib.ecx_tune(b"nontemporal", nt)
-        t = timed(fn, reps)
-        report(name, unit_bytes, units, t, dict(extra or {}, depth=depth, nontemporal=nt))
-    lib.ecx_tune(b"depth", 0)
-    lib.ecx_tune(b"nontemporal", 1)
-
-
-def report(name, unit_bytes, units, sec, extra=None):
-    gbs = unit_bytes * units / sec / 1e9
-    d = {"config": name, "units": units, "bytes_per_unit": unit_bytes, "ms_per_launch": round(sec * 1e3, 3),
-         "GBps": round(gbs, 1), "GiBps": round(unit_bytes * units / sec / 2**30, 1), "frac_of_peak": round(gbs / PEAK, 4)}
-    if extra:
-        d.update(extra)
-    print(json.dumps(d), flush=True)
-
-
-def main():
-    import ctypes
-    import torch
-    ecx = rpamd.load()
-    lib = ecx.lib()
-    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
-    # ---- config 2 encode (stripe generation): Clay(4,2), 32 KiB
+def cases(ecx, torch):
+    out = []
+    # ---- config 2e: Clay(4,2) encode (stripe generation), 32 KiB sub-chunks
     B, P = 32768, 1 << 13
     pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 1)
     par = torch.empty((P, 16, B), dtype=torch.uint8, device="cuda")
     enc = ecx.ClayCodeErasureDecodingStep([4, 5], 4, 2)
-    sweep(lib, "Clay(4,2) encode, 32 KiB (16x32 map)", 32 * B + 16 * B, P,
-          lambda: enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B))
-    del pool, par
-    # ---- config 3: LRC 12+4 XOR groups, 64 KiB blocks: encode and repair of block 2
-    B, S = 65536, 1 << 14
-    pool = torch.empty((S, 16, B), dtype=torch.uint8, device="cuda")
-    ecx.fill_random(pool, pool.numel(), 2)
-    import numpy as np
+    out.append(("Clay(4,2) encode, 32 KiB (16x32 map)", 32 * B + 16 * B, P,
+                lambda: enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B), {}, (pool, par, enc)))
+    # ---- config 3: LRC 12+4 XOR groups, 64 KiB blocks: encode, and repair of block 2
+    B3, S3 = 65536, 1 << 14
+    lpool = torch.empty((S3, 16, B3), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(lpool, lpool.numel(), 2)
     encm = np.zeros((4, 16), np.uint8)
     for g in range(4):
         encm[g, 4 * g:4 * g + 3] = 1
     emap = ecx.GfMap.from_matrix(encm, in_slot=list(range(16)), out_slot=[3, 7, 11, 15])
-    sweep(lib, "LRC encode, 64 KiB blocks", 16 * B, S, lambda: emap.apply_batch(pool, 16 * B, B, pool, 16 * B, B, S, B))
+    out.append(("LRC encode, 64 KiB blocks", 16 * B3, S3,
+                lambda: emap.apply_batch(lpool, 16 * B3, B3, lpool, 16 * B3, B3, S3, B3), {}, (lpool, emap)))
     rmap = ecx.GfMap.from_matrix(np.array([[1, 1, 1]], np.uint8), in_slot=[0, 1, 3], out_slot=[0])
-    out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
-    sweep(lib, "LRC repair of block 2, 64 KiB", 4 * B, S, lambda: rmap.apply_batch(pool, 16 * B, B, out, B, B, S, B))
-    del pool, out
+    lout = torch.empty((S3, 1, B3), dtype=torch.uint8, device="cuda")
+    out.append(("LRC repair of block 2, 64 KiB", 4 * B3, S3,
+                lambda: rmap.apply_batch(lpool, 16 * B3, B3, lout, B3, B3, S3, B3), {}, (lout, rmap)))
     # ---- config 4: shortened Clay(10,4), 1 MiB node block = 256 x 4 KiB, single repair
-    k, m, v, B, S = 10, 4, 2, 4096, 2048
+    k, m, v, B4, S4 = 10, 4, 2, 4096, 2048
     n, a = 14, 256
-    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
-    ecx.fill_random(pool, pool.numel(), 3)
-    out = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
+    cpool = torch.empty((S4, n * a, B4), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(cpool, cpool.numel(), 3)
+    cout = torch.empty((S4, a, B4), dtype=torch.uint8, device="cuda")
     step = ecx.ClayCodeErasureDecodingStep([3], k, m, virtualUnits=v)
     inf = step.map().info()
-    sweep(lib, "Clay(10,4) shortened, 1 MiB blocks, single repair (e=3)", (inf["n_in"] + inf["n_out"]) * B, S,
-          lambda: step.performCodingBatch(pool, n * a * B, B, out, a * B, B, S, B), reps=5, extra={"map": inf})
-    del pool, out
-    # ---- config 5: RS(12,4), 4 MiB shards, erasures {0,1}, in place
-    L, S = 4 << 20, 256
+    out.append(("Clay(10,4) shortened, 1 MiB blocks, single repair (e=3)", (inf["n_in"] + inf["n_out"]) * B4, S4,
+                lambda: step.performCodingBatch(cpool, n * a * B4, B4, cout, a * B4, B4, S4, B4), {"map": inf},
+                (cpool, cout, step)))
+    # ---- config 5: RS(12,4), 4 MiB shards, erasures {0,1}, decoded in place.  A power-of-two
+    # shard pitch puts the 12 streams of one byte position on the same HBM banks; a 4 KiB pad
+    # per shard spreads them (profiles/r01_rs124.jsonl).
+    L, S5 = 4 << 20, 256
     rs = ecx.ReedSolomon.create(12, 4)
-    pool = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
-    ecx.fill_random(pool, pool.numel(), 4)
     dmap = rs.decode_map([False, False] + [True] * 14)
-    sweep(lib, "RS(12,4) 2-erasure decode, 4 MiB", 14 * L, S,
-          lambda: dmap.apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L), reps=5)
+    for pad, label in ((0, "in place, pitch 4 MiB"), (4096, "in place, pitch 4 MiB + 4 KiB")):
+        Lp = L + pad
+        rpool = torch.empty((S5, 16, Lp), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(rpool, rpool.numel(), 4)
+        out.append(("RS(12,4) 2-erasure decode, 4 MiB", 14 * L, S5,
+                    lambda rpool=rpool, Lp=Lp: dmap.apply_batch(rpool, 16 * Lp, Lp, rpool, 16 * Lp, Lp, S5, L),
+                    {"layout": label}, (rpool, dmap, rs)))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sweep", action="store_true", help="also the non-default launch shapes of SWEEP")
+    args = ap.parse_args()
+    import torch
+    ecx = rpamd.load()
+    lib = ecx.lib()
+    lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    cs = cases(ecx, torch)
+    for depth, nt in (SWEEP if args.sweep else SWEEP[:1]):
+        lib.ecx_tune(b"depth", depth)
+        lib.ecx_tune(b"nontemporal", nt)
+        times = {i: [] for i in range(len(cs))}
+        for _ in range(args.rounds):
+            for i, (_name, _ub, _u, fn, _x, _keep) in enumerate(cs):
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                times[i].append(e0.elapsed_time(e1) / args.reps * 1e-3)
+        for i, (name, unit_bytes, units, _fn, extra, _keep) in enumerate(cs):
+            sec = statistics.median(times[i])
+            gbs = unit_bytes * units / sec / 1e9
+            d = {"config": name, "units": units, "bytes_per_unit": unit_bytes, "ms_per_launch": round(sec * 1e3, 3),
+                 "GBps": round(gbs, 1), "GiBps": round(unit_bytes * units / sec / 2**30, 1),
+                 "frac_of_peak": round(gbs / PEAK, 4), "rounds": args.rounds, "reps": args.reps}
+            d.update(extra)
+            d.update(depth=depth, nontemporal=nt)
+            print(json.dumps(d), flush=True)
+    lib.ecx_tune(b"depth", 0)
+    lib.ecx_tune(b"nontemporal", 1)
 
 
 if __name__ == "__main__":

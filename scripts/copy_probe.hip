@@ -1,0 +1,111 @@
+// copy_probe.hip -- which load/store cache policy and which work shape move HBM
+// bytes fastest on MI355X, for a pure copy and for the repair kernel's
+// 20-read : 8-write mix.  Every kernel moves 16 B per lane per access; the store
+// policy is chosen by inline asm (vector stores only).
+//
+//   hipcc --offload-arch=gfx950 -O3 scripts/copy_probe.hip -o scripts/copy_probe && ./scripts/copy_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
+template <int LP>  // 0 plain, 1 nt
+__device__ __forceinline__ u32x4 ld(const uint8_t *p) {
+    if (LP == 1) return __builtin_nontemporal_load((const gu32x4 *)p);
+    return *(const gu32x4 *)p;
+}
+
+template <int SP>  // 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 nt sc1, 5 nt sc0 sc1
+__device__ __forceinline__ void st(uint8_t *p, u32x4 v) {
+    if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+    if constexpr (SP == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+    if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    if constexpr (SP == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+
+// Copy: each workgroup moves 16 KiB (4 x 256 lanes x 16 B).
+template <int LP, int SP>
+__global__ void __launch_bounds__(256) k_copy(const uint8_t *src, uint8_t *dst) {
+    const int64_t base = (int64_t)blockIdx.x * 16384 + threadIdx.x * 16;
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = ld<LP>(src + base + k * 4096);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st<SP>(dst + base + k * 4096, v[k]);
+}
+
+// Repair-shaped mix: one workgroup per 4 KiB chunk of a "stripe" of 28 slots of
+// 32 KiB; reads slots 0..19 (XOR-folded), writes slots 20..27 (8 different values).
+template <int LP, int SP>
+__global__ void __launch_bounds__(256) k_mix(const uint8_t *pool, uint8_t *out) {
+    const int64_t stripe = blockIdx.x >> 3, chunk = blockIdx.x & 7;
+    const uint8_t *in = pool + stripe * (20 * 32768) + chunk * 4096 + threadIdx.x * 16;
+    uint8_t *o = out + stripe * (8 * 32768) + chunk * 4096 + threadIdx.x * 16;
+    u32x4 acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 20; i += 4) {
+        u32x4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = ld<LP>(in + (int64_t)(i + u) * 32768);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[(i + u) & 7] ^= x[u];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st<SP>(o + (int64_t)r * 32768, acc[r]);
+}
+
+template <int LP, int SP>
+void run(const char *lname, const char *sname, uint8_t *a, uint8_t *b, int64_t n) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best_copy = 1e9f, best_mix = 1e9f;
+    const unsigned copy_blocks = (unsigned)(n / 16384);
+    const int64_t stripes = n / (20 * 32768);
+    const unsigned mix_blocks = (unsigned)(stripes * 8);
+    for (int rep = 0; rep < 6; ++rep) {
+        float ms = 0;
+        hipEventRecord(e0);
+        hipLaunchKernelGGL((k_copy<LP, SP>), dim3(copy_blocks), dim3(256), 0, 0, a, b);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best_copy = ms < best_copy ? ms : best_copy;
+        hipEventRecord(e0);
+        hipLaunchKernelGGL((k_mix<LP, SP>), dim3(mix_blocks), dim3(256), 0, 0, a, b);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best_mix = ms < best_mix ? ms : best_mix;
+    }
+    printf("{\"loads\": \"%s\", \"stores\": \"%s\", \"copy_GBps\": %.1f, \"mix20r8w_GBps\": %.1f}\n", lname, sname,
+           2.0 * n / (best_copy * 1e-3) / 1e9, (double)stripes * 28 * 32768 / (best_mix * 1e-3) / 1e9);
+    fflush(stdout);
+}
+
+int main() {
+    const int64_t n = (int64_t)8 << 30;
+    uint8_t *a, *b;
+    if (hipMalloc(&a, n) != hipSuccess || hipMalloc(&b, n) != hipSuccess) return 1;
+    hipMemset(a, 1, n);
+    hipMemset(b, 2, n);
+    hipDeviceSynchronize();
+    run<1, 1>("nt", "nt", a, b, n);
+    run<1, 0>("nt", "plain", a, b, n);
+    run<1, 2>("nt", "sc1", a, b, n);
+    run<1, 3>("nt", "sc0 sc1", a, b, n);
+    run<1, 4>("nt", "sc1 nt", a, b, n);
+    run<1, 5>("nt", "sc0 sc1 nt", a, b, n);
+    run<0, 0>("plain", "plain", a, b, n);
+    run<0, 1>("plain", "nt", a, b, n);
+    run<0, 3>("plain", "sc0 sc1", a, b, n);
+    run<1, 1>("nt", "nt", a, b, n);
+    return 0;
+}

@@ -5,6 +5,7 @@ bytes).  Modes:
     tiles   -- k_gf_apply: one workgroup per tile, identity block order (default)
     tiles_sgpr    -- as tiles, every split-table dword from SGPRs (lds_tables 0)
     tiles_lds_all -- as tiles, low table dwords from LDS for single-tile maps too (lds_tables 2)
+    tiles_sc      -- as tiles, output stores `nt sc0 sc1` (store_scope 1)
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -56,17 +57,18 @@ def cases(ecx, torch, only):
     return out
 
 
-MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1},
-         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1},
-         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0},
-         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2},
-         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1}}
+MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0},
+         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0},
+         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0},
+         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0},
+         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1},
+         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
-    ap.add_argument("--mode", default=None, choices=list(MODES))
+    ap.add_argument("--mode", default=None, help="comma-separated subset of MODES")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
@@ -74,7 +76,7 @@ def main():
     ecx = rpamd.load()
     lib = ecx.lib()
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
-    modes = [args.mode] if args.mode else list(MODES)
+    modes = args.mode.split(",") if args.mode else list(MODES)
     cs = cases(ecx, torch, args.only)
     res = {(c[0], x): [] for c in cs for x in modes}
     for _ in range(args.rounds):
