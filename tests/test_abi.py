@@ -119,3 +119,23 @@ def test_batch_layout_checked_before_any_device_work(ecx):
         with pytest.raises(ecx.EcxError) as e:
             gm.apply_batch_host(t_in, 48 * B, B, out, 8 * B, B, S, B)
         assert e.value.code == -10
+
+
+def test_tuning_keys(ecx):
+    """ecx_tune (include/ecx_tune.h) accepts every documented knob with its valid
+    values, rejects unknown keys and out-of-range values, and is host-only."""
+    lib = ecx.lib()
+    tune = lib.ecx_tune
+    tune.argtypes, tune.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+    header = (ROOT / "include" / "ecx_tune.h").read_text()
+    documented = re.findall(r'^ \*\s+"([a-z_]+)"', header, flags=re.M)
+    defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "wave_groups": 0, "lds_tables": 1, "store_scope": 0,
+                "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 256}
+    assert sorted(documented) == sorted(defaults)
+    for key, val in defaults.items():
+        assert tune(key.encode(), val) == 0, key
+    assert tune(b"no_such_knob", 1) == -1
+    for key, bad in (("depth", 5), ("nontemporal", 3), ("xcd_group", -1), ("lds_tables", 3), ("host_buffers", 9)):
+        assert tune(key.encode(), bad) == -1, key
+    for key, val in defaults.items():  # restore
+        tune(key.encode(), val)
