@@ -14,6 +14,16 @@ sub-chunks read + 8 repaired sub-chunks written = 917,504 B; GiB/s = bytes
 ``cpu_baseline`` times the oracle (the C restatement of the reference's JVM
 path, stage by stage) on this host for a bounded sample: one thread, then one
 thread per host core (oracle/orc_bench.c).
+
+``--workload`` runs the other multi-GPU BASELINE configs with the same
+contract (same launch, timing and JSON line; the default is the headline):
+  clay104  config 4: shortened Clay(10,4), 1 MiB node blocks (256 x 4 KiB sub-chunks),
+           single repair of node 3, 2,048 resident stripes per GPU
+  rs124    config 5: RS(12,4), 4 MiB shards, 2-erasure decode {0,1} in place,
+           512 resident stripes per GPU (shard pitch 4 MiB + 4 KiB, --pitch-pad)
+  lrc      config 3: LRC (12 data, 4 XOR local parities), 64 KiB blocks, repair of
+           data block 2 from its local group, 2^15 resident stripes per GPU
+The cpu_baseline leg runs for the headline workload only.
 """
 import argparse
 import json
@@ -38,19 +48,35 @@ HBM_PEAK_GBS = 8000.0                        # MI355X HBM3E spec (MI355X_MICROAR
 KERNEL = "k_gf_apply<false,true,1,8,false>"  # dominant kernel (SAFE=false, NT loads, NT stores, depth 8, SGPR tables)
 METRIC = "GiB/s repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU"
 
+# workload -> (metric, default resident pool per GPU, default stripes per step per GPU)
+WORKLOADS = {
+    "clay42": (METRIC, 1 << 15, 1 << 20),
+    "clay104": ("GiB/s repair-decode (device-resident), Clay(10,4) 1 MiB blocks, 1/2/4/8 GPU", 2048, 1 << 15),
+    "rs124": ("GiB/s 2-erasure decode (device-resident), RS(12,4) 4 MiB blocks, 1/2/4/8 GPU", 512, 4096),
+    "lrc": ("GiB/s local-group repair (device-resident), LRC(12,4) 64 KiB blocks, 1/2/4/8 GPU", 1 << 15, 1 << 18),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--stripes-per-step", type=int, default=1 << 20)
-    ap.add_argument("--pool", type=int, default=1 << 15, help="resident stripes per GPU (48 GiB at 2^15)")
-    ap.add_argument("--erased", type=int, default=1, help="erased node (README: '1 LP 1 pipeline')")
+    ap.add_argument("--workload", default="clay42", choices=list(WORKLOADS))
+    ap.add_argument("--stripes-per-step", type=int, default=None, help="default: per workload (2^20 for clay42)")
+    ap.add_argument("--pool", type=int, default=None, help="resident stripes per GPU (clay42: 2^15 = 48 GiB)")
+    ap.add_argument("--erased", type=int, default=None, help="erased node (clay42: 1, README '1 LP 1 pipeline')")
+    ap.add_argument("--pitch-pad", type=int, default=4096, help="rs124: bytes of padding per 4 MiB shard")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample; 0 = skip")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-probes", action="store_true", help="skip the in-run memory ceiling probes")
-    return ap.parse_args()
+    args = ap.parse_args()
+    _metric, pool, per_step = WORKLOADS[args.workload]
+    args.pool = args.pool or pool
+    args.stripes_per_step = args.stripes_per_step or per_step
+    if args.erased is None:
+        args.erased = {"clay42": 1, "clay104": 3}.get(args.workload, 0)
+    return args
 
 
 def _cpu_model() -> str:
@@ -126,12 +152,12 @@ def pmc_traffic(pool: int):
     return None
 
 
-def memory_probes(ecx, torch, pool, reps: int = 5):
+def memory_probes(ecx, torch, region, reads: int, writes: int, reps: int = 5):
     """In-run memory ceilings on this GPU: NT read stream, NT copy
     kernel, hipMemcpyDtoD (torch copy_), each the best of `reps` over 8 GiB regions of
     the (already verified and timed) pool.  The mix model prices this workload's
-    20-read : 8-write bytes from the read and copy probes."""
-    flat = pool.view(-1)
+    reads : writes streams from the read and copy probes."""
+    flat = region.view(-1)
     n = min(8 << 30, flat.numel() // 2) // 16384 * 16384
     src, dst = flat[:n], flat[n:2 * n]
 
@@ -150,9 +176,150 @@ def memory_probes(ecx, torch, pool, reps: int = 5):
     cp = best(lambda: ecx.probe_bandwidth(1, src, dst, n, True), 2 * n)
     dd = best(lambda: dst.copy_(src), 2 * n)
     w = 1.0 / (2.0 / cp - 1.0 / rd)  # write-equivalent rate implied by the copy probe
-    mix = (20 + 8) / (20 / rd + 8 / w)
+    mix = (reads + writes) / (reads / rd + writes / w)
     return {"read_probe_GBps": round(rd, 1), "copy_probe_GBps": round(cp, 1), "dtod_copy_GBps": round(dd, 1),
             "mix_model_GBps": round(mix, 1)}
+
+
+class Workload:
+    """A resident pool of valid stripes and one batch launch over all of it."""
+    unit_bytes = ALGO_BYTES           # algorithmic bytes per stripe (BASELINE.md section 3)
+    write_bytes = WRITE_BYTES         # of which written
+    reads, writes = 20, 8             # equal-sized streams read / written per unit (mix model)
+    kernel = KERNEL
+    description = ""
+
+    def launch(self):
+        raise NotImplementedError
+
+    def verify(self) -> bool:
+        raise NotImplementedError
+
+
+class Clay42(Workload):
+    """Config 2 (headline): Clay(4,2), B = 32 KiB, single-node repair."""
+
+    def __init__(self, ecx, torch, dev, P, erased, seed):
+        self.P, self.erased, self.torch = P, erased, torch
+        self.pool = torch.empty((P, N_NODES * ALPHA, B), dtype=torch.uint8, device=dev)
+        self.out = torch.empty((P, ALPHA, B), dtype=torch.uint8, device=dev)
+        par = torch.empty((P, M * ALPHA, B), dtype=torch.uint8, device=dev)
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
+        enc = ecx.ClayCodeErasureDecodingStep(list(range(K, N_NODES)), K, M)
+        enc.performCodingBatch(self.pool, STRIPE_BYTES, B, par, M * ALPHA * B, B, P, B)
+        self.pool.view(P, ALPHA, N_NODES, B)[:, :, K:, :] = par.view(P, ALPHA, M, B)
+        del par
+        self.step = ecx.ClayCodeErasureDecodingStep([erased], K, M)
+        self.region = self.pool
+        self.description = "Clay(4,2) single-node repair (erased node %d), CLAY_BLOCK_SIZE=32768" % erased
+
+    def launch(self):
+        self.step.performCodingBatch(self.pool, STRIPE_BYTES, B, self.out, ALPHA * B, B, self.P, B)
+
+    def verify(self):
+        return bool(self.torch.equal(self.out, self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.erased, :]))
+
+
+class Clay104(Workload):
+    """Config 4: shortened Clay(10,4) (Clay(12,4) with 2 virtual zero data nodes),
+    1 MiB node blocks = 256 planes x 4 KiB sub-chunks, single-node repair."""
+    k, m, v, b, alpha = 10, 4, 2, 4096, 256
+    kernel = "k_gf_apply<false,false,1,8,true>"
+
+    def __init__(self, ecx, torch, dev, P, erased, seed):
+        k, m, v, b, a = self.k, self.m, self.v, self.b, self.alpha
+        n = k + m
+        self.P, self.erased, self.torch, self.n = P, erased, torch, n
+        self.pool = torch.empty((P, n * a, b), dtype=torch.uint8, device=dev)
+        self.out = torch.empty((P, a, b), dtype=torch.uint8, device=dev)
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
+        enc = ecx.ClayCodeErasureDecodingStep(list(range(k, n)), k, m, virtualUnits=v)
+        par = torch.empty((P, m * a, b), dtype=torch.uint8, device=dev)
+        enc.performCodingBatch(self.pool, n * a * b, b, par, m * a * b, b, P, b)
+        self.pool.view(P, a, n, b)[:, :, k:, :] = par.view(P, a, m, b)
+        del par
+        self.step = ecx.ClayCodeErasureDecodingStep([erased], k, m, virtualUnits=v)
+        info = self.step.map().info()
+        self.unit_bytes = (info["n_in"] + info["n_out"]) * b  # 832 helper + 256 repaired sub-chunks
+        self.write_bytes = info["n_out"] * b
+        self.reads, self.writes = info["n_in"], info["n_out"]
+        self.region = self.pool
+        self.description = ("Clay(10,4) (shortened Clay(12,4), 2 virtual nodes) single-node repair (erased node %d), "
+                            "1 MiB node blocks = 256 x 4096-B sub-chunks" % erased)
+
+    def launch(self):
+        n, a, b = self.n, self.alpha, self.b
+        self.step.performCodingBatch(self.pool, n * a * b, b, self.out, a * b, b, self.P, b)
+
+    def verify(self):
+        orig = self.pool.view(self.P, self.alpha, self.n, self.b)[:, :, self.erased, :]
+        return bool(self.torch.equal(self.out, orig))
+
+
+class RS124(Workload):
+    """Config 5: RS(12,4), 4 MiB shards, erasures {0,1} decoded in place (the first 12
+    present shards, ReedSolomon.decodeMissing)."""
+    k, m, L = 12, 4, 4 << 20
+    reads, writes = 12, 2
+    unit_bytes = 14 * (4 << 20)
+    write_bytes = 2 * (4 << 20)
+    kernel = "k_gf_apply<false,true,1,8,false>"
+
+    def __init__(self, ecx, torch, dev, P, pad, seed):
+        self.P, self.torch, self.pitch = P, torch, self.L + pad
+        rs = ecx.ReedSolomon.create(self.k, self.m)
+        p, L = self.pitch, self.L
+        self.pool = torch.empty((P, 16, p), dtype=torch.uint8, device=dev)
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
+        rs.encode_map().apply_batch(self.pool, 16 * p, p, self.pool, 16 * p, p, P, L)
+        self.orig = self.pool[:, 0:2, :L].clone()
+        self.pool[:, 0:2, :L] = 0  # the erased shards
+        self.rs = rs
+        self.dmap = rs.decode_map([False, False] + [True] * 14)
+        self.region = self.pool
+        self.description = "RS(12,4) 2-erasure decode {0,1} in place, 4 MiB shards, shard pitch %d B" % p
+
+    def launch(self):
+        p = self.pitch
+        self.dmap.apply_batch(self.pool, 16 * p, p, self.pool, 16 * p, p, self.P, self.L)
+
+    def verify(self):
+        return bool(self.torch.equal(self.pool[:, 0:2, :self.L], self.orig))
+
+
+class LRC(Workload):
+    """Config 3: LRC (LRCErasureCodeExample shapes: 12 data blocks in 4 local groups of 3,
+    each with an XOR parity), 64 KiB blocks; repair of data block 2 from its group."""
+    b = 65536
+    reads, writes = 3, 1
+    unit_bytes = 4 * 65536
+    write_bytes = 65536
+    kernel = "k_gf_apply<false,true,1,4,false>"
+
+    def __init__(self, ecx, torch, dev, P, seed):
+        import numpy as np
+        b = self.b
+        self.P, self.torch = P, torch
+        self.pool = torch.empty((P, 16, b), dtype=torch.uint8, device=dev)
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
+        enc = np.zeros((4, 16), np.uint8)
+        for g in range(4):
+            enc[g, 4 * g:4 * g + 3] = 1
+        ecx.GfMap.from_matrix(enc, in_slot=list(range(16)), out_slot=[3, 7, 11, 15]).apply_batch(
+            self.pool, 16 * b, b, self.pool, 16 * b, b, P, b)
+        rs = ecx.ReedSolomon.create(3, 1)
+        mat, _ins, _outs = rs.decode_map([True, True, False, True]).matrix()
+        self.rmap = ecx.GfMap.from_matrix(mat, in_slot=[0, 1, 3], out_slot=[0])
+        self.out = torch.empty((P, 1, b), dtype=torch.uint8, device=dev)
+        self.region = self.pool
+        self.description = "LRC(12 data, 4 XOR local parities) repair of data block 2, 64 KiB blocks"
+
+    def launch(self):
+        b = self.b
+        self.rmap.apply_batch(self.pool, 16 * b, b, self.out, b, b, self.P, b)
+
+    def verify(self):
+        return bool(self.torch.equal(self.out[:, 0], self.pool[:, 2]))
 
 
 def main():
@@ -183,32 +350,29 @@ def main():
     P = args.pool
     passes = max(1, args.stripes_per_step // P)
     stripes_per_step = passes * P
+    seed = 0x5EED + rank
 
-    # ---- resident pool of valid Clay(4,2) stripes: random data + GPU encode
-    pool = torch.empty((P, N_NODES * ALPHA, B), dtype=torch.uint8, device=dev)
-    out = torch.empty((P, ALPHA, B), dtype=torch.uint8, device=dev)
-    par = torch.empty((P, M * ALPHA, B), dtype=torch.uint8, device=dev)
-    ecx.fill_random(pool, pool.numel(), 0x5EED + rank)
-    enc = ecx.ClayCodeErasureDecodingStep(list(range(K, N_NODES)), K, M)
-    enc.performCodingBatch(pool, STRIPE_BYTES, B, par, M * ALPHA * B, B, P, B)
-    pool.view(P, ALPHA, N_NODES, B)[:, :, K:, :] = par.view(P, ALPHA, M, B)
-    del par
-    step_obj = ecx.ClayCodeErasureDecodingStep([args.erased], K, M)
+    # ---- resident pool of valid stripes: random data + GPU encode
+    if args.workload == "clay42":
+        wl = Clay42(ecx, torch, dev, P, args.erased, seed)
+    elif args.workload == "clay104":
+        wl = Clay104(ecx, torch, dev, P, args.erased, seed)
+    elif args.workload == "rs124":
+        wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed)
+    else:
+        wl = LRC(ecx, torch, dev, P, seed)
 
-    def repair():
-        step_obj.performCodingBatch(pool, STRIPE_BYTES, B, out, ALPHA * B, B, P, B)
-
-    repair()
+    wl.launch()
     torch.cuda.synchronize()
     verified = None
     if not args.no_verify:
-        verified = bool(torch.equal(out, pool.view(P, ALPHA, N_NODES, B)[:, :, args.erased, :]))
+        verified = wl.verify()
         if not verified:
-            raise SystemExit("repair output differs from the erased node's original sub-chunks")
+            raise SystemExit("repair output differs from the erased originals")
 
     for _ in range(args.warmup):
         for _ in range(passes):
-            repair()
+            wl.launch()
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -222,7 +386,7 @@ def main():
     for _ in range(args.steps):
         for _ in range(passes):
             evs[i][0].record(stream)
-            repair()
+            wl.launch()
             evs[i][1].record(stream)
             i += 1
     torch.cuda.synchronize()
@@ -235,16 +399,16 @@ def main():
         el = float(t.item())
 
     launch_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-    per_launch_bytes = P * ALGO_BYTES
+    per_launch_bytes = P * wl.unit_bytes
     achieved = per_launch_bytes / (launch_ms * 1e-3) / 1e9
     total_stripes = stripes_per_step * args.steps * world
-    value = total_stripes * ALGO_BYTES / el / 2**30
-    traffic = pmc_traffic(P)
+    value = total_stripes * wl.unit_bytes / el / 2**30
+    traffic = pmc_traffic(P) if args.workload == "clay42" else None
 
     sample = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:  # one repaired stripe for the oracle check
-        sample = (pool[P // 2].cpu().numpy(), out[P // 2].cpu().numpy())
-    probes = memory_probes(ecx, torch, pool) if not args.no_probes else None
+    if args.workload == "clay42" and rank == 0 and world == 1 and args.cpu_seconds > 0:
+        sample = (wl.pool[P // 2].cpu().numpy(), wl.out[P // 2].cpu().numpy())  # one stripe for the oracle check
+    probes = memory_probes(ecx, torch, wl.region, wl.reads, wl.writes) if not args.no_probes else None
 
     cpu = None
     if sample is not None:
@@ -252,7 +416,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": WORKLOADS[args.workload][0],
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -263,11 +427,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (device splitmix64 data, GPU Clay(4,2) encode -> valid stripes)",
+            "data": "synthetic (device splitmix64 data, GPU encode -> valid stripes)",
             "config": {
-                "workload": "Clay(4,2) single-node repair (erased node %d), CLAY_BLOCK_SIZE=32768, "
-                            "%d stripes per GPU per step over a resident pool of %d" % (args.erased,
-                                                                                         stripes_per_step, P),
+                "workload": "%s, %d stripes per GPU per step over a resident pool of %d" % (wl.description,
+                                                                                            stripes_per_step, P),
                 "global_batch": stripes_per_step * world,
                 "parallelism": "stripe-partitioned dp%d (no data-path collective)" % world,
             },
@@ -278,13 +441,13 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": KERNEL,
+                "kernel": wl.kernel,
                 "avg_launch_ms": round(launch_ms, 4),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "measured_ceilings": probes,
                 "frac_of_mix_model": round(achieved / probes["mix_model_GBps"], 4) if probes else None,
             },
-            "repaired_output_GiBps": round(total_stripes * WRITE_BYTES / el / 2**30, 3),
+            "repaired_output_GiBps": round(total_stripes * wl.write_bytes / el / 2**30, 3),
             "cpu_baseline": cpu,
             "verified": verified,
         }

@@ -121,6 +121,7 @@ struct ApplyArgs {
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
     int lane_zero;        // always 0 (keeps k_gf_apply's LDS table base in a VGPR)
+    int chunk_major;      // k_gf_apply block order: 0 = stripe by stripe, 1 = chunk c of every stripe, then c + 1
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -140,6 +141,8 @@ struct Tuning {
     // Non-temporal output stores: 0 = `nt`; 1 = `nt sc0 sc1` (written through, dropped
     // from L2; scripts/copy_probe.hip).
     int store_scope = 0;
+    // k_gf_apply block order: 0 = stripe-major (a stripe's chunks back to back), 1 = chunk-major.
+    int chunk_major = 0;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -259,8 +259,11 @@ __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
-    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
-    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+    // chunk_major: consecutive units take the same chunk of consecutive stripes
+    // (a launch covers whole stripes, so gridDim.x / (n_tiles * n_chunks) is its stripe count).
+    const uint32_t nst = gridDim.x / ((uint32_t)a.n_tiles * (uint32_t)a.n_chunks);
+    const int64_t c = a.chunk_begin + (int64_t)(a.chunk_major ? rest / nst : rest % (uint32_t)a.n_chunks);
+    const int64_t s = a.stripe_begin + (int64_t)(a.chunk_major ? rest % nst : rest / (uint32_t)a.n_chunks);
     const int64_t cbase = c * (THREADS * 16);
     int valid = 16;
     if (SAFE) {
@@ -396,6 +399,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.unions = plan.unions;
     a.atab = plan.atab;
     a.lane_zero = 0;
+    a.chunk_major = tuning().chunk_major;
     a.n_groups = cm.n_groups();
     a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;

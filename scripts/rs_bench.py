@@ -1,7 +1,8 @@
 """RS(12,4) 2-erasure decode (BASELINE config 5) launch/layout A/B, interleaved
 rounds in one process, median algorithmic GB/s (12 shards read + 2 written per
 stripe).  Variants: in place vs separate output, shard pitch L vs L + 4 KiB,
-shard length 4 MiB / 1 MiB / 256 KiB (same total bytes), ring depth 4 vs 8."""
+shard length 4 MiB / 1 MiB / 256 KiB (same total bytes), ring depth 4 vs 8, and
+block order stripe-major vs chunk-major (ecx_tune "chunk_major")."""
 import json
 import statistics
 import sys
@@ -32,11 +33,13 @@ def main():
         name = f"L={L >> 10}KiB pitch=L+{pad} {'in-place' if inplace else 'separate out'}"
         cases.append((name, S * 14 * L, lambda buf=buf, out=out, S=S, pitch=pitch, L=L, ost=ost, osl=osl:
                       dmap.apply_batch(buf, 16 * pitch, pitch, out, ost, osl, S, L)))
-    res = {(c[0], d): [] for c in cases for d in (0, 4, 8)}
+    shapes = [(d, cm) for d in (0, 4, 8) for cm in (0, 1)]
+    res = {(c[0], s): [] for c in cases for s in shapes}
     for _ in range(3):
         for name, nbytes, fn in cases:
-            for d in (0, 4, 8):
+            for d, cm in shapes:
                 ecx.tune("depth", d)
+                ecx.tune("chunk_major", cm)
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -45,11 +48,12 @@ def main():
                     fn()
                 e1.record()
                 torch.cuda.synchronize()
-                res[(name, d)].append(nbytes / (e0.elapsed_time(e1) / 5 * 1e-3) / 1e9)
+                res[(name, (d, cm))].append(nbytes / (e0.elapsed_time(e1) / 5 * 1e-3) / 1e9)
     ecx.tune("depth", 0)
-    for (name, d), v in res.items():
+    ecx.tune("chunk_major", 0)
+    for (name, (d, cm)), v in res.items():
         med = statistics.median(v)
-        print(json.dumps({"case": "RS(12,4) decode {0,1}, " + name, "depth": d or "auto",
+        print(json.dumps({"case": "RS(12,4) decode {0,1}, " + name, "depth": d or "auto", "chunk_major": cm,
                           "GBps_median": round(med, 1), "frac": round(med / 8000, 4)}), flush=True)
 
 

@@ -580,7 +580,8 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     """Every launch shape gives the same bytes: the LDS tile-group kernel
     (k_gf_apply_lds, 1 KiB chunks + byte-safe tail) and the one-workgroup-per-tile
     kernel with its split tables read from SGPRs only or partly from LDS
-    (lds_tables 0 / 1 / 2) and with `nt sc0 sc1` output stores; all match the oracle on a sampled stripe.  The last
+    (lds_tables 0 / 1 / 2), with `nt sc0 sc1` output stores and in chunk-major
+    block order; all match the oracle on a sampled stripe.  The last
     case is a single-tile map (Clay(4,2) repair)."""
     torch = torch_dev
     step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
@@ -589,10 +590,11 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 31)
     outs = []
-    for wg, lt, sc in ((1, 1, 0), (0, 0, 0), (0, 1, 0), (0, 2, 0), (0, 1, 1)):
+    for wg, lt, sc, cm in ((1, 1, 0, 0), (0, 0, 0, 0), (0, 1, 0, 0), (0, 2, 0, 0), (0, 1, 1, 0), (0, 1, 0, 1)):
         ecx.tune("wave_groups", wg)
         ecx.tune("lds_tables", lt)
         ecx.tune("store_scope", sc)
+        ecx.tune("chunk_major", cm)
         o = torch.full((S, len(erased) * a, B), 7, dtype=torch.uint8, device="cuda")
         step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
         torch.cuda.synchronize()
@@ -600,6 +602,7 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     ecx.tune("wave_groups", 0)  # the defaults
     ecx.tune("lds_tables", 1)
     ecx.tune("store_scope", 0)
+    ecx.tune("chunk_major", 0)
     for o in outs[1:]:
         assert (o == outs[0]).all()
     if v == 0:
