@@ -830,14 +830,26 @@ int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
                 for (int64_t i = 0; i < len; ++i)
                     ref[(size_t)m.out_slot[o] * len + i] ^= f.mul(c, in[(size_t)m.in_slot[j] * len + i]);
             }
-        for (bool via_unions : {false, true}) {
-            std::vector<uint8_t> got(ref.size(), 0);
-            cm.emulate(in.data(), got.data(), len, via_unions);
+        auto check = [&](const std::vector<uint8_t> &got, const char *what) {
             for (int o = 0; o < m.n_out; ++o)
                 if (!std::equal(got.begin() + (size_t)m.out_slot[o] * len, got.begin() + (size_t)(m.out_slot[o] + 1) * len,
                                 ref.begin() + (size_t)m.out_slot[o] * len))
-                    throw Error(ECX_E_ILLEGAL_ARGUMENT, via_unions ? "plan (union view) differs from the map"
-                                                                   : "plan (slot view) differs from the map");
+                    throw Error(ECX_E_ILLEGAL_ARGUMENT, what);
+        };
+        for (bool via_unions : {false, true}) {
+            std::vector<uint8_t> got(ref.size(), 0);
+            cm.emulate(in.data(), got.data(), len, via_unions);
+            check(got, via_unions ? "plan (union view) differs from the map" : "plan (slot view) differs from the map");
+        }
+        // The padded arrays the device receives, at both ring depths, with the split
+        // tables read as k_gf_apply reads them (SGPRs only, or low dwords from LDS).
+        for (int depth : {4, 8}) {
+            const HostPlan hp = cm.padded_plan(depth);
+            for (bool tlds : {false, true}) {
+                std::vector<uint8_t> got(ref.size(), 0);
+                cm.emulate_padded(hp, in.data(), got.data(), len, tlds);
+                check(got, tlds ? "padded plan (LDS tables) differs from the map" : "padded plan differs from the map");
+            }
         }
         return ECX_OK;
     });

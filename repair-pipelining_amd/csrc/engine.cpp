@@ -325,63 +325,104 @@ CompiledMap::~CompiledMap() {
     }
 }
 
+HostPlan CompiledMap::padded_plan(int depth) const {
+    HostPlan p;
+    // Pad each tile to a multiple of `depth` entries so the kernel's load ring
+    // runs branch-free (engine.hpp); padding entries load the zero page.
+    p.tiles = tiles_;
+    for (int t = 0; t < n_tiles_; ++t) {
+        uint32_t *tile = p.tiles.data() + (size_t)t * kTileDwords;
+        const uint32_t begin = tile[0], count = tile[1];
+        tile[0] = (uint32_t)(p.entries.size() / kEntryDwords);
+        p.entries.insert(p.entries.end(), entries_.begin() + (size_t)begin * kEntryDwords,
+                         entries_.begin() + (size_t)(begin + count) * kEntryDwords);
+        const uint32_t padded = count == 0 ? 0 : (count + depth - 1) / depth * depth;
+        for (uint32_t d = count; d < padded; ++d) {
+            uint32_t rec[kEntryDwords] = {0};
+            rec[0] = kDummySlot;
+            p.entries.insert(p.entries.end(), rec, rec + kEntryDwords);
+        }
+        tile[1] = padded;
+        p.max_tile_entries = std::max(p.max_tile_entries, (int)padded);
+    }
+    if (p.entries.empty()) p.entries.assign(kEntryDwords, 0);
+    for (size_t e = 0; e < p.entries.size() / kEntryDwords; ++e)
+        for (int r = 0; r < kTileRows; ++r) {
+            p.atab.push_back(p.entries[e * kEntryDwords + 4 + 5 * r]);      // T0a
+            p.atab.push_back(p.entries[e * kEntryDwords + 4 + 5 * r + 2]);  // T1a
+        }
+    // Unions: each group's list padded with zero-page entries to a multiple of
+    // group_size * depth, i.e. whole stages of the LDS kernel's load ring.
+    p.groups = groups_;
+    const int gsz = std::max(1, group_size_);
+    for (int g = 0; g < n_groups_; ++g) {
+        uint32_t *rec = p.groups.data() + (size_t)g * kGroupDwords;
+        const uint32_t begin = rec[8], count = rec[9];
+        rec[8] = (uint32_t)p.unions.size();
+        p.unions.insert(p.unions.end(), unions_.begin() + begin, unions_.begin() + begin + count);
+        const uint32_t quantum = (uint32_t)(gsz * depth);
+        const uint32_t padded = (count + quantum - 1) / quantum * quantum;
+        p.unions.resize(p.unions.size() + (padded - count), kDummySlot);
+        rec[9] = padded;
+    }
+    if (p.unions.empty()) p.unions.assign(1, kDummySlot);
+    return p;
+}
+
+void CompiledMap::emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds) const {
+    auto table_byte = [](uint32_t lo, uint32_t hi, int idx) {
+        return (uint8_t)((idx < 4 ? lo : hi) >> (8 * (idx & 3)));
+    };
+    std::vector<uint8_t> acc((size_t)kTileRows * len);
+    for (int t = 0; t < n_tiles_; ++t) {
+        const uint32_t *tile = p.tiles.data() + (size_t)t * kTileDwords;
+        std::fill(acc.begin(), acc.end(), 0);
+        if (tile[1] % 4) throw Error(ECX_E_ILLEGAL_ARGUMENT, "tile entry count not padded to the ring depth");
+        for (uint32_t e = 0; e < tile[1]; ++e) {
+            const size_t ei = (size_t)tile[0] + e;
+            const uint32_t *rec = p.entries.data() + ei * kEntryDwords;
+            if (rec[0] == kDummySlot) {
+                if (rec[1] | rec[2]) throw Error(ECX_E_ILLEGAL_ARGUMENT, "padding entry with coefficients");
+                continue;  // reads the zero page: contributes nothing
+            }
+            const uint8_t *x = in + (int64_t)rec[0] * len;
+            for (int r = 0; r < (int)tile[2]; ++r) {
+                uint8_t *a = acc.data() + (size_t)r * len;
+                if (rec[2] & (1u << r))
+                    for (int64_t i = 0; i < len; ++i) a[i] ^= x[i];
+                if (rec[1] & (1u << r)) {
+                    const uint32_t *tb = rec + 4 + 5 * r;
+                    const uint32_t t0a = tlds ? p.atab[ei * kAtabDwords + 2 * r] : tb[0];
+                    const uint32_t t1a = tlds ? p.atab[ei * kAtabDwords + 2 * r + 1] : tb[2];
+                    for (int64_t i = 0; i < len; ++i)
+                        a[i] ^= table_byte(t0a, tb[1], x[i] & 7) ^ table_byte(t1a, tb[3], (x[i] >> 3) & 7) ^
+                                table_byte(tb[4], tb[4], x[i] >> 6);
+                }
+            }
+        }
+        for (int r = 0; r < (int)tile[2]; ++r)
+            std::copy(acc.begin() + (size_t)r * len, acc.begin() + (size_t)(r + 1) * len, out + (int64_t)tile[4 + r] * len);
+    }
+}
+
 const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     int dev = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
     std::lock_guard<std::mutex> lk(mu_);
     auto it = dev_.find({dev, depth});
     if (it != dev_.end()) return it->second;
-    // Pad each tile to a multiple of `depth` entries so the kernel's load ring
-    // runs branch-free (engine.hpp); padding entries load the zero page.
-    std::vector<uint32_t> ents, tiles = tiles_;
-    for (int t = 0; t < n_tiles_; ++t) {
-        uint32_t *tile = tiles.data() + (size_t)t * kTileDwords;
-        const uint32_t begin = tile[0], count = tile[1];
-        tile[0] = (uint32_t)(ents.size() / kEntryDwords);
-        ents.insert(ents.end(), entries_.begin() + (size_t)begin * kEntryDwords,
-                    entries_.begin() + (size_t)(begin + count) * kEntryDwords);
-        const uint32_t padded = count == 0 ? 0 : (count + depth - 1) / depth * depth;
-        for (uint32_t d = count; d < padded; ++d) {
-            uint32_t rec[kEntryDwords] = {0};
-            rec[0] = kDummySlot;
-            ents.insert(ents.end(), rec, rec + kEntryDwords);
-        }
-        tile[1] = padded;
-    }
-    if (ents.empty()) ents.assign(kEntryDwords, 0);
+    const HostPlan h = padded_plan(depth);
     DevicePlan p;
-    std::vector<uint32_t> atab;
-    for (size_t e = 0; e < ents.size() / kEntryDwords; ++e)
-        for (int r = 0; r < kTileRows; ++r) {
-            atab.push_back(ents[e * kEntryDwords + 4 + 5 * r]);      // T0a
-            atab.push_back(ents[e * kEntryDwords + 4 + 5 * r + 2]);  // T1a
-        }
-    for (int t = 0; t < n_tiles_; ++t) p.max_tile_entries = std::max(p.max_tile_entries, (int)tiles[(size_t)t * kTileDwords + 1]);
-    check_hip(hipMalloc(&p.atab, atab.size() * 4), "hipMalloc(plan atab)");
-    check_hip(hipMemcpy(p.atab, atab.data(), atab.size() * 4, hipMemcpyHostToDevice), "plan upload");
-    check_hip(hipMalloc(&p.entries, ents.size() * 4), "hipMalloc(plan entries)");
-    check_hip(hipMalloc(&p.tiles, tiles.size() * 4), "hipMalloc(plan tiles)");
-    // Unions: each group's list padded with zero-page entries to a multiple of
-    // group_size * depth, i.e. whole stages of the LDS kernel's load ring.
-    std::vector<uint32_t> groups = groups_, unions;
-    const int gsz = std::max(1, group_size_);
-    for (int g = 0; g < n_groups_; ++g) {
-        uint32_t *rec = groups.data() + (size_t)g * kGroupDwords;
-        const uint32_t begin = rec[8], count = rec[9];
-        rec[8] = (uint32_t)unions.size();
-        unions.insert(unions.end(), unions_.begin() + begin, unions_.begin() + begin + count);
-        const uint32_t quantum = (uint32_t)(gsz * depth);
-        const uint32_t padded = (count + quantum - 1) / quantum * quantum;
-        unions.resize(unions.size() + (padded - count), kDummySlot);
-        rec[9] = padded;
-    }
-    if (unions.empty()) unions.assign(1, kDummySlot);
-    check_hip(hipMalloc(&p.groups, groups.size() * 4), "hipMalloc(plan groups)");
-    check_hip(hipMemcpy(p.groups, groups.data(), groups.size() * 4, hipMemcpyHostToDevice), "plan upload");
-    check_hip(hipMalloc(&p.unions, unions.size() * 4), "hipMalloc(plan unions)");
-    check_hip(hipMemcpy(p.unions, unions.data(), unions.size() * 4, hipMemcpyHostToDevice), "plan upload");
-    check_hip(hipMemcpy(p.entries, ents.data(), ents.size() * 4, hipMemcpyHostToDevice), "plan upload");
-    check_hip(hipMemcpy(p.tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    p.max_tile_entries = h.max_tile_entries;
+    auto upload = [](uint32_t **dst, const std::vector<uint32_t> &src, const char *what) {
+        check_hip(hipMalloc(dst, src.size() * 4), what);
+        check_hip(hipMemcpy(*dst, src.data(), src.size() * 4, hipMemcpyHostToDevice), "plan upload");
+    };
+    upload(&p.entries, h.entries, "hipMalloc(plan entries)");
+    upload(&p.tiles, h.tiles, "hipMalloc(plan tiles)");
+    upload(&p.groups, h.groups, "hipMalloc(plan groups)");
+    upload(&p.unions, h.unions, "hipMalloc(plan unions)");
+    upload(&p.atab, h.atab, "hipMalloc(plan atab)");
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;
 }
 

@@ -55,6 +55,14 @@ struct DevicePlan {
 constexpr int kAtabDwords = 2 * kTileRows;
 constexpr int kMaxLdsTileEntries = 512;  // 32 KiB of LDS per workgroup at most
 
+// The padded plan exactly as uploaded to a device for one load-ring depth
+// (CompiledMap::padded_plan): entries/tiles padded to multiples of `depth`,
+// group unions padded to whole LDS stages, and the TLDS low-table array.
+struct HostPlan {
+    std::vector<uint32_t> entries, tiles, groups, unions, atab;
+    int max_tile_entries = 0;
+};
+
 // 4 KiB of zeros per device, never written: the load target of padding entries
 // (always L2-resident, so padding costs no HBM traffic).
 const uint8_t *zero_page_for_current_device();
@@ -89,6 +97,12 @@ public:
     // ([max_in_slot+1][len]) and writes `out` ([max_out_slot+1][len]).  Throws
     // if the union bookkeeping is inconsistent.
     void emulate(const uint8_t *in, uint8_t *out, int64_t len, bool via_unions) const;
+    // The host arrays plan_for_current_device(depth) uploads.
+    HostPlan padded_plan(int depth) const;
+    // Host interpretation of a padded plan as k_gf_apply reads it: padding entries
+    // read zeros, and with `tlds` the low dword of each 8-entry table comes from
+    // HostPlan::atab (the LDS copy) instead of the entry.
+    void emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds) const;
     CompiledMap &compact();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();

@@ -664,3 +664,40 @@ def test_per_call_paths_agree(ecx, L):
             assert all((sh[i] == ref[i]).all() for i in range(6))
     finally:
         ecx.tune("host_gather_kib", 256)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_maps_on_device(ecx, torch_dev, seed):
+    """Random GF(256) maps of every shape class (single- and multi-tile, sparse and
+    dense, coefficient-1 entries, scattered slots) applied by the device batch path at
+    ring depths 4 and 8, with and without the LDS table copy, on a ragged byte count
+    over several stripes: each equals the oracle's table-driven product."""
+    from conftest import gf_apply_numpy
+    torch = torch_dev
+    rng = np.random.default_rng(1000 + seed)
+    n_out, n_in = int(rng.integers(1, 41)), int(rng.integers(1, 41))
+    m = rng.integers(2, 256, (n_out, n_in)).astype(np.uint8)
+    m[rng.random((n_out, n_in)) < 0.2] = 1
+    m[rng.random((n_out, n_in)) >= rng.uniform(0.1, 1.0)] = 0
+    in_slot = sorted(rng.choice(2 * n_in, n_in, replace=False).tolist())
+    out_slot = rng.permutation(rng.choice(2 * n_out, n_out, replace=False)).tolist()
+    gm = ecx.GfMap.from_matrix(m, in_slot=in_slot, out_slot=out_slot)
+    S, L = 3, 4096 * 3 + int(rng.integers(0, 4096))
+    ni, no = 2 * n_in, 2 * n_out
+    inp = torch.empty((S, ni, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(inp, inp.numel(), seed)
+    host = inp.cpu().numpy()
+    ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
+    for depth in (4, 8):
+        for lt in (0, 2):
+            ecx.tune("depth", depth)
+            ecx.tune("lds_tables", lt)
+            out = torch.full((S, no, L), 0x5A, dtype=torch.uint8, device="cuda")
+            gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            for s in range(S):
+                for o, slot in enumerate(out_slot):
+                    assert (got[s, slot] == ref[s][o]).all(), (depth, lt, s, o)
+    ecx.tune("depth", 0)
+    ecx.tune("lds_tables", 1)

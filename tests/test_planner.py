@@ -214,3 +214,28 @@ def test_lrc_maps_match_reference_groups(ecx):
     with pytest.raises(ecx.EcxError) as e:
         ecx.LRCErasureCode.map(pres)
     assert e.value.code == -2
+
+
+def test_compiled_plan_selftest_random_maps(ecx):
+    """Property test over random GF(256) maps: any shape (1..48 outputs, 1..48 inputs),
+    any sparsity, coefficient-1 entries, all-zero rows and columns, and scattered
+    (non-contiguous) slot numbers.  The compiled plan -- row tiles, entry tables, the
+    padded arrays uploaded for ring depths 4 and 8 (with and without the LDS table
+    copy), tile groups and their unions -- interpreted on the host reproduces the map."""
+    import numpy as np
+    hyp = pytest.importorskip("hypothesis")
+    st = hyp.strategies
+
+    @hyp.settings(max_examples=60, deadline=None, derandomize=True)
+    @hyp.given(st.integers(1, 48), st.integers(1, 48), st.floats(0.0, 1.0), st.floats(0.0, 0.5),
+               st.integers(0, 2**32 - 1))
+    def check(n_out, n_in, density, ones, seed):
+        rng = np.random.default_rng(seed)
+        m = rng.integers(2, 256, (n_out, n_in)).astype(np.uint8)
+        m[rng.random((n_out, n_in)) < ones] = 1
+        m[rng.random((n_out, n_in)) >= density] = 0
+        in_slot = sorted(rng.choice(4 * n_in, n_in, replace=False).tolist())
+        out_slot = rng.permutation(rng.choice(4 * n_out, n_out, replace=False)).tolist()
+        ecx.GfMap.from_matrix(m, in_slot=in_slot, out_slot=out_slot).selftest(seed & 0xFFFF)
+
+    check()
