@@ -20,6 +20,8 @@
  *                      (system scope: written through, dropped from L2)
  *   "chunk_major"      block order of the one-workgroup-per-tile kernel: 0 = stripe-major
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
+ *   "block_threads"    one-workgroup-per-tile kernel: 256 threads over 4 KiB chunks (default)
+ *                      or 64 threads (one wave) over 1 KiB chunks
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -770,6 +770,10 @@ int ecx_tune(const char *key, int value) {
     else if (k == "wave_groups") t.wave_groups = value != 0;
     else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "chunk_major") t.chunk_major = value != 0;
+    else if (k == "block_threads") {
+        if (value != 64 && value != 256) return ECX_E_ILLEGAL_ARGUMENT;
+        t.block_threads = value;
+    }
     else if (k == "lds_tables") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.lds_tables = value;

@@ -157,6 +157,9 @@ struct Tuning {
     int store_scope = 0;
     // k_gf_apply block order: 0 = stripe-major (a stripe's chunks back to back), 1 = chunk-major.
     int chunk_major = 0;
+    // k_gf_apply workgroup: 256 threads over 4 KiB chunks (default) or 64 threads (one
+    // wave) over 1 KiB chunks.
+    int block_threads = kBlockThreads;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

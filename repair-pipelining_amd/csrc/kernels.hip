@@ -18,6 +18,8 @@
 //   * no LDS, no MFMA: this is HBM-bound byte work.
 #include "engine.hpp"
 
+#include <type_traits>
+
 namespace ecx {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -180,7 +182,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS>
+template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS>
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint64_t in_base, uint64_t out_base,
                                            uint32_t lane16, int valid, uint2 *lds_tab) {
     const uint8_t *ib = reinterpret_cast<const uint8_t *>(in_base) + lane16;
@@ -222,7 +224,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
         if (TLDS) {
             u32x4 *dst = (u32x4 *)lds_tab;
             if ((int)threadIdx.x < n16) dst[threadIdx.x] = apiece;
-            for (int i = threadIdx.x + kBlockThreads; i < n16; i += kBlockThreads) dst[i] = asrc[i];  // > 64 entries
+            for (int i = threadIdx.x + THREADS; i < n16; i += THREADS) dst[i] = asrc[i];  // > THREADS / 4 entries
             __syncthreads();
         }
         const int last = ecnt - DEPTH;
@@ -250,12 +252,13 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
     }
 }
 
-// One workgroup = one (stripe, 4 KiB chunk, output tile).  TLDS: dynamic LDS holds
-// the tile's low table dwords (launch_apply sizes it to the longest padded tile).
-template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS>
-__global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
+// One workgroup = one (stripe, THREADS x 16-byte chunk, output tile): 256 threads and
+// 4 KiB chunks by default, or one wave and 1 KiB chunks (ecx_tune "block_threads").
+// TLDS: dynamic LDS holds the tile's low table dwords (launch_apply sizes it to the
+// longest padded tile).
+template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS>
+__global__ void __launch_bounds__(THREADS, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
     extern __shared__ uint2 lds_tab[];
-    constexpr int THREADS = kBlockThreads;
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
@@ -270,7 +273,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEPTH == 4 ? 6 : 5) k_gf_apply(
         const int64_t v = a.nbytes - cbase - (int64_t)threadIdx.x * 16;
         valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
     }
-    apply_tile<SAFE, NTL, NTS, DEPTH, TLDS>(a, plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords,
+    apply_tile<SAFE, NTL, NTS, DEPTH, TLDS, THREADS>(a, plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords,
                                             uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
                                             uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)),
                                             threadIdx.x * 16, valid, lds_tab);
@@ -374,6 +377,45 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
     }
 }
 
+namespace {
+// Run-time launch shape -> template instance of k_gf_apply.
+struct Shape {
+    bool safe, ntl;
+    int nts, depth;
+    bool tlds;
+    int threads;
+};
+
+template <bool SAFE, bool NTL, int NTS, int D, bool TLDS, int T>
+void launch_k(dim3 grid, size_t lds, hipStream_t stream, const ApplyArgs &a) {
+    hipLaunchKernelGGL((k_gf_apply<SAFE, NTL, NTS, D, TLDS, T>), grid, dim3(T), lds, stream, a);
+}
+
+template <int T>
+void launch_shape_t(const Shape &s, dim3 grid, size_t lds, hipStream_t stream, const ApplyArgs &a) {
+    if (s.safe) return launch_k<true, false, 0, 4, false, T>(grid, 0, stream, a);
+    auto by_depth = [&](auto ntl, auto nts) {
+        constexpr bool L = decltype(ntl)::value;
+        constexpr int S = decltype(nts)::value;
+        if (s.depth == 8) {
+            if (s.tlds) launch_k<false, L, S, 8, true, T>(grid, lds, stream, a);
+            else launch_k<false, L, S, 8, false, T>(grid, 0, stream, a);
+        } else {
+            if (s.tlds) launch_k<false, L, S, 4, true, T>(grid, lds, stream, a);
+            else launch_k<false, L, S, 4, false, T>(grid, 0, stream, a);
+        }
+    };
+    using t_ = std::true_type;
+    using f_ = std::false_type;
+    if (s.ntl) {
+        if (s.nts == 2) by_depth(t_{}, std::integral_constant<int, 2>{});
+        else by_depth(t_{}, std::integral_constant<int, 1>{});
+    } else if (s.nts == 2) by_depth(f_{}, std::integral_constant<int, 2>{});
+    else if (s.nts == 1) by_depth(f_{}, std::integral_constant<int, 1>{});
+    else by_depth(f_{}, std::integral_constant<int, 0>{});
+}
+}  // namespace
+
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate) {
@@ -383,10 +425,11 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
     const Tuning &tu = tuning();
-    // Multi-tile maps run as tile groups (one wave per tile, 1 KiB chunks); single-tile
-    // maps as one 256-lane workgroup per 4 KiB chunk.
+    // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
+    // one workgroup per (stripe, chunk, tile) with 4 KiB (256 threads) or 1 KiB (64) chunks.
     const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
-    const int64_t chunk = waves ? kWaveChunkBytes : kChunkBytes;
+    const int threads = tu.block_threads == 64 ? 64 : kBlockThreads;
+    const int64_t chunk = waves ? kWaveChunkBytes : threads * 16;
     const int64_t full = aligned ? nbytes / chunk : 0;               // in units of `chunk`
     const int64_t tail_chunks = (nbytes - full * chunk + chunk - 1) / chunk;
 
@@ -399,7 +442,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.unions = plan.unions;
     a.atab = plan.atab;
     a.lane_zero = 0;
-    a.chunk_major = tuning().chunk_major;
+    a.chunk_major = tu.chunk_major;
     a.n_groups = cm.n_groups();
     a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;
@@ -408,7 +451,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.out_slot_stride = out_slot_stride;
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
-    a.xcd_group = a.n_tiles > 1 ? tuning().xcd_group : 0;
+    a.xcd_group = a.n_tiles > 1 ? tu.xcd_group : 0;
     a.accumulate = accumulate ? 1 : 0;
 
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
@@ -429,36 +472,19 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                 else hipLaunchKernelGGL((k_gf_apply_lds<false, 4>), grid, blk, 0, stream, a);
                 continue;
             }
+            Shape s;
+            s.safe = safe;
+            // Non-temporal policy: 0 never; 1 auto (NT stores, NT loads for single-tile maps); 2 always.
             const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (a.n_tiles == 1 ? 2 : 1) : 0);
-            const dim3 blk(kBlockThreads);
-            const bool tlds = !safe && plan.max_tile_entries > 0 && plan.max_tile_entries <= kMaxLdsTileEntries &&
-                              (tu.lds_tables == 2 || (tu.lds_tables == 1 && a.n_tiles > 1));
-            const size_t lds = tlds ? (size_t)plan.max_tile_entries * kAtabDwords * 4 : 0;
-#define ECX_LAUNCH(NTL, NTS, D)                                                                          \
-    do {                                                                                                 \
-        if (tlds) hipLaunchKernelGGL((k_gf_apply<false, NTL, NTS, D, true>), grid, blk, lds, stream, a); \
-        else hipLaunchKernelGGL((k_gf_apply<false, NTL, NTS, D, false>), grid, blk, 0, stream, a);       \
-    } while (0)
-            const int sts = tu.store_scope ? 2 : 1;  // non-temporal stores: plain nt, or nt sc0 sc1
-            if (safe) hipLaunchKernelGGL((k_gf_apply<true, false, 0, 4, false>), grid, blk, 0, stream, a);
-            else if (depth == 8) {
-                if (ntmode == 2) {
-                    if (sts == 2) ECX_LAUNCH(true, 2, 8);
-                    else ECX_LAUNCH(true, 1, 8);
-                } else if (ntmode == 1) {
-                    if (sts == 2) ECX_LAUNCH(false, 2, 8);
-                    else ECX_LAUNCH(false, 1, 8);
-                } else ECX_LAUNCH(false, 0, 8);
-            } else {
-                if (ntmode == 2) {
-                    if (sts == 2) ECX_LAUNCH(true, 2, 4);
-                    else ECX_LAUNCH(true, 1, 4);
-                } else if (ntmode == 1) {
-                    if (sts == 2) ECX_LAUNCH(false, 2, 4);
-                    else ECX_LAUNCH(false, 1, 4);
-                } else ECX_LAUNCH(false, 0, 4);
-            }
-#undef ECX_LAUNCH
+            s.ntl = ntmode == 2;
+            s.nts = ntmode == 0 ? 0 : (tu.store_scope ? 2 : 1);
+            s.depth = depth;
+            s.tlds = !safe && plan.max_tile_entries > 0 && plan.max_tile_entries <= kMaxLdsTileEntries &&
+                     (tu.lds_tables == 2 || (tu.lds_tables == 1 && a.n_tiles > 1));
+            s.threads = threads;
+            const size_t lds = s.tlds ? (size_t)plan.max_tile_entries * kAtabDwords * 4 : 0;
+            if (threads == 64) launch_shape_t<64>(s, grid, lds, stream, a);
+            else launch_shape_t<kBlockThreads>(s, grid, lds, stream, a);
         }
     };
     run(false, 0, full);

@@ -7,6 +7,7 @@ bytes).  Modes:
     tiles_lds_all -- as tiles, low table dwords from LDS for single-tile maps too (lds_tables 2)
     tiles_sc      -- as tiles, output stores `nt sc0 sc1` (store_scope 1)
     tiles_cm      -- as tiles, chunk-major block order (chunk_major 1)
+    tiles_w64     -- as tiles, one-wave workgroups over 1 KiB chunks (block_threads 64)
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -58,13 +59,15 @@ def cases(ecx, torch, only):
     return out
 
 
-MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0},
-         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0},
-         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0},
-         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0, "chunk_major": 0},
-         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1, "chunk_major": 0},
-         "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1},
-         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0}}
+MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
+         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
+         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
+         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
+         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1, "chunk_major": 0, "block_threads": 256},
+         "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1, "block_threads": 256},
+         "tiles_w64": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
+                       "block_threads": 64},
+         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256}}
 
 
 def main():

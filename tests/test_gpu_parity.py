@@ -580,8 +580,8 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     """Every launch shape gives the same bytes: the LDS tile-group kernel
     (k_gf_apply_lds, 1 KiB chunks + byte-safe tail) and the one-workgroup-per-tile
     kernel with its split tables read from SGPRs only or partly from LDS
-    (lds_tables 0 / 1 / 2), with `nt sc0 sc1` output stores and in chunk-major
-    block order; all match the oracle on a sampled stripe.  The last
+    (lds_tables 0 / 1 / 2), with `nt sc0 sc1` output stores, in chunk-major block
+    order and with one-wave workgroups over 1 KiB chunks; all match the oracle on a sampled stripe.  The last
     case is a single-tile map (Clay(4,2) repair)."""
     torch = torch_dev
     step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
@@ -590,11 +590,13 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 31)
     outs = []
-    for wg, lt, sc, cm in ((1, 1, 0, 0), (0, 0, 0, 0), (0, 1, 0, 0), (0, 2, 0, 0), (0, 1, 1, 0), (0, 1, 0, 1)):
+    for wg, lt, sc, cm, bt in ((1, 1, 0, 0, 256), (0, 0, 0, 0, 256), (0, 1, 0, 0, 256), (0, 2, 0, 0, 256),
+                               (0, 1, 1, 0, 256), (0, 1, 0, 1, 256), (0, 1, 0, 0, 64), (0, 2, 0, 1, 64)):
         ecx.tune("wave_groups", wg)
         ecx.tune("lds_tables", lt)
         ecx.tune("store_scope", sc)
         ecx.tune("chunk_major", cm)
+        ecx.tune("block_threads", bt)
         o = torch.full((S, len(erased) * a, B), 7, dtype=torch.uint8, device="cuda")
         step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
         torch.cuda.synchronize()
@@ -603,6 +605,7 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     ecx.tune("lds_tables", 1)
     ecx.tune("store_scope", 0)
     ecx.tune("chunk_major", 0)
+    ecx.tune("block_threads", 256)
     for o in outs[1:]:
         assert (o == outs[0]).all()
     if v == 0:
@@ -670,7 +673,8 @@ def test_per_call_paths_agree(ecx, L):
 def test_random_maps_on_device(ecx, torch_dev, seed):
     """Random GF(256) maps of every shape class (single- and multi-tile, sparse and
     dense, coefficient-1 entries, scattered slots) applied by the device batch path at
-    ring depths 4 and 8, with and without the LDS table copy, on a ragged byte count
+    ring depths 4 and 8, with and without the LDS table copy, with 256- and 64-thread
+    workgroups, on a ragged byte count
     over several stripes: each equals the oracle's table-driven product."""
     from conftest import gf_apply_numpy
     torch = torch_dev
@@ -688,16 +692,17 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.fill_random(inp, inp.numel(), seed)
     host = inp.cpu().numpy()
     ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
-    for depth in (4, 8):
-        for lt in (0, 2):
-            ecx.tune("depth", depth)
-            ecx.tune("lds_tables", lt)
-            out = torch.full((S, no, L), 0x5A, dtype=torch.uint8, device="cuda")
-            gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
-            torch.cuda.synchronize()
-            got = out.cpu().numpy()
-            for s in range(S):
-                for o, slot in enumerate(out_slot):
-                    assert (got[s, slot] == ref[s][o]).all(), (depth, lt, s, o)
+    for depth, lt, bt in ((4, 0, 256), (4, 2, 256), (8, 0, 256), (8, 2, 256), (8, 2, 64), (4, 0, 64)):
+        ecx.tune("depth", depth)
+        ecx.tune("lds_tables", lt)
+        ecx.tune("block_threads", bt)
+        out = torch.full((S, no, L), 0x5A, dtype=torch.uint8, device="cuda")
+        gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for s in range(S):
+            for o, slot in enumerate(out_slot):
+                assert (got[s, slot] == ref[s][o]).all(), (depth, lt, bt, s, o)
     ecx.tune("depth", 0)
     ecx.tune("lds_tables", 1)
+    ecx.tune("block_threads", 256)
