@@ -10,9 +10,10 @@
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous
  *                      eighth of the grid; 2 = each XCD runs whole (stripe, chunk) units, all
  *                      tiles of a unit back to back (default: see engine.hpp Tuning)
- *   "wave_groups"      multi-tile maps: 1 = one workgroup per group of tiles sharing inputs, one
- *                      wave per tile, the group's input union staged once through LDS;
- *                      0 = one workgroup per tile (default; faster on every measured map)
+ *   "wave_groups"      multi-tile maps: one workgroup per group of tiles sharing inputs, one
+ *                      wave per tile, 1 KiB chunks: 1 = the group's input union staged once
+ *                      through LDS; 2 = each wave loads its own entries (no LDS, no barriers);
+ *                      0 = one workgroup per tile (default)
  *   "lds_tables"       0 = all split-table dwords read as scalars (one v_mov per 8-entry table
  *                      and row); 1 = the low dword of each 8-entry table staged per workgroup
  *                      in LDS, for multi-tile maps (default); 2 = for every map

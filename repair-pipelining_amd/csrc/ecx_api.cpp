@@ -767,7 +767,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.xcd_group = value;
     }
-    else if (k == "wave_groups") t.wave_groups = value != 0;
+    else if (k == "wave_groups") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.wave_groups = value;
+    }
     else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "chunk_major") t.chunk_major = value != 0;
     else if (k == "block_threads") {

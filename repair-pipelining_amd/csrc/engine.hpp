@@ -144,7 +144,8 @@ struct Tuning {
     int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or 4 / 8
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
-    // Multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS).  Off by
+    // Multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS), 2 =
+    // k_gf_apply_grp (tile groups in one workgroup, direct loads).  Off by
     // default: Clay(10,4)'s 64-row groups still need 1.23x the unique inputs and the
     // per-stage barriers cost more than the saved traffic (profiles/r01_multitile.jsonl).
     int wave_groups = 0;

@@ -377,6 +377,36 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
     }
 }
 
+// Multi-tile maps, tile groups without staging: one workgroup = one (stripe, 1 KiB
+// chunk, tile GROUP), one wave per tile, each wave loading its own entries directly.
+// The group's tiles share inputs, and each tile's entry list is ordered by the
+// group's staging schedule (engine.cpp align_group), so the waves of a workgroup --
+// on one CU -- request a shared input at about the same time and the repeats are
+// served by that CU's L1 / the XCD's L2 rather than by another CU's fetch.  No LDS,
+// no barriers: a wave whose slot in the group is empty exits at once.
+template <bool SAFE, int DEPTH>
+__global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_apply_grp(ApplyArgs a) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t b = blockIdx.x;
+    const uint32_t g = b % (uint32_t)a.n_groups;
+    const uint32_t rest = b / (uint32_t)a.n_groups;
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(plan_ptr(a.groups)[g * kGroupDwords + wave]);
+    if (tl == kNoTile) return;
+    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
+    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+    const int64_t cbase = c * kWaveChunkBytes;
+    const uint32_t lane16 = lane * 16;
+    int valid = 16;
+    if (SAFE) {
+        const int64_t v = a.nbytes - cbase - (int64_t)lane16;
+        valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
+    }
+    apply_tile<SAFE, false, SAFE ? 0 : 1, DEPTH, false, 64>(
+        a, plan_ptr(a.tiles) + tl * kTileDwords, uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
+        uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)), lane16, valid, nullptr);
+}
+
 namespace {
 // Run-time launch shape -> template instance of k_gf_apply.
 struct Shape {
@@ -467,6 +497,12 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             const dim3 grid((unsigned)(ns * per_stripe));
             if (waves) {
                 const dim3 blk(64 * cm.group_size());
+                if (tu.wave_groups == 2) {  // direct loads, no LDS staging
+                    if (safe) hipLaunchKernelGGL((k_gf_apply_grp<true, 4>), grid, blk, 0, stream, a);
+                    else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_grp<false, 8>), grid, blk, 0, stream, a);
+                    else hipLaunchKernelGGL((k_gf_apply_grp<false, 4>), grid, blk, 0, stream, a);
+                    continue;
+                }
                 if (safe) hipLaunchKernelGGL((k_gf_apply_lds<true, 4>), grid, blk, 0, stream, a);
                 else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_lds<false, 8>), grid, blk, 0, stream, a);
                 else hipLaunchKernelGGL((k_gf_apply_lds<false, 4>), grid, blk, 0, stream, a);

@@ -8,6 +8,7 @@ bytes).  Modes:
     tiles_sc      -- as tiles, output stores `nt sc0 sc1` (store_scope 1)
     tiles_cm      -- as tiles, chunk-major block order (chunk_major 1)
     tiles_w64     -- as tiles, one-wave workgroups over 1 KiB chunks (block_threads 64)
+    grp     -- k_gf_apply_grp: tile groups in one workgroup, each wave loading its own entries
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -67,6 +68,8 @@ MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_sco
          "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1, "block_threads": 256},
          "tiles_w64": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
                        "block_threads": 64},
+         "grp": {"wave_groups": 2, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
+                 "block_threads": 256},
          "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256}}
 
 

@@ -581,7 +581,8 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     (k_gf_apply_lds, 1 KiB chunks + byte-safe tail) and the one-workgroup-per-tile
     kernel with its split tables read from SGPRs only or partly from LDS
     (lds_tables 0 / 1 / 2), with `nt sc0 sc1` output stores, in chunk-major block
-    order and with one-wave workgroups over 1 KiB chunks; all match the oracle on a sampled stripe.  The last
+    order and with one-wave workgroups over 1 KiB chunks, and the unstaged tile-group
+    kernel (k_gf_apply_grp); all match the oracle on a sampled stripe.  The last
     case is a single-tile map (Clay(4,2) repair)."""
     torch = torch_dev
     step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
@@ -591,7 +592,7 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     ecx.fill_random(pool, pool.numel(), 31)
     outs = []
     for wg, lt, sc, cm, bt in ((1, 1, 0, 0, 256), (0, 0, 0, 0, 256), (0, 1, 0, 0, 256), (0, 2, 0, 0, 256),
-                               (0, 1, 1, 0, 256), (0, 1, 0, 1, 256), (0, 1, 0, 0, 64), (0, 2, 0, 1, 64)):
+                               (0, 1, 1, 0, 256), (0, 1, 0, 1, 256), (0, 1, 0, 0, 64), (0, 2, 0, 1, 64), (2, 1, 0, 0, 256)):
         ecx.tune("wave_groups", wg)
         ecx.tune("lds_tables", lt)
         ecx.tune("store_scope", sc)
