@@ -4,7 +4,7 @@
  * results are bit-identical for every setting, only speed changes.
  *
  *   "depth"            16-B loads per lane in the kernel's load ring: 0 = per map (default:
- *                      8 when every tile has >= 12 entries, else 4), or force 4 / 8
+ *                      8 when every tile has >= 12 entries, else 4), or force 2 / 4 / 8
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous

@@ -756,7 +756,7 @@ int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
     Tuning &t = tuning();
     if (k == "depth") {
-        if (value != 0 && value != 4 && value != 8) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value != 0 && value != 2 && value != 4 && value != 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.depth = value;
     }
     else if (k == "nontemporal") {

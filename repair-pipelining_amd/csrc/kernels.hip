@@ -257,7 +257,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
 // TLDS: dynamic LDS holds the tile's low table dwords (launch_apply sizes it to the
 // longest padded tile).
 template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS>
-__global__ void __launch_bounds__(THREADS, DEPTH == 4 ? 6 : 5) k_gf_apply(ApplyArgs a) {
+__global__ void __launch_bounds__(THREADS, DEPTH == 2 ? 8 : (DEPTH == 4 ? 6 : 5)) k_gf_apply(ApplyArgs a) {
     extern __shared__ uint2 lds_tab[];
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
@@ -423,13 +423,19 @@ void launch_k(dim3 grid, size_t lds, hipStream_t stream, const ApplyArgs &a) {
 
 template <int T>
 void launch_shape_t(const Shape &s, dim3 grid, size_t lds, hipStream_t stream, const ApplyArgs &a) {
-    if (s.safe) return launch_k<true, false, 0, 4, false, T>(grid, 0, stream, a);
+    if (s.safe) {  // the byte-safe kernel's ring must match the plan's padding
+        if (s.depth == 2) return launch_k<true, false, 0, 2, false, T>(grid, 0, stream, a);
+        return launch_k<true, false, 0, 4, false, T>(grid, 0, stream, a);
+    }
     auto by_depth = [&](auto ntl, auto nts) {
         constexpr bool L = decltype(ntl)::value;
         constexpr int S = decltype(nts)::value;
         if (s.depth == 8) {
             if (s.tlds) launch_k<false, L, S, 8, true, T>(grid, lds, stream, a);
             else launch_k<false, L, S, 8, false, T>(grid, 0, stream, a);
+        } else if (s.depth == 2) {
+            if (s.tlds) launch_k<false, L, S, 2, true, T>(grid, lds, stream, a);
+            else launch_k<false, L, S, 2, false, T>(grid, 0, stream, a);
         } else {
             if (s.tlds) launch_k<false, L, S, 4, true, T>(grid, lds, stream, a);
             else launch_k<false, L, S, 4, false, T>(grid, 0, stream, a);
@@ -450,15 +456,18 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
-    const int depth = tuning().depth == 8 ? 8 : (tuning().depth == 4 ? 4 : cm.preferred_depth());
+    const Tuning &tu = tuning();
+    const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
+    const int threads = tu.block_threads == 64 ? 64 : kBlockThreads;
+    // Ring depth: per map, or forced (ecx_tune "depth"); depth 2 exists for the
+    // 256-thread one-workgroup-per-tile kernel only.
+    int depth = tu.depth ? tu.depth : cm.preferred_depth();
+    if (depth == 2 && (waves || threads != kBlockThreads)) depth = 4;
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
-    const Tuning &tu = tuning();
     // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
     // one workgroup per (stripe, chunk, tile) with 4 KiB (256 threads) or 1 KiB (64) chunks.
-    const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
-    const int threads = tu.block_threads == 64 ? 64 : kBlockThreads;
     const int64_t chunk = waves ? kWaveChunkBytes : threads * 16;
     const int64_t full = aligned ? nbytes / chunk : 0;               // in units of `chunk`
     const int64_t tail_chunks = (nbytes - full * chunk + chunk - 1) / chunk;

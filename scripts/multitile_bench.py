@@ -9,6 +9,8 @@ bytes).  Modes:
     tiles_cm      -- as tiles, chunk-major block order (chunk_major 1)
     tiles_w64     -- as tiles, one-wave workgroups over 1 KiB chunks (block_threads 64)
     grp     -- k_gf_apply_grp: tile groups in one workgroup, each wave loading its own entries
+    tiles_d2      -- as tiles_sgpr, load ring of 2 (63 VGPRs, 8 waves per SIMD)
+    tiles_d4      -- as tiles, load ring of 4 (6 waves per SIMD)
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -60,17 +62,21 @@ def cases(ecx, torch, only):
     return out
 
 
-MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
-         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
-         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
-         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0, "chunk_major": 0, "block_threads": 256},
-         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1, "chunk_major": 0, "block_threads": 256},
-         "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1, "block_threads": 256},
+MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
+         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
+         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
+         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
+         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1, "chunk_major": 0, "block_threads": 256, "depth": 0},
+         "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1, "block_threads": 256, "depth": 0},
          "tiles_w64": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
-                       "block_threads": 64},
+                       "block_threads": 64, "depth": 0},
          "grp": {"wave_groups": 2, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
-                 "block_threads": 256},
-         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256}}
+                 "block_threads": 256, "depth": 0},
+         "tiles_d2": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0,
+                      "block_threads": 256, "depth": 2},
+         "tiles_d4": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
+                      "block_threads": 256, "depth": 4},
+         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0}}
 
 
 def main():

@@ -674,7 +674,7 @@ def test_per_call_paths_agree(ecx, L):
 def test_random_maps_on_device(ecx, torch_dev, seed):
     """Random GF(256) maps of every shape class (single- and multi-tile, sparse and
     dense, coefficient-1 entries, scattered slots) applied by the device batch path at
-    ring depths 4 and 8, with and without the LDS table copy, with 256- and 64-thread
+    ring depths 2, 4 and 8, with and without the LDS table copy, with 256- and 64-thread
     workgroups, on a ragged byte count
     over several stripes: each equals the oracle's table-driven product."""
     from conftest import gf_apply_numpy
@@ -693,7 +693,8 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.fill_random(inp, inp.numel(), seed)
     host = inp.cpu().numpy()
     ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
-    for depth, lt, bt in ((4, 0, 256), (4, 2, 256), (8, 0, 256), (8, 2, 256), (8, 2, 64), (4, 0, 64)):
+    for depth, lt, bt in ((4, 0, 256), (4, 2, 256), (8, 0, 256), (8, 2, 256), (8, 2, 64), (4, 0, 64), (2, 0, 256),
+                          (2, 2, 256)):
         ecx.tune("depth", depth)
         ecx.tune("lds_tables", lt)
         ecx.tune("block_threads", bt)
