@@ -121,6 +121,19 @@ int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe
                         uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                         int64_t byte_count, void *stream);
 
+/* ReedSolomon.encodeParity (ReedSolomon.java:94-108) over nstripes device-resident
+ * stripes, in place: stripe s's shard i is base + s*stripe_stride + i*shard_stride; the
+ * parity shards k..n-1 are overwritten for bytes [offset, offset + byte_count). */
+int ecx_rs_encode_parity_batch(ecx_rs *rs, uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
+                               int64_t nstripes, int64_t offset, int64_t byte_count, void *stream);
+/* ReedSolomon.decodeMissing (ReedSolomon.java:189-286) over nstripes device-resident
+ * stripes, in place (same layout): every shard with shard_present[i] == 0 is rebuilt,
+ * data from the first k present shards (ascending index), parity from all data -- the
+ * reference's map exactly.  Fewer than k present: ECX_E_NOT_ENOUGH_SHARDS. */
+int ecx_rs_decode_missing_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base, int64_t stripe_stride,
+                                int64_t shard_stride, int64_t nstripes, int64_t offset, int64_t byte_count,
+                                void *stream);
+
 /* As ecx_map_apply_batch, but XOR-accumulates: out ^= M * in. */
 int ecx_map_accumulate_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
                              int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride,

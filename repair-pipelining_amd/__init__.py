@@ -491,6 +491,24 @@ class ReedSolomon:
                                                  byteCount, 1 if isFirst else 0))
 
     # batched, device-resident
+    def encodeParityBatch(self, shards, stripe_stride, shard_stride, nstripes, offset, byteCount, stream=None):
+        """encodeParity over nstripes device-resident stripes, in place (ecx_rs_encode_parity_batch)."""
+        _check_layout(shards, stripe_stride, shard_stride, self.getTotalShardCount() - 1, nstripes, offset + byteCount,
+                      "shards")
+        check(lib().ecx_rs_encode_parity_batch(self._h, _dev_ptr(shards), stripe_stride, shard_stride, nstripes,
+                                               offset, byteCount, _stream(stream)))
+
+    def decodeMissingBatch(self, shards, shardPresent, stripe_stride, shard_stride, nstripes, offset, byteCount,
+                           stream=None):
+        """decodeMissing over nstripes device-resident stripes, in place (ecx_rs_decode_missing_batch)."""
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        if len(pres) != self.getTotalShardCount():
+            raise EcxError(-1, "wrong number of shardPresent flags")
+        _check_layout(shards, stripe_stride, shard_stride, self.getTotalShardCount() - 1, nstripes, offset + byteCount,
+                      "shards")
+        check(lib().ecx_rs_decode_missing_batch(self._h, pres.ctypes.data, _dev_ptr(shards), stripe_stride,
+                                                shard_stride, nstripes, offset, byteCount, _stream(stream)))
+
     def decodePartialBatch(self, shardPresent, shardIndex, inp, in_stripe_stride, acc, acc_stripe_stride,
                            acc_row_stride, nstripes, byteCount, isFirst, stream=None):
         """Batched decodeMissingSingle for every missing shard (data and parity)."""

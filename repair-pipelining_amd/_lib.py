@@ -84,6 +84,8 @@ SIGNATURES = {
     "ecx_map_accumulate_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_rs_decode_map": (I, [P, P, ctypes.POINTER(P)]),
+    "ecx_rs_encode_parity_batch": (I, [P, P, I64, I64, I64, I64, I64, P]),
+    "ecx_rs_decode_missing_batch": (I, [P, P, P, I64, I64, I64, I64, I64, P]),
     "ecx_rs_decode_partial_batch": (I, [P, P, I, P, I64, P, I64, I64, I64, I64, I, P]),
     "ecx_rs_encode_partial_batch": (I, [P, I, P, I64, P, I64, I64, I64, I64, I, P]),
     "ecx_clay_create": (I, [I, I, P, I, ctypes.POINTER(P)]),

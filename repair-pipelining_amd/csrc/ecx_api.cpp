@@ -288,6 +288,36 @@ int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **
     });
 }
 
+int ecx_rs_encode_parity_batch(ecx_rs *rs, uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
+                               int64_t nstripes, int64_t offset, int64_t byte_count, void *stream) {
+    return guarded([&]() -> int {
+        if (nstripes < 0 || offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!base) throw Error(ECX_E_NULL, "null device pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_encode_map(rs, &m);
+        if (st) return st;
+        launch_apply(const_cast<ecx_map *>(m)->cm, base + offset, stripe_stride, shard_stride, base + offset,
+                     stripe_stride, shard_stride, nstripes, byte_count, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_decode_missing_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base, int64_t stripe_stride,
+                                int64_t shard_stride, int64_t nstripes, int64_t offset, int64_t byte_count,
+                                void *stream) {
+    return guarded([&]() -> int {
+        if (nstripes < 0 || offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!base) throw Error(ECX_E_NULL, "null device pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_decode_map(rs, shard_present, &m);  // Not enough shards -> -2
+        if (st) return st;
+        if (m->cm.map().n_out == 0) return ECX_OK;  // all present (ReedSolomon.java:216-218)
+        launch_apply(const_cast<ecx_map *>(m)->cm, base + offset, stripe_stride, shard_stride, base + offset,
+                     stripe_stride, shard_stride, nstripes, byte_count, (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
 int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int offset,
                          int byte_count) {
     return guarded([&]() -> int {

@@ -708,3 +708,43 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.tune("depth", 0)
     ecx.tune("lds_tables", 1)
     ecx.tune("block_threads", 256)
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
+def test_rs_batch_codec_entry_points(ecx, torch_dev, k, m):
+    """ecx_rs_encode_parity_batch / ecx_rs_decode_missing_batch: encodeParity and
+    decodeMissing over many device-resident stripes, in place, with a byte window
+    (offset, ragged count) and a padded shard pitch.  Every stripe matches the oracle's
+    encode_parity / decode_missing on the same bytes, including non-codeword inputs
+    (the exact first-k-present map), for several erasure patterns."""
+    torch = torch_dev
+    n, S, pitch, off, cnt = k + m, 4, 3072 + 16, 16, 2983
+    rs = ecx.ReedSolomon.create(k, m)
+    dev = torch.empty((S, n, pitch), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(dev, dev.numel(), 77 + k)
+    host = dev.cpu().numpy()
+    rs.encodeParityBatch(dev, n * pitch, pitch, S, off, cnt)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    for s in range(S):
+        ref = [host[s, i].copy() for i in range(n)]
+        O.ReedSolomon(k, m).encode_parity(ref, off, cnt)
+        assert all((got[s, i] == ref[i]).all() for i in range(n)), s
+    rng = np.random.default_rng(k)
+    for _ in range(4):
+        present = [True] * n
+        for i in rng.choice(n, m, replace=False):
+            present[i] = False
+        dev = torch.empty((S, n, pitch), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(dev, dev.numel(), int(rng.integers(1 << 30)))  # non-codeword stripes
+        host = dev.cpu().numpy()
+        rs.decodeMissingBatch(dev, present, n * pitch, pitch, S, off, cnt)
+        torch.cuda.synchronize()
+        got = dev.cpu().numpy()
+        for s in range(S):
+            ref = [host[s, i].copy() for i in range(n)]
+            O.ReedSolomon(k, m).decode_missing(ref, present, off, cnt)
+            assert all((got[s, i] == ref[i]).all() for i in range(n)), (present, s)
+    with pytest.raises(ecx.EcxError) as e:
+        rs.decodeMissingBatch(dev, [False] * (m + 1) + [True] * (k - 1), n * pitch, pitch, S, off, cnt)
+    assert e.value.code == -2
