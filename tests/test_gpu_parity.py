@@ -118,6 +118,42 @@ def test_rs_decode_all_subsets(ecx):
             assert all((x == y).all() for x, y in zip(allsh, test)), subset
 
 
+def test_rs_big_encode_decode(ecx):
+    """ReedSolomonTest.testBigEncodeDecode (:90-103) on the device: RS(64,64) with
+    200-B shards of java.util.Random(0).nextInt(256) -- a multi-tile map (8 row tiles
+    of 64 entries each).  The encode equals the oracle's; decoding every erasure
+    subset of size <= 2 among shards [0, 10) restores the stripe (the reference's
+    subsets), and so do random 64-shard erasures; on non-codeword shards decodeMissing
+    equals the oracle's map."""
+    import itertools
+    r = O.JavaRandom(0)
+    data = [np.array([r.next_int(256) for _ in range(200)], np.uint8) for _ in range(64)]
+    allsh = [d.copy() for d in data] + [np.zeros(200, np.uint8) for _ in range(64)]
+    ref = [d.copy() for d in data] + [np.zeros(200, np.uint8) for _ in range(64)]
+    rs = ecx.ReedSolomon.create(64, 64)
+    rs.encodeParity(allsh, 0, 200)
+    O.ReedSolomon(64, 64).encode_parity(ref, 0, 200)
+    assert all((a == b).all() for a, b in zip(allsh, ref))
+    rng = np.random.default_rng(64)
+    subsets = [s for n in range(3) for s in itertools.combinations(range(10), n)]
+    subsets += [tuple(int(i) for i in rng.choice(128, 64, replace=False)) for _ in range(4)]
+    for subset in subsets:
+        test = [s.copy() for s in allsh]
+        present = [True] * 128
+        for s in subset:
+            test[s][:] = 0
+            present[s] = False
+        rs.decodeMissing(test, present, 0, 200)
+        assert all((a == b).all() for a, b in zip(allsh, test)), subset
+    for subset in subsets[-2:]:
+        junk = [rng.integers(0, 256, 200, dtype=np.uint8) for _ in range(128)]
+        a, b = [x.copy() for x in junk], [x.copy() for x in junk]
+        present = [i not in subset for i in range(128)]
+        rs.decodeMissing(a, present, 0, 200)
+        O.ReedSolomon(64, 64).decode_missing(b, present, 0, 200)
+        assert all((x == y).all() for x, y in zip(a, b))
+
+
 def test_rs_decode_noncodeword_vs_oracle(ecx):
     rng = np.random.default_rng(12)
     for present in ([1, 0, 1, 1, 0, 1], [0, 1, 1, 1, 1, 1], [1, 1, 1, 1, 0, 0], [0, 0, 1, 1, 1, 1]):
