@@ -4,7 +4,8 @@
  * results are bit-identical for every setting, only speed changes.
  *
  *   "depth"            16-B loads per lane in the kernel's load ring: 0 = per map (default:
- *                      8 when every tile has >= 12 entries, else 4), or force 2 / 4 / 8
+ *                      8 when every tile has >= 12 entries, else 4), or force 2 / 4 / 8 / 12
+ *                      (2: 8-row tiles only; 12: small tiles only; otherwise clamped)
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous
@@ -23,6 +24,8 @@
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
  *   "block_threads"    one-workgroup-per-tile kernel: 256 threads over 4 KiB chunks (default)
  *                      or 64 threads (one wave) over 1 KiB chunks
+ *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
+ *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel (default)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -786,7 +786,7 @@ int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
     Tuning &t = tuning();
     if (k == "depth") {
-        if (value != 0 && value != 2 && value != 4 && value != 8) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value != 0 && value != 2 && value != 4 && value != 8 && value != 12) return ECX_E_ILLEGAL_ARGUMENT;
         t.depth = value;
     }
     else if (k == "nontemporal") {
@@ -803,6 +803,7 @@ int ecx_tune(const char *key, int value) {
     }
     else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "chunk_major") t.chunk_major = value != 0;
+    else if (k == "small_tiles") t.small_tiles = value != 0;
     else if (k == "block_threads") {
         if (value != 64 && value != 256) return ECX_E_ILLEGAL_ARGUMENT;
         t.block_threads = value;

@@ -239,6 +239,7 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         tile[1] = (uint32_t)cols[t].size();
         tile[2] = (uint32_t)rows;
         tile[3] = (uint32_t)cols[t].size();  // unpadded count (k_gf_apply_lds)
+        max_tile_rows_ = std::max(max_tile_rows_, rows);
         for (int r = 0; r < rows; ++r) tile[4 + r] = (uint32_t)map_.out_slot[order[r0 + r]];
         tiles_.insert(tiles_.end(), tile, tile + kTileDwords);
     }

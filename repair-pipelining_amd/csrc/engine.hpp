@@ -85,6 +85,7 @@ public:
     // Load-ring depth for this map: 8 when every non-empty tile has >= 12 entries
     // (padding to a multiple of 8 then costs little), else 4 (profiles/r01_configs_depth.jsonl, r01_configs_sweep2.jsonl).
     int preferred_depth() const { return preferred_depth_; }
+    int max_tile_rows() const { return max_tile_rows_; }
     // The plan uploaded for the current device, each tile's entry list padded to a
     // multiple of `depth` with zero-coefficient kDummySlot entries.
     const DevicePlan &plan_for_current_device(int depth);
@@ -114,7 +115,7 @@ private:
     std::vector<uint32_t> entries_, tiles_;  // unpadded
     std::vector<uint32_t> groups_, unions_;  // unpadded unions
     int n_groups_ = 0, group_size_ = 0;
-    int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1, preferred_depth_ = 4;
+    int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1, preferred_depth_ = 4, max_tile_rows_ = 0;
     std::mutex mu_;
     std::map<std::pair<int, int>, DevicePlan> dev_;  // (device, depth)
 };
@@ -161,6 +162,9 @@ struct Tuning {
     // k_gf_apply workgroup: 256 threads over 4 KiB chunks (default) or 64 threads (one
     // wave) over 1 KiB chunks.
     int block_threads = kBlockThreads;
+    // Single-tile maps of at most 2 / 4 rows: 1 = k_gf_apply variants with that many
+    // accumulator rows (fewer VGPRs, depth-12 rings possible); 0 = the 8-row kernel.
+    int small_tiles = 0;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

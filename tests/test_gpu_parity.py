@@ -784,3 +784,35 @@ def test_rs_batch_codec_entry_points(ecx, torch_dev, k, m):
     with pytest.raises(ecx.EcxError) as e:
         rs.decodeMissingBatch(dev, [False] * (m + 1) + [True] * (k - 1), n * pitch, pitch, S, off, cnt)
     assert e.value.code == -2
+
+
+@pytest.mark.parametrize("n_out", [1, 2, 3, 4])
+def test_small_tile_variants(ecx, torch_dev, n_out):
+    """Single-tile maps of at most 2 / 4 rows on the small-tile kernel variants
+    (ecx_tune "small_tiles"): ring depths 4, 8 and 12 (tiles padded to multiples of
+    12), 1 to 24 entries, coefficient-1 entries, an unaligned tail; each equals the
+    8-row kernel and the oracle's table-driven product."""
+    from conftest import gf_apply_numpy
+    torch = torch_dev
+    rng = np.random.default_rng(50 + n_out)
+    for n_in in (1, 3, 12, 13, 24):
+        m = rng.integers(1, 256, (n_out, n_in)).astype(np.uint8)
+        m[rng.random((n_out, n_in)) < 0.2] = 1
+        gm = ecx.GfMap.from_matrix(m, in_slot=list(range(n_in)), out_slot=list(range(n_out)))
+        S, L = 3, 4096 * 2 + 100
+        inp = torch.empty((S, n_in, L), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(inp, inp.numel(), n_in)
+        host = inp.cpu().numpy()
+        ref = [gf_apply_numpy(m, [host[s, j] for j in range(n_in)]) for s in range(S)]
+        for st, depth in ((0, 0), (1, 4), (1, 8), (1, 12), (1, 0)):
+            ecx.tune("small_tiles", st)
+            ecx.tune("depth", depth)
+            out = torch.full((S, n_out, L), 0xA5, dtype=torch.uint8, device="cuda")
+            gm.apply_batch(inp, n_in * L, L, out, n_out * L, L, S, L)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            for s in range(S):
+                for o in range(n_out):
+                    assert (got[s, o] == ref[s][o]).all(), (n_in, st, depth, s, o)
+    ecx.tune("small_tiles", 0)
+    ecx.tune("depth", 0)
