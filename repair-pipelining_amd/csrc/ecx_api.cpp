@@ -804,6 +804,7 @@ int ecx_tune(const char *key, int value) {
     else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "chunk_major") t.chunk_major = value != 0;
     else if (k == "small_tiles") t.small_tiles = value != 0;
+    else if (k == "host_zero_copy") t.host_zero_copy = value != 0;
     else if (k == "block_threads") {
         if (value != 64 && value != 256) return ECX_E_ILLEGAL_ARGUMENT;
         t.block_threads = value;

@@ -165,6 +165,10 @@ struct Tuning {
     // Single-tile maps of at most 2 / 4 rows: 1 = k_gf_apply variants with that many
     // accumulator rows (fewer VGPRs, depth-12 rings possible); 0 = the 8-row kernel.
     int small_tiles = 0;
+    // Per-call host APIs on the gather path: 1 = the kernel reads / writes the pinned
+    // staging area directly over PCIe instead of one H2D and one D2H copy (20-40 % lower
+    // latency per call, profiles/r01_percall_native.jsonl).
+    int host_zero_copy = 1;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -42,10 +42,13 @@ def main():
         step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
         cases.append((f"Clay(4,2) performCoding repair e=1, B={B}", 28 * B,
                       lambda inputs=inputs, outs=outs, step=step, B=B: step.performCoding(inputs, outs, B)))
-    for name, nbytes, gpu in cases:
-        tg = timeit(gpu)
-        print(json.dumps({"case": name, "us_per_call": round(tg * 1e6, 1), "GiBps": round(nbytes / tg / 2**30, 3)}),
-              flush=True)
+    for zc in (0, 1):
+        ecx.tune("host_zero_copy", zc)
+        for name, nbytes, gpu in cases:
+            tg = timeit(gpu)
+            print(json.dumps({"case": name, "host_zero_copy": zc, "us_per_call": round(tg * 1e6, 1),
+                              "GiBps": round(nbytes / tg / 2**30, 3)}), flush=True)
+    ecx.tune("host_zero_copy", 1)
 
 
 if __name__ == "__main__":

@@ -680,16 +680,18 @@ def test_lrc_batch_abi_encode_and_decode(ecx, torch_dev):
 
 @pytest.mark.parametrize("L", [1, 4097, 300000])
 def test_per_call_paths_agree(ecx, L):
-    """Per-call host entry points: the pinned gather path (one H2D / one D2H) and the
-    per-slot copy path give the oracle's bytes for encode, check and decodeMissing."""
+    """Per-call host entry points: the pinned gather path (one H2D / one D2H), the
+    zero-copy gather path (the kernel reads and writes pinned memory over PCIe) and
+    the per-slot copy path give the oracle's bytes for encode, check and decodeMissing."""
     rng = np.random.default_rng(L)
     base = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(6)]
     ref = [b.copy() for b in base]
     O.ReedSolomon(4, 2).encode_parity(ref, 0, L)
     rs = ecx.ReedSolomon.create(4, 2)
     try:
-        for gather_kib in (0, 1 << 20):
+        for gather_kib, zc in ((0, 0), (1 << 20, 0), (1 << 20, 1)):
             ecx.tune("host_gather_kib", gather_kib)
+            ecx.tune("host_zero_copy", zc)
             sh = [b.copy() for b in base]
             rs.encodeParity(sh, 0, L)
             assert all((sh[i] == ref[i]).all() for i in range(6))
@@ -704,6 +706,7 @@ def test_per_call_paths_agree(ecx, L):
             assert all((sh[i] == ref[i]).all() for i in range(6))
     finally:
         ecx.tune("host_gather_kib", 256)
+        ecx.tune("host_zero_copy", 1)
 
 
 @pytest.mark.parametrize("seed", range(12))
