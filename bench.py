@@ -10,7 +10,7 @@ scaling); the only collectives are the timing barrier and the max-over-ranks.
 Metric: algorithmic bytes per stripe = 20 helper
 sub-chunks read + 8 repaired sub-chunks written = 917,504 B; GiB/s = bytes
 * stripes / time / 2^30, whole job.  ``roofline`` prices the dominant kernel
-(k_gf_apply<false,true,1,8,false,256>) against the MI355X HBM peak from per-launch HIP events;
+(k_gf_apply<false,true,1,8,false,256,8>) against the MI355X HBM peak from per-launch HIP events;
 ``cpu_baseline`` times the oracle (the C restatement of the reference's JVM
 path, stage by stage) on this host for a bounded sample: one thread, then one
 thread per host core (oracle/orc_bench.c).
@@ -45,7 +45,7 @@ READ_BYTES = 20 * B                          # helper sub-chunks read by one rep
 WRITE_BYTES = ALPHA * B                      # repaired sub-chunks written
 ALGO_BYTES = READ_BYTES + WRITE_BYTES        # 917,504 B per stripe
 HBM_PEAK_GBS = 8000.0                        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL = "k_gf_apply<false,true,1,8,false,256>"  # dominant kernel (SAFE=false, NT loads, NT stores, depth 8, SGPR tables)
+KERNEL = "k_gf_apply<false,true,1,8,false,256,8>"  # dominant kernel (SAFE=false, NT loads, NT stores, depth 8, SGPR tables)
 METRIC = "GiB/s repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU"
 
 # workload -> (metric, default resident pool per GPU, default stripes per step per GPU)
@@ -224,7 +224,7 @@ class Clay104(Workload):
     """Config 4: shortened Clay(10,4) (Clay(12,4) with 2 virtual zero data nodes),
     1 MiB node blocks = 256 planes x 4 KiB sub-chunks, single-node repair."""
     k, m, v, b, alpha = 10, 4, 2, 4096, 256
-    kernel = "k_gf_apply<false,false,1,8,true,256>"
+    kernel = "k_gf_apply<false,false,1,8,true,256,8>"
 
     def __init__(self, ecx, torch, dev, P, erased, seed):
         k, m, v, b, a = self.k, self.m, self.v, self.b, self.alpha
@@ -263,7 +263,7 @@ class RS124(Workload):
     reads, writes = 12, 2
     unit_bytes = 14 * (4 << 20)
     write_bytes = 2 * (4 << 20)
-    kernel = "k_gf_apply<false,true,1,8,false,256>"
+    kernel = "k_gf_apply<false,true,1,8,false,256,8>"
 
     def __init__(self, ecx, torch, dev, P, pad, seed):
         self.P, self.torch, self.pitch = P, torch, self.L + pad
@@ -294,7 +294,7 @@ class LRC(Workload):
     reads, writes = 3, 1
     unit_bytes = 4 * 65536
     write_bytes = 65536
-    kernel = "k_gf_apply<false,true,1,4,false,256>"
+    kernel = "k_gf_apply<false,true,1,4,false,256,8>"
 
     def __init__(self, ecx, torch, dev, P, seed):
         import numpy as np
