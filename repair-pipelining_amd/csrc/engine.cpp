@@ -562,24 +562,34 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
     if (byte_count <= 0 || cm.map().n_out == 0) return;
     DeviceContext &ctx = DeviceContext::current();
     std::lock_guard<std::mutex> lk(ctx.mu);
-    if (byte_count <= tuning().host_gather_max && tuning().host_zero_copy) {
+    const int64_t zc_pitch = (byte_count + 255) / 256 * 256;
+    void *zc_dev = nullptr;
+    bool zero_copy = byte_count <= tuning().host_gather_max && tuning().host_zero_copy;
+    if (zero_copy) {
+        const size_t bytes = (size_t)(zc_pitch * (int64_t)(cm.used_in_slots().size() + cm.used_out_slots().size()));
+        if (hipHostGetDevicePointer(&zc_dev, ctx.ensure_pinned(bytes), 0) != hipSuccess) {
+            (void)hipGetLastError();  // clear the sticky error; use the copy path
+            zero_copy = false;
+        }
+    }
+    if (zero_copy) {
         // Zero-copy variant: the kernel reads the gathered inputs from, and writes the
-        // output rows to, the pinned staging area itself over PCIe (no DMA copies).
+        // output rows to, the pinned staging area itself over PCIe (no DMA copies).  If
+        // the staging area is not mapped into the device's address space, the copy path
+        // below runs instead.
         CompiledMap &cc = cm.compact();
         const std::vector<int> &ins = cm.used_in_slots(), &outs = cm.used_out_slots();
         for (int slot : outs)
             if (!outputs[slot]) throw Error(ECX_E_NULL, "output buffer is null");
-        const int64_t pitch = (byte_count + 255) / 256 * 256;
+        const int64_t pitch = zc_pitch;
         const int64_t nin = (int64_t)ins.size(), nout = (int64_t)outs.size();
-        uint8_t *host = ctx.ensure_pinned((size_t)(pitch * (nin + nout)));
+        uint8_t *host = ctx.ensure_pinned((size_t)(pitch * (nin + nout)));  // the same area (already large enough)
         for (int64_t u = 0; u < nin; ++u) {
             const uint8_t *src = inputs[ins[u]];
             if (!src) throw Error(ECX_E_NULL, "input buffer is null");
             std::memcpy(host + u * pitch, src + offset, (size_t)byte_count);
         }
-        void *dptr = nullptr;
-        check_hip(hipHostGetDevicePointer(&dptr, host, 0), "hipHostGetDevicePointer");
-        uint8_t *dev = static_cast<uint8_t *>(dptr);
+        uint8_t *dev = static_cast<uint8_t *>(zc_dev);
         launch_apply(cc, dev, 0, pitch, dev + pitch * nin, 0, pitch, 1, byte_count, ctx.stream);
         check_hip(hipStreamSynchronize(ctx.stream), "hipStreamSynchronize");
         for (int64_t v = 0; v < nout; ++v)
