@@ -9,8 +9,8 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def declared_symbols():
-    text = (ROOT / "include" / "ecx.h").read_text()
+def declared_symbols(header="ecx.h"):
+    text = (ROOT / "include" / header).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(ecx_[a-z0-9_]+)\s*\(", text)))
 
@@ -25,9 +25,13 @@ def test_header_declares_the_boundary():
 
 
 def test_library_exports_every_declared_symbol(ecx):
+    """Every function declared by every header under include/ is exported."""
     lib = ctypes.CDLL(str(ecx.LIB_PATH))
-    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    headers = sorted(p.name for p in (ROOT / "include").glob("*.h"))
+    assert headers == ["ecx.h", "ecx_tune.h"]
+    missing = [s for h in headers for s in declared_symbols(h) if not hasattr(lib, s)]
     assert not missing, missing
+    assert len(declared_symbols("ecx_tune.h")) == 4
 
 
 def test_binding_table_matches_header(ecx):
