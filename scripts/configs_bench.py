@@ -75,6 +75,22 @@ def cases(ecx, torch):
         out.append(("RS(12,4) 2-erasure decode, 4 MiB", 14 * L, S5,
                     lambda rpool=rpool, Lp=Lp: dmap.apply_batch(rpool, 16 * Lp, Lp, rpool, 16 * Lp, Lp, S5, L),
                     {"layout": label}, (rpool, dmap, rs)))
+    # ---- f4: multi-erasure Clay (doDecodeMulti), Clay(4,2) repair of nodes {0, 3}, 32 KiB
+    mrep = ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2)
+    minf = mrep.map().info()
+    mout = torch.empty((P, 16, B), dtype=torch.uint8, device="cuda")
+    out.append(("Clay(4,2) 2-erasure repair {0,3} (doDecodeMulti), 32 KiB", (minf["n_in"] + minf["n_out"]) * B, P,
+                lambda: mrep.performCodingBatch(pool, 48 * B, B, mout, 16 * B, B, P, B), {"map": minf}, (mout, mrep)))
+    # ---- f2: one helper's decodeMissingSingle contribution along a repair chain, XOR-accumulated
+    # into the 2 missing shards' partial sums: RS(12,4), 4 MiB shards; reads the helper's shard and
+    # the 2 partials, writes the 2 partials (5 x 4 MiB per stripe).
+    Sp = 128
+    hin = torch.empty((Sp, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(hin, hin.numel(), 5)
+    acc = torch.zeros((Sp, 2, L), dtype=torch.uint8, device="cuda")
+    present = [False, False] + [True] * 14
+    out.append(("RS(12,4) chain partial sum (decodeMissingSingle batch, accumulate), 4 MiB", 5 * L, Sp,
+                lambda: rs.decodePartialBatch(present, 5, hin, L, acc, 2 * L, L, Sp, L, False), {}, (hin, acc)))
     return out
 
 
