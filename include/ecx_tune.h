@@ -26,6 +26,9 @@
  *                      or 64 threads (one wave) over 1 KiB chunks
  *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
  *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel (default)
+ *   "wide_tiles"       multi-tile maps: pairs of 8-row tiles that share inputs in one workgroup
+ *                      (16 accumulator rows, each shared input loaded once).  1 = when pairing
+ *                      saves >= 1/6 of the input reads (default), 2 = always, 0 = never
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

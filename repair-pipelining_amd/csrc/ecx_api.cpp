@@ -805,6 +805,10 @@ int ecx_tune(const char *key, int value) {
     else if (k == "chunk_major") t.chunk_major = value != 0;
     else if (k == "small_tiles") t.small_tiles = value != 0;
     else if (k == "host_zero_copy") t.host_zero_copy = value != 0;
+    else if (k == "wide_tiles") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.wide_tiles = value;
+    }
     else if (k == "block_threads") {
         if (value != 64 && value != 256) return ECX_E_ILLEGAL_ARGUMENT;
         t.block_threads = value;
@@ -884,6 +888,11 @@ int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
         // tables read as k_gf_apply reads them (SGPRs only, or low dwords from LDS).
         for (int depth : {4, 8}) {
             const HostPlan hp = cm.padded_plan(depth);
+            if (cm.n_wide_tiles() > 0) {
+                std::vector<uint8_t> got(ref.size(), 0);
+                cm.emulate_wide(hp, in.data(), got.data(), len);
+                check(got, "padded plan (wide tiles) differs from the map");
+            }
             for (bool tlds : {false, true}) {
                 std::vector<uint8_t> got(ref.size(), 0);
                 cm.emulate_padded(hp, in.data(), got.data(), len, tlds);

@@ -243,6 +243,69 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         for (int r = 0; r < rows; ++r) tile[4 + r] = (uint32_t)map_.out_slot[order[r0 + r]];
         tiles_.insert(tiles_.end(), tile, tile + kTileDwords);
     }
+    // Wide tiles: pair the 8-row tiles greedily by shared inputs (ties: lowest index);
+    // each pair's entries run over the sorted union of the two tiles' input columns.
+    if (n_tiles_ > 1) {
+        std::vector<std::map<int, uint32_t>> entry_of(n_tiles_);  // column -> entry index
+        for (int t = 0; t < n_tiles_; ++t) {
+            const uint32_t b = tiles_[(size_t)t * kTileDwords], n = tiles_[(size_t)t * kTileDwords + 1];
+            for (uint32_t e = 0; e < n; ++e) entry_of[t][cols[t][e]] = b + e;
+        }
+        std::vector<char> paired(n_tiles_, 0);
+        int min_count = 1 << 30;
+        for (int a = 0; a < n_tiles_; ++a) {
+            if (paired[a]) continue;
+            paired[a] = 1;
+            int b = -1, best = -1;
+            for (int t = 0; t < n_tiles_; ++t) {
+                if (paired[t]) continue;
+                int shared = 0;
+                for (auto &kv : entry_of[t]) shared += entry_of[a].count(kv.first) ? 1 : 0;
+                if (shared > best) {
+                    best = shared;
+                    b = t;
+                }
+            }
+            if (b >= 0) paired[b] = 1;
+            std::vector<int> uni;
+            for (auto &kv : entry_of[a]) uni.push_back(kv.first);
+            if (b >= 0)
+                for (auto &kv : entry_of[b]) uni.push_back(kv.first);
+            std::sort(uni.begin(), uni.end());
+            uni.erase(std::unique(uni.begin(), uni.end()), uni.end());
+            uint32_t rec[kWideTileDwords] = {0};
+            rec[0] = (uint32_t)(wentries_.size() / kWideEntryDwords);
+            rec[1] = (uint32_t)uni.size();
+            rec[2] = tiles_[(size_t)a * kTileDwords + 2];
+            rec[3] = b >= 0 ? tiles_[(size_t)b * kTileDwords + 2] : 0u;
+            for (int r = 0; r < kTileRows; ++r) {
+                rec[4 + r] = tiles_[(size_t)a * kTileDwords + 4 + r];
+                rec[12 + r] = b >= 0 ? tiles_[(size_t)b * kTileDwords + 4 + r] : 0u;
+            }
+            for (int j : uni) {
+                for (int half = 0; half < 2; ++half) {
+                    const int t = half == 0 ? a : b;
+                    uint32_t e[kEntryDwords] = {0};
+                    e[0] = (uint32_t)map_.in_slot[j];
+                    if (t >= 0) {
+                        auto it = entry_of[t].find(j);
+                        if (it != entry_of[t].end()) {
+                            std::copy(entries_.begin() + (size_t)it->second * kEntryDwords,
+                                      entries_.begin() + (size_t)(it->second + 1) * kEntryDwords, e);
+                            e[3] = 0;
+                        }
+                    }
+                    wentries_.insert(wentries_.end(), e, e + kEntryDwords);
+                }
+            }
+            wtiles_.insert(wtiles_.end(), rec, rec + kWideTileDwords);
+            wide_reads_ += (int64_t)entry_of[a].size() + (b >= 0 ? (int64_t)entry_of[b].size() : 0);
+            wide_union_ += (int64_t)uni.size();
+            min_count = std::min(min_count, (int)uni.size());
+            ++n_wide_;
+        }
+        wide_depth_ = min_count >= 12 ? 8 : 4;
+    }
     if (tiles_.empty()) tiles_.assign(kTileDwords, 0);
     if (entries_.empty()) entries_.assign(kEntryDwords, 0);
     if (groups_.empty()) {
@@ -322,6 +385,8 @@ CompiledMap::~CompiledMap() {
         (void)hipFree(kv.second.groups);
         (void)hipFree(kv.second.unions);
         (void)hipFree(kv.second.atab);
+        (void)hipFree(kv.second.wentries);
+        (void)hipFree(kv.second.wtiles);
         (void)hipSetDevice(cur);
     }
 }
@@ -367,7 +432,66 @@ HostPlan CompiledMap::padded_plan(int depth) const {
         rec[9] = padded;
     }
     if (p.unions.empty()) p.unions.assign(1, kDummySlot);
+    // Wide tiles: entry lists padded to a multiple of `depth` with zero-page pairs.
+    p.wtiles = wtiles_;
+    for (int w = 0; w < n_wide_; ++w) {
+        uint32_t *rec = p.wtiles.data() + (size_t)w * kWideTileDwords;
+        const uint32_t begin = rec[0], count = rec[1];
+        rec[0] = (uint32_t)(p.wentries.size() / kWideEntryDwords);
+        p.wentries.insert(p.wentries.end(), wentries_.begin() + (size_t)begin * kWideEntryDwords,
+                          wentries_.begin() + (size_t)(begin + count) * kWideEntryDwords);
+        const uint32_t padded = count == 0 ? 0 : (count + depth - 1) / depth * depth;
+        for (uint32_t d = count; d < padded; ++d) {
+            uint32_t e[kWideEntryDwords] = {0};
+            e[0] = e[kEntryDwords] = kDummySlot;
+            p.wentries.insert(p.wentries.end(), e, e + kWideEntryDwords);
+        }
+        rec[1] = padded;
+    }
+    if (p.wentries.empty()) p.wentries.assign(kWideEntryDwords, 0);
+    if (p.wtiles.empty()) p.wtiles.assign(kWideTileDwords, 0);
     return p;
+}
+
+void CompiledMap::emulate_wide(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const {
+    auto table_byte = [](uint32_t lo, uint32_t hi, int idx) {
+        return (uint8_t)((idx < 4 ? lo : hi) >> (8 * (idx & 3)));
+    };
+    std::vector<uint8_t> acc((size_t)2 * kTileRows * len);
+    for (int w = 0; w < n_wide_; ++w) {
+        const uint32_t *rec = p.wtiles.data() + (size_t)w * kWideTileDwords;
+        std::fill(acc.begin(), acc.end(), 0);
+        if (rec[1] % 4) throw Error(ECX_E_ILLEGAL_ARGUMENT, "wide tile not padded to the ring depth");
+        for (uint32_t e = 0; e < rec[1]; ++e) {
+            const uint32_t *we = p.wentries.data() + ((size_t)rec[0] + e) * kWideEntryDwords;
+            if (we[0] != we[kEntryDwords]) throw Error(ECX_E_ILLEGAL_ARGUMENT, "wide entry halves name different inputs");
+            if (we[0] == kDummySlot) {
+                if (we[1] | we[2] | we[kEntryDwords + 1] | we[kEntryDwords + 2])
+                    throw Error(ECX_E_ILLEGAL_ARGUMENT, "padding entry with coefficients");
+                continue;
+            }
+            const uint8_t *x = in + (int64_t)we[0] * len;
+            for (int half = 0; half < 2; ++half) {
+                const uint32_t *r = we + half * kEntryDwords;
+                for (int o = 0; o < kTileRows; ++o) {
+                    uint8_t *a = acc.data() + (size_t)(half * kTileRows + o) * len;
+                    if (r[2] & (1u << o))
+                        for (int64_t i = 0; i < len; ++i) a[i] ^= x[i];
+                    if (r[1] & (1u << o)) {
+                        const uint32_t *tb = r + 4 + 5 * o;
+                        for (int64_t i = 0; i < len; ++i)
+                            a[i] ^= table_byte(tb[0], tb[1], x[i] & 7) ^ table_byte(tb[2], tb[3], (x[i] >> 3) & 7) ^
+                                    table_byte(tb[4], tb[4], x[i] >> 6);
+                    }
+                }
+            }
+        }
+        for (int half = 0; half < 2; ++half)
+            for (uint32_t o = 0; o < rec[2 + half]; ++o)
+                std::copy(acc.begin() + (size_t)(half * kTileRows + o) * len,
+                          acc.begin() + (size_t)(half * kTileRows + o + 1) * len,
+                          out + (int64_t)rec[4 + 8 * half + o] * len);
+    }
 }
 
 void CompiledMap::emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds) const {
@@ -424,6 +548,8 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     upload(&p.groups, h.groups, "hipMalloc(plan groups)");
     upload(&p.unions, h.unions, "hipMalloc(plan unions)");
     upload(&p.atab, h.atab, "hipMalloc(plan atab)");
+    upload(&p.wentries, h.wentries, "hipMalloc(plan wide entries)");
+    upload(&p.wtiles, h.wtiles, "hipMalloc(plan wide tiles)");
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;
 }
 

@@ -50,16 +50,25 @@ struct DevicePlan {
     // Per padded entry, kTileRows x {T0a, T1a}: the low table dwords of every row,
     // staged per workgroup into LDS by k_gf_apply<..., TLDS=true> (kernels.hip).
     uint32_t *atab = nullptr;
+    uint32_t *wentries = nullptr;  // wide tiles (k_gf_apply_wide)
+    uint32_t *wtiles = nullptr;
     int max_tile_entries = 0;  // padded
 };
 constexpr int kAtabDwords = 2 * kTileRows;
+// Wide tiles (k_gf_apply_wide): two 8-row tiles A, B applied by one workgroup over the
+// union of their inputs.  A wide entry is A's entry for the input followed by B's
+// (kEntryDwords each; zero masks where a half does not read the input).  A wide tile
+// record: [0] first wide entry [1] entry count [2] rows of A [3] rows of B
+// [4..12) output slots of A's rows [12..20) output slots of B's rows.
+constexpr int kWideEntryDwords = 2 * kEntryDwords;
+constexpr int kWideTileDwords = 32;
 constexpr int kMaxLdsTileEntries = 512;  // 32 KiB of LDS per workgroup at most
 
 // The padded plan exactly as uploaded to a device for one load-ring depth
 // (CompiledMap::padded_plan): entries/tiles padded to multiples of `depth`,
 // group unions padded to whole LDS stages, and the TLDS low-table array.
 struct HostPlan {
-    std::vector<uint32_t> entries, tiles, groups, unions, atab;
+    std::vector<uint32_t> entries, tiles, groups, unions, atab, wentries, wtiles;
     int max_tile_entries = 0;
 };
 
@@ -79,6 +88,13 @@ public:
     int n_groups() const { return n_groups_; }
     int group_size() const { return group_size_; }
     int n_entries() const { return (int)(entries_.size() / kEntryDwords); }  // unpadded (1 if empty)
+    // Wide tiles: the 8-row tiles paired by shared inputs (multi-tile maps only).
+    int n_wide_tiles() const { return n_wide_; }
+    int wide_entries() const { return (int)(wentries_.size() / kWideEntryDwords); }  // unpadded
+    int wide_depth() const { return wide_depth_; }
+    // Input reads saved by pairing: (sum of the paired tiles' input counts) / (sum of
+    // the pairs' union sizes); 1.0 = the pairs share nothing.
+    double wide_sharing() const { return wide_union_ ? (double)wide_reads_ / (double)wide_union_ : 1.0; }
     int union_total() const { return (int)unions_.size(); }                   // unpadded
     int max_in_slot() const { return max_in_slot_; }
     int max_out_slot() const { return max_out_slot_; }
@@ -104,6 +120,8 @@ public:
     // read zeros, and with `tlds` the low dword of each 8-entry table comes from
     // HostPlan::atab (the LDS copy) instead of the entry.
     void emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds) const;
+    // The same for the padded wide-tile arrays (k_gf_apply_wide).
+    void emulate_wide(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const;
     CompiledMap &compact();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
@@ -114,7 +132,9 @@ private:
     std::vector<int> used_in_, used_out_;
     std::vector<uint32_t> entries_, tiles_;  // unpadded
     std::vector<uint32_t> groups_, unions_;  // unpadded unions
-    int n_groups_ = 0, group_size_ = 0;
+    std::vector<uint32_t> wentries_, wtiles_;  // unpadded wide tiles
+    int n_groups_ = 0, group_size_ = 0, n_wide_ = 0, wide_depth_ = 4;
+    int64_t wide_reads_ = 0, wide_union_ = 0;
     int n_tiles_ = 0, max_in_slot_ = -1, max_out_slot_ = -1, preferred_depth_ = 4, max_tile_rows_ = 0;
     std::mutex mu_;
     std::map<std::pair<int, int>, DevicePlan> dev_;  // (device, depth)
@@ -128,10 +148,13 @@ struct ApplyArgs {
     const uint32_t *groups;
     const uint32_t *unions;
     const uint32_t *atab;
+    const uint32_t *wentries;
+    const uint32_t *wtiles;
     const uint8_t *zero_page;
     int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
     int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
     int n_tiles;
+    int n_wide;           // k_gf_apply_wide: wide tiles (workgroups per chunk)
     int n_groups;         // k_gf_apply_lds: tile groups (workgroups per chunk)
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
@@ -169,6 +192,9 @@ struct Tuning {
     // staging area directly over PCIe instead of one H2D and one D2H copy (20-40 % lower
     // latency per call, profiles/r01_percall_native.jsonl).
     int host_zero_copy = 1;
+    // Multi-tile maps: 1 = wide tiles (pairs of 8-row tiles sharing inputs, one
+    // workgroup each: 16 accumulator rows, each shared input loaded once per pair).
+    int wide_tiles = 1;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -118,6 +118,78 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
     }
 }
 
+// Wide tiles: one 256-thread workgroup = one (stripe, 4 KiB chunk, pair of 8-row
+// tiles A and B).  Each input of the pair's union is loaded once and applied to
+// both halves (A's and B's entry tables), so a pair that shares inputs reads each of
+// them once instead of twice.  16 accumulator rows; otherwise the loop of apply_tile
+// (zero-page-padded ring of DEPTH loads, SGPR tables).
+template <bool SAFE, bool NTL, int NTS, int DEPTH>
+__global__ void __launch_bounds__(kBlockThreads, 4) k_gf_apply_wide(ApplyArgs a) {
+    const uint32_t w = blockIdx.x % (uint32_t)a.n_wide;
+    const uint32_t rest = blockIdx.x / (uint32_t)a.n_wide;
+    const int64_t c = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);
+    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+    const int64_t cbase = c * kChunkBytes;
+    const uint32_t lane16 = threadIdx.x * 16;
+    int valid = 16;
+    if (SAFE) {
+        const int64_t v = a.nbytes - cbase - (int64_t)lane16;
+        valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
+    }
+    cu32 *rec = plan_ptr(a.wtiles) + __builtin_amdgcn_readfirstlane(w) * kWideTileDwords;
+    const uint8_t *ib = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase))) +
+                        lane16;
+    auto load = [&](uint32_t slot) -> u32x4 {
+        const uint8_t *p = slot == kDummySlot ? a.zero_page + lane16 : ib + (int64_t)slot * a.in_slot_stride;
+        return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
+    };
+    u32x4 acc_a[kTileRows], acc_b[kTileRows];
+#pragma unroll
+    for (int r = 0; r < kTileRows; ++r) acc_a[r] = acc_b[r] = (u32x4){0u, 0u, 0u, 0u};
+    const int ecnt = (int)rec[1];
+    cu32 *ent = plan_ptr(a.wentries) + (int64_t)rec[0] * kWideEntryDwords;
+    if (ecnt > 0) {
+        u32x4 ring[DEPTH];
+#pragma unroll
+        for (int u = 0; u < DEPTH; ++u) ring[u] = load(ent[u * kWideEntryDwords]);
+        const int last = ecnt - DEPTH;
+        for (int e0 = 0; e0 < last; e0 += DEPTH) {
+#pragma unroll
+            for (int u = 0; u < DEPTH; ++u) {
+                cu32 *r = ent + (int64_t)(e0 + u) * kWideEntryDwords;
+                apply_entry<false>(r, ring[u], acc_a, nullptr);
+                apply_entry<false>(r + kEntryDwords, ring[u], acc_b, nullptr);
+                ring[u] = load(r[DEPTH * kWideEntryDwords]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < DEPTH; ++u) {
+            cu32 *r = ent + (int64_t)(last + u) * kWideEntryDwords;
+            apply_entry<false>(r, ring[u], acc_a, nullptr);
+            apply_entry<false>(r + kEntryDwords, ring[u], acc_b, nullptr);
+        }
+    }
+    uint8_t *ob = reinterpret_cast<uint8_t *>(uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase))) + lane16;
+    const int rows_a = (int)rec[2], rows_b = (int)rec[3];
+#pragma unroll
+    for (int o = 0; o < kTileRows; ++o) {
+        if (o < rows_a) {
+            uint8_t *p = ob + (int64_t)rec[4 + o] * a.out_slot_stride;
+            u32x4 v = acc_a[o];
+            if (a.accumulate) v ^= SAFE ? load_partial(p, valid) : load16(p);
+            if (SAFE) store_partial(p, v, valid);
+            else st16<NTS>(p, v);
+        }
+        if (o < rows_b) {
+            uint8_t *p = ob + (int64_t)rec[12 + o] * a.out_slot_stride;
+            u32x4 v = acc_b[o];
+            if (a.accumulate) v ^= SAFE ? load_partial(p, valid) : load16(p);
+            if (SAFE) store_partial(p, v, valid);
+            else st16<NTS>(p, v);
+        }
+    }
+}
+
 // Multi-tile maps, tile groups without staging: one workgroup = one (stripe, 1 KiB
 // chunk, tile GROUP), one wave per tile, each wave loading its own entries directly.
 // The group's tiles share inputs, and each tile's entry list is ordered by the
@@ -169,6 +241,13 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         if (depth == 12) depth = 8;
         if (depth == 2 && (waves || threads != kBlockThreads || nts != 1)) depth = 4;
     }
+    // Wide tiles (pairs of 8-row tiles) for multi-tile maps: auto (1) when pairing
+    // saves at least 1/6 of the input reads (Clay(4,2) encode / repair {0,3}: 40 reads
+    // over a 32-column union, +7-10 %; Clay(10,4) shortened: 80 over 76, where the
+    // 16-row workgroup is 2x slower -- profiles/r01_wide.jsonl), forced (2), off (0).
+    const bool wide = (tu.wide_tiles == 2 || (tu.wide_tiles == 1 && cm.wide_sharing() >= 1.2)) && !waves &&
+                      cm.n_wide_tiles() > 0 && threads == kBlockThreads && rows == kTileRows;
+    if (wide) depth = tu.depth == 8 || tu.depth == 4 ? tu.depth : cm.wide_depth();
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
@@ -186,6 +265,9 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.groups = plan.groups;
     a.unions = plan.unions;
     a.atab = plan.atab;
+    a.wentries = plan.wentries;
+    a.wtiles = plan.wtiles;
+    a.n_wide = cm.n_wide_tiles();
     a.lane_zero = 0;
     a.chunk_major = tu.chunk_major;
     a.n_groups = cm.n_groups();
@@ -203,7 +285,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
         a.n_chunks = n_chunks;
-        const int64_t per_stripe = n_chunks * (waves ? a.n_groups : a.n_tiles);
+        const int64_t per_stripe = n_chunks * (waves ? a.n_groups : (wide ? a.n_wide : a.n_tiles));
         const int64_t max_blocks = (int64_t)1 << 30;
         const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / per_stripe);
         for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
@@ -221,6 +303,19 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                 if (safe) hipLaunchKernelGGL((k_gf_apply_lds<true, 4>), grid, blk, 0, stream, a);
                 else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_lds<false, 8>), grid, blk, 0, stream, a);
                 else hipLaunchKernelGGL((k_gf_apply_lds<false, 4>), grid, blk, 0, stream, a);
+                continue;
+            }
+            if (wide) {
+                const dim3 blk(kBlockThreads);
+                const bool ntl = ntmode == 2 || (ntmode == 1 && a.n_wide == 1);  // one pair: no re-reads
+                if (safe) hipLaunchKernelGGL((k_gf_apply_wide<true, false, 0, 4>), grid, blk, 0, stream, a);
+                else if (depth == 8) {
+                    if (ntl) hipLaunchKernelGGL((k_gf_apply_wide<false, true, 1, 8>), grid, blk, 0, stream, a);
+                    else hipLaunchKernelGGL((k_gf_apply_wide<false, false, 1, 8>), grid, blk, 0, stream, a);
+                } else {
+                    if (ntl) hipLaunchKernelGGL((k_gf_apply_wide<false, true, 1, 4>), grid, blk, 0, stream, a);
+                    else hipLaunchKernelGGL((k_gf_apply_wide<false, false, 1, 4>), grid, blk, 0, stream, a);
+                }
                 continue;
             }
             Shape s;

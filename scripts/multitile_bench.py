@@ -11,6 +11,7 @@ bytes).  Modes:
     grp     -- k_gf_apply_grp: tile groups in one workgroup, each wave loading its own entries
     tiles_d2      -- as tiles_sgpr, load ring of 2 (63 VGPRs, 8 waves per SIMD)
     tiles_d4      -- as tiles, load ring of 4 (6 waves per SIMD)
+    wide    -- k_gf_apply_wide: pairs of 8-row tiles sharing inputs in one workgroup (wide_tiles 2 = forced)
     tiles2  -- k_gf_apply with xcd_group 2 (whole units per XCD)
 
     python scripts/multitile_bench.py                          # all configs x all modes
@@ -50,6 +51,16 @@ def cases(ecx, torch, only):
         out.append(("clay42 encode, 32 KiB", 48 * B * P,
                     lambda pool=pool, par=par, enc=enc, B=B, P=P:
                     enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B), (pool, par, enc)))
+    if only in (None, "clay42multi"):
+        B, P = 32768, 1 << 13
+        pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(pool, pool.numel(), 5)
+        o = torch.empty((P, 16, B), dtype=torch.uint8, device="cuda")
+        mrep = ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2)
+        inf = mrep.map().info()
+        out.append(("clay42 2-erasure repair {0,3}, 32 KiB", (inf["n_in"] + inf["n_out"]) * B * P,
+                    lambda pool=pool, o=o, mrep=mrep, B=B, P=P:
+                    mrep.performCodingBatch(pool, 48 * B, B, o, 16 * B, B, P, B), (pool, o, mrep)))
     if only in (None, "clay42rep"):
         B, P = 32768, 1 << 13
         pool = torch.empty((P, 48, B), dtype=torch.uint8, device="cuda")
@@ -62,21 +73,23 @@ def cases(ecx, torch, only):
     return out
 
 
-MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
-         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
-         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
-         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0},
-         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1, "chunk_major": 0, "block_threads": 256, "depth": 0},
-         "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1, "block_threads": 256, "depth": 0},
+MODES = {"waves": {"wave_groups": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0, "wide_tiles": 0},
+         "tiles": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0, "wide_tiles": 0},
+         "tiles_sgpr": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0, "wide_tiles": 0},
+         "tiles_lds_all": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 2, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0, "wide_tiles": 0},
+         "tiles_sc": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 1, "chunk_major": 0, "block_threads": 256, "depth": 0, "wide_tiles": 0},
+         "tiles_cm": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 1, "block_threads": 256, "depth": 0, "wide_tiles": 0},
          "tiles_w64": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
-                       "block_threads": 64, "depth": 0},
+                       "block_threads": 64, "depth": 0, "wide_tiles": 0},
          "grp": {"wave_groups": 2, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
-                 "block_threads": 256, "depth": 0},
+                 "block_threads": 256, "depth": 0, "wide_tiles": 0},
          "tiles_d2": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 0, "store_scope": 0, "chunk_major": 0,
-                      "block_threads": 256, "depth": 2},
+                      "block_threads": 256, "depth": 2, "wide_tiles": 0},
          "tiles_d4": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
-                      "block_threads": 256, "depth": 4},
-         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0}}
+                      "block_threads": 256, "depth": 4, "wide_tiles": 0},
+         "wide": {"wave_groups": 0, "xcd_group": 0, "lds_tables": 1, "store_scope": 0, "chunk_major": 0,
+                  "block_threads": 256, "depth": 0, "wide_tiles": 2},
+         "tiles2": {"wave_groups": 0, "xcd_group": 2, "lds_tables": 1, "store_scope": 0, "chunk_major": 0, "block_threads": 256, "depth": 0, "wide_tiles": 0}}
 
 
 def main():

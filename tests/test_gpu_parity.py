@@ -617,8 +617,8 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     (k_gf_apply_lds, 1 KiB chunks + byte-safe tail) and the one-workgroup-per-tile
     kernel with its split tables read from SGPRs only or partly from LDS
     (lds_tables 0 / 1 / 2), with `nt sc0 sc1` output stores, in chunk-major block
-    order and with one-wave workgroups over 1 KiB chunks, and the unstaged tile-group
-    kernel (k_gf_apply_grp); all match the oracle on a sampled stripe.  The last
+    order and with one-wave workgroups over 1 KiB chunks, the unstaged tile-group
+    kernel (k_gf_apply_grp) and wide tiles (k_gf_apply_wide); all match the oracle on a sampled stripe.  The last
     case is a single-tile map (Clay(4,2) repair)."""
     torch = torch_dev
     step = ecx.ClayCodeErasureDecodingStep(erased, k, m, virtualUnits=v)
@@ -627,13 +627,16 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 31)
     outs = []
-    for wg, lt, sc, cm, bt in ((1, 1, 0, 0, 256), (0, 0, 0, 0, 256), (0, 1, 0, 0, 256), (0, 2, 0, 0, 256),
-                               (0, 1, 1, 0, 256), (0, 1, 0, 1, 256), (0, 1, 0, 0, 64), (0, 2, 0, 1, 64), (2, 1, 0, 0, 256)):
+    for wg, lt, sc, cm, bt, wd in ((1, 1, 0, 0, 256, 0), (0, 0, 0, 0, 256, 0), (0, 1, 0, 0, 256, 0),
+                                   (0, 2, 0, 0, 256, 0), (0, 1, 1, 0, 256, 0), (0, 1, 0, 1, 256, 0),
+                                   (0, 1, 0, 0, 64, 0), (0, 2, 0, 1, 64, 0), (2, 1, 0, 0, 256, 0),
+                                   (0, 1, 0, 0, 256, 2)):
         ecx.tune("wave_groups", wg)
         ecx.tune("lds_tables", lt)
         ecx.tune("store_scope", sc)
         ecx.tune("chunk_major", cm)
         ecx.tune("block_threads", bt)
+        ecx.tune("wide_tiles", wd)
         o = torch.full((S, len(erased) * a, B), 7, dtype=torch.uint8, device="cuda")
         step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
         torch.cuda.synchronize()
@@ -643,6 +646,7 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     ecx.tune("store_scope", 0)
     ecx.tune("chunk_major", 0)
     ecx.tune("block_threads", 256)
+    ecx.tune("wide_tiles", 1)
     for o in outs[1:]:
         assert (o == outs[0]).all()
     if v == 0:
@@ -732,21 +736,23 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.fill_random(inp, inp.numel(), seed)
     host = inp.cpu().numpy()
     ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
-    for depth, lt, bt in ((4, 0, 256), (4, 2, 256), (8, 0, 256), (8, 2, 256), (8, 2, 64), (4, 0, 64), (2, 0, 256),
-                          (2, 2, 256)):
+    for depth, lt, bt, wd in ((4, 0, 256, 0), (4, 2, 256, 0), (8, 0, 256, 0), (8, 2, 256, 0), (8, 2, 64, 0),
+                              (4, 0, 64, 0), (2, 0, 256, 0), (2, 2, 256, 0), (4, 0, 256, 2), (8, 0, 256, 2)):
         ecx.tune("depth", depth)
         ecx.tune("lds_tables", lt)
         ecx.tune("block_threads", bt)
+        ecx.tune("wide_tiles", wd)
         out = torch.full((S, no, L), 0x5A, dtype=torch.uint8, device="cuda")
         gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         for s in range(S):
             for o, slot in enumerate(out_slot):
-                assert (got[s, slot] == ref[s][o]).all(), (depth, lt, bt, s, o)
+                assert (got[s, slot] == ref[s][o]).all(), (depth, lt, bt, wd, s, o)
     ecx.tune("depth", 0)
     ecx.tune("lds_tables", 1)
     ecx.tune("block_threads", 256)
+    ecx.tune("wide_tiles", 1)
 
 
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
