@@ -713,6 +713,77 @@ def test_per_call_paths_agree(ecx, L):
         ecx.tune("host_zero_copy", 1)
 
 
+def test_per_call_concurrent_threads(ecx):
+    """The reference's callers are per-process pub/sub threads (SURVEY.md section 8b,
+    "Threading"); the C ABI is documented thread-safe.  Eight host threads call the
+    per-call entry points at once -- two sharing one RS(4,2) codec, the others with
+    their own RS or Clay(4,2) objects -- over sizes that take the zero-copy gather
+    path (4 KiB, 32 KiB) and the per-slot copy path (300,000 B); every result must be
+    the oracle's."""
+    import threading
+
+    sizes = (4096, 32768, 300000)
+    rng = np.random.default_rng(99)
+    rs_data = {}
+    for L in sizes:
+        base = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(6)]
+        ref = [b.copy() for b in base]
+        O.ReedSolomon(4, 2).encode_parity(ref, 0, L)
+        rs_data[L] = (base, ref)
+    clay_data = {}
+    for e in (0, 1, 4):
+        B = 4096
+        inputs = [None if (i % 6) == e else rng.integers(0, 256, B, dtype=np.uint8) for i in range(48)]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(4, 2, [e]).perform_coding(inputs, ref, B)
+        clay_data[e] = (inputs, ref)
+    shared_rs = ecx.ReedSolomon.create(4, 2)
+    errors = []
+
+    def rs_worker(tid, rs):
+        try:
+            for it in range(12):
+                L = sizes[(tid + it) % len(sizes)]
+                base, ref = rs_data[L]
+                sh = [b.copy() for b in base]
+                rs.encodeParity(sh, 0, L)
+                if not all((sh[i] == ref[i]).all() for i in range(6)):
+                    errors.append(("encode", tid, it, L))
+                present = [True] * 6
+                present[it % 6] = present[(it + 3) % 6] = False
+                sh[it % 6][:] = 0
+                sh[(it + 3) % 6][:] = 0
+                rs.decodeMissing(sh, present, 0, L)
+                if not all((sh[i] == ref[i]).all() for i in range(6)):
+                    errors.append(("decode", tid, it, L))
+        except Exception as exc:  # noqa: BLE001 -- reported below
+            errors.append(("raised", tid, repr(exc)))
+
+    def clay_worker(tid):
+        try:
+            e = (0, 1, 4)[tid % 3]
+            step = ecx.ClayCodeErasureDecodingStep([e], 4, 2)
+            inputs, ref = clay_data[e]
+            for it in range(12):
+                got = [np.zeros(4096, np.uint8) for _ in range(8)]
+                step.performCoding(inputs, got, 4096)
+                if not all((got[o] == ref[o]).all() for o in range(8)):
+                    errors.append(("clay", tid, it, e))
+        except Exception as exc:  # noqa: BLE001
+            errors.append(("raised", tid, repr(exc)))
+
+    threads = [threading.Thread(target=rs_worker, args=(0, shared_rs)),
+               threading.Thread(target=rs_worker, args=(1, shared_rs))]
+    threads += [threading.Thread(target=rs_worker, args=(t, ecx.ReedSolomon.create(4, 2))) for t in (2, 3, 4)]
+    threads += [threading.Thread(target=clay_worker, args=(t,)) for t in (5, 6, 7)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=90)
+    assert not any(t.is_alive() for t in threads), "a worker thread hung"
+    assert not errors, errors[:5]
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_random_maps_on_device(ecx, torch_dev, seed):
     """Random GF(256) maps of every shape class (single- and multi-tile, sparse and
