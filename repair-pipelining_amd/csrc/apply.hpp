@@ -287,4 +287,8 @@ struct Shape {
 template <int T>
 void launch_shape_t(const Shape &s, dim3 grid, size_t lds, hipStream_t stream, const ApplyArgs &a);
 
+// k_gf_apply_skew (apply_skew.hip): single-tile maps, K = 2 or 4 chunks per workgroup
+// with rotated chunk order; grid = stripes x chunk groups (ApplyArgs::n_chunks groups).
+void launch_skew(int k, int rows, int depth, bool ntl, dim3 grid, hipStream_t stream, const ApplyArgs &a);
+
 }  // namespace ecx

@@ -805,6 +805,10 @@ int ecx_tune(const char *key, int value) {
     else if (k == "chunk_major") t.chunk_major = value != 0;
     else if (k == "small_tiles") t.small_tiles = value != 0;
     else if (k == "host_zero_copy") t.host_zero_copy = value != 0;
+    else if (k == "skew_chunks") {
+        if (value < 0 || value > 4 || value == 3) return ECX_E_ILLEGAL_ARGUMENT;
+        t.skew_chunks = value;
+    }
     else if (k == "wide_tiles") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.wide_tiles = value;

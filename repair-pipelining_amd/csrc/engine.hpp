@@ -195,6 +195,10 @@ struct Tuning {
     // Multi-tile maps: 1 = wide tiles (pairs of 8-row tiles sharing inputs, one
     // workgroup each: 16 accumulator rows, each shared input loaded once per pair).
     int wide_tiles = 1;
+    // Single-tile maps: 2 / 4 = k_gf_apply_skew with that many 4 KiB chunks per
+    // workgroup, each entry's chunk rotated; 1 = 4 when the input slot pitch is a
+    // multiple of 4 MiB; 0 = off.
+    int skew_chunks = 1;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -248,9 +248,22 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool wide = (tu.wide_tiles == 2 || (tu.wide_tiles == 1 && cm.wide_sharing() >= 1.2)) && !waves &&
                       cm.n_wide_tiles() > 0 && threads == kBlockThreads && rows == kTileRows;
     if (wide) depth = tu.depth == 8 || tu.depth == 4 ? tu.depth : cm.wide_depth();
-    const DevicePlan &plan = cm.plan_for_current_device(depth);
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
+    // Skewed chunk order (k_gf_apply_skew) for single-tile maps: forced (2 / 4 chunks),
+    // or auto (1) when the input slot pitch is a multiple of 4 MiB -- the layouts whose
+    // same-offset streams collide in HBM, where rotation recovers +10-17 %; on other
+    // pitches it helps or costs by layout (profiles/r01_pitch_sweep.jsonl).  Auto needs
+    // at least 4 input streams: one helper's partial sum (1 input) only loses.
+    const bool skew_auto = in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4;
+    int skew = tu.skew_chunks == 1 ? (skew_auto ? 4 : 0) : tu.skew_chunks;
+    const int skew_rows = cm.max_tile_rows() <= 2 ? 2 : (cm.max_tile_rows() <= 4 ? 4 : kTileRows);
+    if (skew == 4 && skew_rows == kTileRows) skew = 2;  // 8 rows x 4 chunks would not fit the VGPRs
+    if (!(skew && cm.n_tiles() == 1 && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1 && aligned &&
+          nbytes >= skew * kChunkBytes))
+        skew = 0;
+    if (skew) depth = depth == 4 || skew_rows == kTileRows ? 4 : 8;
+    const DevicePlan &plan = cm.plan_for_current_device(depth);
     // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
     // one workgroup per (stripe, chunk, tile) with 4 KiB (256 threads) or 1 KiB (64) chunks.
     const int64_t chunk = waves ? kWaveChunkBytes : threads * 16;
@@ -333,7 +346,21 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             else launch_shape_t<kBlockThreads>(s, grid, lds, stream, a);
         }
     };
-    run(false, 0, full);
+    int64_t first = 0;  // first full chunk left to the one-chunk kernels
+    if (skew) {
+        const int64_t groups = full / skew;
+        a.chunk_begin = 0;
+        a.n_chunks = groups;
+        const int64_t max_blocks = (int64_t)1 << 30;
+        const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / groups);
+        for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
+            const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
+            a.stripe_begin = s0;
+            launch_skew(skew, skew_rows, depth, true, dim3((unsigned)(ns * groups)), stream, a);
+        }
+        first = groups * skew;
+    }
+    run(false, first, full - first);
     run(true, full, tail_chunks);
     check_hip(hipGetLastError(), "k_gf_apply launch");
 }

@@ -896,3 +896,44 @@ def test_small_tile_variants(ecx, torch_dev, n_out):
                     assert (got[s, o] == ref[s][o]).all(), (n_in, st, depth, s, o)
     ecx.tune("small_tiles", 0)
     ecx.tune("depth", 0)
+
+
+@pytest.mark.parametrize("nbytes", [8192 * 3 + 4096, 4096 * 9 + 100, 65536])
+def test_skew_chunks_agree(ecx, torch_dev, nbytes):
+    """k_gf_apply_skew (ecx_tune "skew_chunks" 2 / 4: several chunks per workgroup,
+    rotated chunk order) gives the bytes of the one-chunk kernel for 2-, 4- and 8-row
+    single-tile maps, with chunk counts that leave a remainder for the one-chunk kernel
+    and a ragged tail, in place (RS) and with accumulation (partial sums)."""
+    torch = torch_dev
+    S = 3
+    rs = ecx.ReedSolomon.create(12, 4)
+    maps = [rs.decode_map([False, False] + [True] * 14)]                  # 2 rows
+    encm = np.zeros((4, 16), np.uint8)
+    for g in range(4):
+        encm[g, 4 * g:4 * g + 3] = 1
+    maps.append(ecx.GfMap.from_matrix(encm, in_slot=list(range(16)), out_slot=[3, 7, 11, 15]))  # 4 rows
+    maps.append(ecx.ClayCodeErasureDecodingStep([1], 4, 2).map())         # 8 rows
+    pitch = nbytes + 512
+    src = torch.empty((S, 48, pitch), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(src, src.numel(), 11)
+    try:
+        for mp in maps:
+            nin = int(mp.matrix()[1].max()) + 1
+            nout = int(mp.matrix()[2].max()) + 1
+            outs = []
+            for skew in (0, 2, 4, 1):
+                ecx.tune("skew_chunks", skew)
+                for acc in (False, True):
+                    o = torch.zeros((S, nout, pitch), dtype=torch.uint8, device="cuda")
+                    if acc:
+                        o.fill_(0x5A)
+                        mp.accumulate_batch(src, 48 * pitch, pitch, o, nout * pitch, pitch, S, nbytes)
+                    else:
+                        mp.apply_batch(src, 48 * pitch, pitch, o, nout * pitch, pitch, S, nbytes)
+                    torch.cuda.synchronize()
+                    outs.append((skew, acc, o))
+            for skew, acc, o in outs:
+                ref = [x for s2, a2, x in outs if s2 == 0 and a2 == acc][0]
+                assert torch.equal(o, ref), (mp.info(), skew, acc, nin)
+    finally:
+        ecx.tune("skew_chunks", 1)
