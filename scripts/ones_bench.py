@@ -47,6 +47,8 @@ def main():
                   16 * B2, P, B2))
     cases.append(("clay42 repair", ecx.ClayCodeErasureDecodingStep([1], 4, 2).map(), pool2, 48 * B2, par,
                   16 * B2, P, B2))
+    cases.append(("clay42 2-erasure repair {0,3}", ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2).map(), pool2,
+                  48 * B2, par, 16 * B2, P, B2))
 
     runs = []
     for name, gmap, inp, iss, out, oss, ns, nb in cases:
