@@ -784,12 +784,12 @@ def test_per_call_concurrent_threads(ecx):
     assert not errors, errors[:5]
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(24))
 def test_random_maps_on_device(ecx, torch_dev, seed):
     """Random GF(256) maps of every shape class (single- and multi-tile, sparse and
     dense, coefficient-1 entries, scattered slots) applied by the device batch path at
     ring depths 2, 4 and 8, with and without the LDS table copy, with 256- and 64-thread
-    workgroups, on a ragged byte count
+    workgroups, on wide tiles and with the skewed chunk order, on a ragged byte count
     over several stripes: each equals the oracle's table-driven product."""
     from conftest import gf_apply_numpy
     torch = torch_dev
@@ -807,23 +807,26 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.fill_random(inp, inp.numel(), seed)
     host = inp.cpu().numpy()
     ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
-    for depth, lt, bt, wd in ((4, 0, 256, 0), (4, 2, 256, 0), (8, 0, 256, 0), (8, 2, 256, 0), (8, 2, 64, 0),
-                              (4, 0, 64, 0), (2, 0, 256, 0), (2, 2, 256, 0), (4, 0, 256, 2), (8, 0, 256, 2)):
+    for depth, lt, bt, wd, sk in ((4, 0, 256, 0, 0), (4, 2, 256, 0, 0), (8, 0, 256, 0, 0), (8, 2, 256, 0, 0),
+                                  (8, 2, 64, 0, 0), (4, 0, 64, 0, 0), (2, 0, 256, 0, 0), (2, 2, 256, 0, 0),
+                                  (4, 0, 256, 2, 0), (8, 0, 256, 2, 0), (8, 0, 256, 0, 2), (4, 0, 256, 0, 4)):
         ecx.tune("depth", depth)
         ecx.tune("lds_tables", lt)
         ecx.tune("block_threads", bt)
         ecx.tune("wide_tiles", wd)
+        ecx.tune("skew_chunks", sk)
         out = torch.full((S, no, L), 0x5A, dtype=torch.uint8, device="cuda")
         gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         for s in range(S):
             for o, slot in enumerate(out_slot):
-                assert (got[s, slot] == ref[s][o]).all(), (depth, lt, bt, wd, s, o)
+                assert (got[s, slot] == ref[s][o]).all(), (depth, lt, bt, wd, sk, s, o)
     ecx.tune("depth", 0)
     ecx.tune("lds_tables", 1)
     ecx.tune("block_threads", 256)
     ecx.tune("wide_tiles", 1)
+    ecx.tune("skew_chunks", 1)
 
 
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
