@@ -940,3 +940,23 @@ def test_skew_chunks_agree(ecx, torch_dev, nbytes):
                 assert torch.equal(o, ref), (mp.info(), skew, acc, nin)
     finally:
         ecx.tune("skew_chunks", 1)
+
+
+def test_every_product_on_device(ecx, torch_dev):
+    """Every GF(256) product c*x through the device kernel's split tables: a 256 x 1
+    map whose row c has coefficient c (0 and 1 included), over an input holding every
+    byte value at every lane position, equals the oracle's MULTIPLICATION_TABLE
+    (Galois.java:178,298-306) -- for each byte lane of the 16-B loads and for the
+    ragged byte-safe tail."""
+    torch = torch_dev
+    mt = O.mul_table()
+    gm = ecx.GfMap.from_matrix(np.arange(256, dtype=np.uint8).reshape(256, 1), in_slot=[0],
+                               out_slot=list(range(256)))
+    L = 256 * 17 + 5  # every byte value at 17 different 16-B lane offsets, plus a ragged tail
+    x = (np.arange(L) * 7 + np.arange(L) // 256) % 256
+    inp = torch.from_numpy(x.astype(np.uint8)).reshape(1, 1, L).cuda()
+    out = torch.zeros((1, 256, L), dtype=torch.uint8, device="cuda")
+    gm.apply_batch(inp, L, L, out, 256 * L, L, 1, L)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()[0]
+    assert (got == mt[:, x]).all()

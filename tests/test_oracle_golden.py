@@ -43,10 +43,12 @@ def test_field_axioms_and_mul_table():
     assert (mt[1] == np.arange(256)).all() and (mt[0] == 0).all()
     for a in range(1, 256):  # inverse: a * (1/a) == 1
         assert mt[a, O.gf_divide(1, a)] == 1
-    rng = np.random.default_rng(1)
-    a, b, c = rng.integers(0, 256, (3, 2000))
-    assert (mt[a, mt[b, c]] == mt[mt[a, b], c]).all()          # associativity
-    assert (mt[a, b ^ c] == (mt[a, b] ^ mt[a, c])).all()        # distributivity
+    # associativity (GaloisTest.java:28-47) and distributivity (:85-100) over all 256^3 triples
+    a = np.arange(256).reshape(256, 1, 1)
+    b = np.arange(256).reshape(1, 256, 1)
+    c = np.arange(256).reshape(1, 1, 256)
+    assert (mt[a, mt[b, c]] == mt[mt[a, b], c]).all()
+    assert (mt[a, b ^ c] == (mt[a, b] ^ mt[a, c])).all()
     for x in (0, 1, 2, 3, 77, 255):                            # exp == repeated multiply (:102-112)
         p = 1
         for n in range(256):
