@@ -1,8 +1,10 @@
 // ecx_api.cpp -- the C ABI (include/ecx.h).  Translates planner/HIP errors into
 // ecx_status codes; every arithmetic entry point executes on the HIP device.
 #include <cstring>
+#include <list>
 #include <map>
 #include <memory>
+#include <unordered_map>
 #include <mutex>
 #include <string>
 
@@ -78,6 +80,50 @@ LinearMap dense_map(const uint8_t *m, int n_out, int n_in) {
     for (int j = 0; j < n_in; ++j) lm.in_slot.push_back(j);
     for (int o = 0; o < n_out; ++o) lm.out_slot.push_back(o);
     return lm;
+}
+
+// The CodingLoop entry points receive their matrix with every call: the reference
+// passes the codec's parity rows or decode rows each time (ReedSolomon.java:105-107,
+// :262-264).  Compiling a plan costs the planner, a device upload and, when the plan
+// is dropped, a hipFree that synchronises the device, so plans are cached by the
+// map's content (least recently used first out; ecx_tune "plan_cache" sets the size,
+// 0 compiles every call).
+std::shared_ptr<CompiledMap> cached_plan(LinearMap lm) {
+    const size_t cap = (size_t)tuning().plan_cache;
+    if (cap == 0) return std::make_shared<CompiledMap>(std::move(lm));
+    std::string key(sizeof(int) * (2 + lm.in_slot.size() + lm.out_slot.size()) + lm.a.size(), '\0');
+    char *k = &key[0];
+    std::memcpy(k, &lm.n_out, sizeof(int));
+    std::memcpy(k + sizeof(int), &lm.n_in, sizeof(int));
+    k += 2 * sizeof(int);
+    std::memcpy(k, lm.in_slot.data(), lm.in_slot.size() * sizeof(int));
+    k += lm.in_slot.size() * sizeof(int);
+    std::memcpy(k, lm.out_slot.data(), lm.out_slot.size() * sizeof(int));
+    k += lm.out_slot.size() * sizeof(int);
+    std::memcpy(k, lm.a.data(), lm.a.size());
+    using Entry = std::pair<std::string, std::shared_ptr<CompiledMap>>;
+    static std::mutex mu;
+    static std::list<Entry> lru;  // front = most recently used
+    static std::unordered_map<std::string, std::list<Entry>::iterator> index;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = index.find(key);
+        if (it != index.end()) {
+            lru.splice(lru.begin(), lru, it->second);
+            return it->second->second;
+        }
+    }
+    auto plan = std::make_shared<CompiledMap>(std::move(lm));  // compiled outside the lock
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = index.find(key);
+    if (it != index.end()) return it->second->second;  // another thread compiled it first
+    lru.emplace_front(key, plan);
+    index[key] = lru.begin();
+    while (lru.size() > cap) {
+        index.erase(lru.back().first);
+        lru.pop_back();  // the plan is freed when its last in-flight user drops it
+    }
+    return plan;
 }
 
 std::vector<bool> present_vec(const uint8_t *p, int n) {
@@ -203,8 +249,8 @@ int ecx_code_some_shards(const uint8_t *matrix_rows, const uint8_t *const *input
     return guarded([&]() -> int {
         if (input_count <= 0 || output_count < 0 || offset < 0 || byte_count < 0)
             throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
-        CompiledMap cm(dense_map(matrix_rows, output_count, input_count).pruned());
-        run_host(cm, inputs, outputs, offset, byte_count);
+        const std::shared_ptr<CompiledMap> cm = cached_plan(dense_map(matrix_rows, output_count, input_count).pruned());
+        run_host(*cm, inputs, outputs, offset, byte_count);
         // Rows with every coefficient zero have no entries but are still written (as zeros) by the kernel.
         return ECX_OK;
     });
@@ -231,8 +277,8 @@ int ecx_check_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inpu
         for (int j = 0; j < w; ++j) lm.in_slot.push_back(j);
         std::vector<const uint8_t *> ptrs(inputs, inputs + input_count);
         ptrs.insert(ptrs.end(), to_check, to_check + check_count);
-        CompiledMap cm(lm.pruned());
-        return run_host_all_zero(cm, ptrs.data(), offset, byte_count) ? 1 : 0;
+        const std::shared_ptr<CompiledMap> cm = cached_plan(lm.pruned());
+        return run_host_all_zero(*cm, ptrs.data(), offset, byte_count) ? 1 : 0;
     });
 }
 
@@ -243,10 +289,10 @@ int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *i
         if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
         const uint8_t c = matrix_rows[(size_t)output_index * row_length + index];
         const uint8_t row[2] = {c, (uint8_t)(is_first_time ? 0 : 1)};
-        CompiledMap cm(dense_map(row, 1, 2));
+        const std::shared_ptr<CompiledMap> cm = cached_plan(dense_map(row, 1, 2));
         const uint8_t *ins[2] = {input, output};
         uint8_t *outs[1] = {output};
-        run_host(cm, ins, outs, offset, byte_count);
+        run_host(*cm, ins, outs, offset, byte_count);
         return ECX_OK;
     });
 }
@@ -805,6 +851,10 @@ int ecx_tune(const char *key, int value) {
     else if (k == "chunk_major") t.chunk_major = value != 0;
     else if (k == "small_tiles") t.small_tiles = value != 0;
     else if (k == "host_zero_copy") t.host_zero_copy = value != 0;
+    else if (k == "plan_cache") {
+        if (value < 0 || value > 4096) return ECX_E_ILLEGAL_ARGUMENT;
+        t.plan_cache = value;
+    }
     else if (k == "skew_chunks") {
         if (value < 0 || value > 4 || value == 3) return ECX_E_ILLEGAL_ARGUMENT;
         t.skew_chunks = value;

@@ -199,6 +199,8 @@ struct Tuning {
     // workgroup, each entry's chunk rotated; 1 = 4 when the input slot pitch is a
     // multiple of 4 MiB; 0 = off.
     int skew_chunks = 1;
+    // Per-call CodingLoop entry points: compiled plans kept, by map content (0 = none).
+    int plan_cache = 256;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

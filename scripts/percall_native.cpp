@@ -67,6 +67,28 @@ int main() {
         }
     }
     ecx_tune("host_zero_copy", 1);
+    // The CodingLoop operator API (EcxCodingLoop.codeSomeShards): the matrix comes with
+    // every call; with and without the plan cache.
+    {
+        uint8_t mat[6 * 4];
+        ecx_rs_matrix(rs, mat);
+        for (int cache : {0, 256}) {
+            ecx_tune("plan_cache", cache);
+            for (int L : {4096, 32768}) {
+                std::vector<std::vector<uint8_t>> sh(6, std::vector<uint8_t>(L));
+                for (auto &s : sh) fill(s);
+                std::vector<const uint8_t *> ip(4);
+                std::vector<uint8_t *> op(2);
+                for (int i = 0; i < 4; ++i) ip[i] = sh[i].data();
+                for (int o = 0; o < 2; ++o) op[o] = sh[4 + o].data();
+                const double us = median_us([&] { return ecx_code_some_shards(mat + 16, ip.data(), 4, op.data(), 2, 0, L); });
+                printf("{\"case\": \"CodingLoop.codeSomeShards RS(4,2) parity, %d B shards\", \"plan_cache\": %d, "
+                       "\"us_per_call\": %.1f}\n", L, cache, us);
+                fflush(stdout);
+            }
+        }
+        ecx_tune("plan_cache", 256);
+    }
     ecx_clay_destroy(clay);
     ecx_rs_destroy(rs);
     return 0;

@@ -960,3 +960,38 @@ def test_every_product_on_device(ecx, torch_dev):
     torch.cuda.synchronize()
     got = out.cpu().numpy()[0]
     assert (got == mt[:, x]).all()
+
+
+def test_code_some_shards_plan_cache(ecx):
+    """CodingLoop.codeSomeShards / checkSomeShards / InputOutputByteTableCodingLoopSingle
+    with the plan cache: repeated matrices (hits), matrices differing in one
+    coefficient or in shape (separate entries), and a cache of 2 plans cycled through
+    5 matrices (evictions) all give the oracle's bytes."""
+    rng = np.random.default_rng(77)
+    mats = [rng.integers(0, 256, (2, 4), dtype=np.uint8) for _ in range(3)]
+    mats.append(mats[0].copy())
+    mats[3][1, 2] ^= 0x11                      # one coefficient apart from mats[0]
+    mats.append(rng.integers(0, 256, (3, 4), dtype=np.uint8))  # another shape
+    loop = ecx.CodingLoop()
+    try:
+        for cap in (256, 2, 0):
+            ecx.tune("plan_cache", cap)
+            for it in range(3):
+                for mi, m in enumerate(mats):
+                    L = 1000 + 37 * it + mi
+                    ins = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(4)]
+                    outs = [np.zeros(L, np.uint8) for _ in range(m.shape[0])]
+                    ref = [np.zeros(L, np.uint8) for _ in range(m.shape[0])]
+                    O.code_some_shards(list(m), ins, ref, 0, L)
+                    loop.codeSomeShards(m, ins, 4, outs, m.shape[0], 0, L)
+                    assert all((a == b).all() for a, b in zip(outs, ref)), (cap, it, mi)
+                    assert loop.checkSomeShards(m, ins, 4, outs, m.shape[0], 0, L)
+                    outs[-1][L // 3] ^= 1
+                    assert not loop.checkSomeShards(m, ins, 4, outs, m.shape[0], 0, L)
+                    x = rng.integers(0, 256, L, dtype=np.uint8)
+                    o = rng.integers(0, 256, L, dtype=np.uint8)
+                    exp = o ^ O.mul_table()[m[0][1]][x]
+                    ecx.InputOutputByteTableCodingLoopSingle().codeSomeShards(m, x, 1, o, 0, 0, L, False)
+                    assert (o == exp).all()
+    finally:
+        ecx.tune("plan_cache", 256)
