@@ -26,9 +26,10 @@
  *                      or 64 threads (one wave) over 1 KiB chunks
  *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
  *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel (default)
- *   "plan_cache"       per-call CodingLoop entry points (ecx_code_some_shards, ecx_check_some_shards,
- *                      ecx_code_single): compiled plans kept, by matrix content (default 256; 0 =
- *                      compile every call)
+ *   "plan_cache"       per-call entry points that receive or derive their coefficients per call
+ *                      (ecx_code_some_shards, ecx_check_some_shards, ecx_code_single,
+ *                      ecx_rs_encode_parity_single, ecx_rs_decode_missing_single): compiled plans
+ *                      kept, by matrix content (default 256; 0 = compile every call)
  *   "skew_chunks"      single-tile maps: 2 / 4 = each workgroup takes that many 4 KiB chunks and
  *                      rotates the chunk each input is read at; 1 = 4 when the input slot pitch
  *                      is a multiple of 4 MiB, else one chunk per workgroup (default); 0 = never

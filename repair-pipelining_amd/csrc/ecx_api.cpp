@@ -384,10 +384,10 @@ int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *outpu
             throw Error(ECX_E_INDEX, "parity row / column index");
         if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
         const uint8_t row[2] = {c.parity_row(output_index)[input_index], 1};
-        CompiledMap cm(dense_map(row, 1, 2));
+        const std::shared_ptr<CompiledMap> cm = cached_plan(dense_map(row, 1, 2));
         const uint8_t *ins[2] = {shard, output};
         uint8_t *outs[1] = {output};
-        run_host(cm, ins, outs, offset, byte_count);
+        run_host(*cm, ins, outs, offset, byte_count);
         return ECX_OK;
     });
 }
@@ -470,8 +470,8 @@ int ecx_rs_decode_missing_single(ecx_rs *rs, const uint8_t *shard, int shard_ind
         for (int j = 0; j < w; ++j) lm.in_slot.push_back(j);
         std::vector<const uint8_t *> ins(1, shard);
         ins.insert(ins.end(), outputs, outputs + output_count);
-        CompiledMap cm(lm.pruned());
-        run_host(cm, ins.data(), outputs, offset, byte_count);
+        const std::shared_ptr<CompiledMap> cm = cached_plan(lm.pruned());
+        run_host(*cm, ins.data(), outputs, offset, byte_count);
         return ECX_OK;
     });
 }

@@ -84,6 +84,14 @@ int main() {
                 const double us = median_us([&] { return ecx_code_some_shards(mat + 16, ip.data(), 4, op.data(), 2, 0, L); });
                 printf("{\"case\": \"CodingLoop.codeSomeShards RS(4,2) parity, %d B shards\", \"plan_cache\": %d, "
                        "\"us_per_call\": %.1f}\n", L, cache, us);
+                // one helper's hop of the pipelined chain (ClayCodeNode.kt:182-186): decodeMissingSingle
+                const uint8_t present[6] = {0, 1, 1, 1, 1, 1};
+                uint8_t *acc[1] = {sh[0].data()};
+                const double us2 = median_us([&] {
+                    return ecx_rs_decode_missing_single(rs, sh[2].data(), 2, 1, present, acc, 1, 0, L, 0);
+                });
+                printf("{\"case\": \"decodeMissingSingle RS(4,2), one helper, accumulate, %d B shards\", "
+                       "\"plan_cache\": %d, \"us_per_call\": %.1f}\n", L, cache, us2);
                 fflush(stdout);
             }
         }
