@@ -12,7 +12,9 @@ import subprocess
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libecx.so"
+# ECX_LIB_PATH: load another build of the same ABI (A/B runs of two kernel builds,
+# scripts/ab_configs.sh); the default is the in-tree build.
+LIB_PATH = Path(os.environ["ECX_LIB_PATH"]) if os.environ.get("ECX_LIB_PATH") else PKG_DIR / "libecx.so"
 HEADER = PKG_DIR.parent / "include" / "ecx.h"
 
 STATUS = {

@@ -37,6 +37,11 @@ def cases(ecx, torch):
     enc = ecx.ClayCodeErasureDecodingStep([4, 5], 4, 2)
     out.append(("Clay(4,2) encode, 32 KiB (16x32 map)", 32 * B + 16 * B, P,
                 lambda: enc.performCodingBatch(pool, 48 * B, B, par, 16 * B, B, P, B), {}, (pool, par, enc)))
+    # ---- config 2 (the headline): Clay(4,2) single repair of node 1, 32 KiB
+    rep = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    rout = torch.empty((P, 8, B), dtype=torch.uint8, device="cuda")
+    out.append(("Clay(4,2) single repair e=1, 32 KiB (headline map)", 28 * B, P,
+                lambda: rep.performCodingBatch(pool, 48 * B, B, rout, 8 * B, B, P, B), {}, (rout, rep)))
     # ---- config 3: LRC 12+4 XOR groups, 64 KiB blocks: encode, and repair of block 2
     B3, S3 = 65536, 1 << 14
     lpool = torch.empty((S3, 16, B3), dtype=torch.uint8, device="cuda")
