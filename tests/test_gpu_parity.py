@@ -995,3 +995,45 @@ def test_code_some_shards_plan_cache(ecx):
                     assert (o == exp).all()
     finally:
         ecx.tune("plan_cache", 256)
+
+
+def test_rs_max_shards_on_device(ecx):
+    """The largest codec the reference accepts (ReedSolomon.java:48-50: at most 256
+    shards): RS(224,32) encode and a 32-shard decode (data and parity mixed) through
+    the per-call host path, against the oracle; one more shard is rejected."""
+    k, m, L = 224, 32, 4096 + 3
+    rng = np.random.default_rng(256)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    a = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+    b = [d.copy() for d in data] + [np.zeros(L, np.uint8) for _ in range(m)]
+    rs = ecx.ReedSolomon.create(k, m)
+    rs.encodeParity(a, 0, L)
+    O.ReedSolomon(k, m).encode_parity(b, 0, L)
+    assert all((x == y).all() for x, y in zip(a, b))
+    erased = sorted(rng.choice(k + m, m, replace=False).tolist())
+    present = [i not in erased for i in range(k + m)]
+    t = [s.copy() for s in a]
+    for i in erased:
+        t[i][:] = 0
+    rs.decodeMissing(t, present, 0, L)
+    assert all((x == y).all() for x, y in zip(a, t)), erased
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.ReedSolomon.create(k, m + 1)
+    assert e.value.code == -4
+
+
+def test_batch_empty_calls_are_noops(ecx, torch_dev):
+    """Zero stripes or a zero byte count (the reference's zero-size encode,
+    ReedSolomonTest.java:32-37, at the batch level) launch nothing and touch nothing."""
+    torch = torch_dev
+    B = 4096
+    pool = torch.full((2, 48, B), 7, dtype=torch.uint8, device="cuda")
+    out = torch.full((2, 8, B), 9, dtype=torch.uint8, device="cuda")
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    step.performCodingBatch(pool, 48 * B, B, out, 8 * B, B, 0, B)
+    step.performCodingBatch(pool, 48 * B, B, out, 8 * B, B, 2, 0)
+    rs = ecx.ReedSolomon.create(12, 4)
+    rs.encodeParityBatch(pool, 48 * B, B, 0, 0, B)
+    rs.encodeParityBatch(pool, 48 * B, B, 2, 0, 0)
+    torch.cuda.synchronize()
+    assert (out == 9).all() and (pool == 7).all()
