@@ -10,7 +10,7 @@ scaling); the only collectives are the timing barrier and the max-over-ranks.
 Metric: algorithmic bytes per stripe = 20 helper
 sub-chunks read + 8 repaired sub-chunks written = 917,504 B; GiB/s = bytes
 * stripes / time / 2^30, whole job.  ``roofline`` prices the dominant kernel
-(k_gf_apply<false,true,1,8,false,256,8>) against the MI355X HBM peak from per-launch HIP events;
+(k_gf_apply<false,true,1,20,false,256,8>: the whole 20-entry tile in flight) against the MI355X HBM peak from per-launch HIP events;
 ``cpu_baseline`` times the oracle (the C restatement of the reference's JVM
 path, stage by stage) on this host for a bounded sample: one thread, then one
 thread per host core (oracle/orc_bench.c).
@@ -45,7 +45,7 @@ READ_BYTES = 20 * B                          # helper sub-chunks read by one rep
 WRITE_BYTES = ALPHA * B                      # repaired sub-chunks written
 ALGO_BYTES = READ_BYTES + WRITE_BYTES        # 917,504 B per stripe
 HBM_PEAK_GBS = 8000.0                        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL = "k_gf_apply<false,true,1,8,false,256,8>"  # dominant kernel (SAFE=false, NT loads, NT stores, depth 8, SGPR tables)
+KERNEL = "k_gf_apply<false,true,1,20,false,256,8>"  # dominant kernel (SAFE=false, NT loads, NT stores, 20-deep ring, SGPR tables)
 METRIC = "GiB/s repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU"
 
 # workload -> (metric, default resident pool per GPU, default stripes per step per GPU)

@@ -251,7 +251,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
 // ROWS < kTileRows: every tile of the map has at most ROWS rows (Shape::rows).
 template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS, int ROWS>
 __global__ void __launch_bounds__(THREADS, ROWS < kTileRows ? (DEPTH >= 12 ? 5 : 6)
-                                                            : (DEPTH == 2 ? 8 : (DEPTH == 4 ? 6 : 5)))
+                                                            : (DEPTH == 2 ? 8 : (DEPTH == 4 ? 6 : (DEPTH <= 8 ? 5 : (DEPTH <= 12 ? 4 : 3)))))
     k_gf_apply(ApplyArgs a) {
     extern __shared__ uint2 lds_tab[];
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);

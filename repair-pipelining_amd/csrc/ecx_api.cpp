@@ -832,7 +832,9 @@ int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
     Tuning &t = tuning();
     if (k == "depth") {
-        if (value != 0 && value != 2 && value != 4 && value != 8 && value != 12) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value != 0 && value != 2 && value != 4 && value != 8 && value != 10 && value != 12 && value != 16 &&
+            value != 20 && value != 24)
+            return ECX_E_ILLEGAL_ARGUMENT;
         t.depth = value;
     }
     else if (k == "nontemporal") {
@@ -940,16 +942,16 @@ int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
         }
         // The padded arrays the device receives, at both ring depths, with the split
         // tables read as k_gf_apply reads them (SGPRs only, or low dwords from LDS).
-        for (int depth : {4, 8}) {
+        for (int depth : {4, 8, 10, 12, 20}) {
             const HostPlan hp = cm.padded_plan(depth);
-            if (cm.n_wide_tiles() > 0) {
+            if (cm.n_wide_tiles() > 0 && depth <= 8) {  // wide tiles run at depth 4 / 8
                 std::vector<uint8_t> got(ref.size(), 0);
                 cm.emulate_wide(hp, in.data(), got.data(), len);
                 check(got, "padded plan (wide tiles) differs from the map");
             }
             for (bool tlds : {false, true}) {
                 std::vector<uint8_t> got(ref.size(), 0);
-                cm.emulate_padded(hp, in.data(), got.data(), len, tlds);
+                cm.emulate_padded(hp, in.data(), got.data(), len, tlds, depth);
                 check(got, tlds ? "padded plan (LDS tables) differs from the map" : "padded plan differs from the map");
             }
         }

@@ -318,6 +318,12 @@ CompiledMap::CompiledMap(LinearMap m) : map_(std::move(m)) {
         if (c > 0) min_count = std::min(min_count, c);
     }
     preferred_depth_ = (min_count != (1 << 30) && min_count >= 12) ? 8 : 4;
+    // A single full (8-row) tile of 17-20 entries -- every Clay(4,2) single repair
+    // (20 helper sub-chunks) -- runs best with all of its loads in flight at once:
+    // a 20-deep ring, no refill, 3 waves/SIMD (+2.3-2.9 % over depth 8 in interleaved
+    // runs, scripts/depth_bench.py, profiles/r01_depth.jsonl).  Shorter or narrower
+    // tiles (RS decode, LRC) measured flat or slower with deep rings.
+    if (n_tiles_ == 1 && max_tile_rows_ == kTileRows && min_count > 16 && min_count <= 20) preferred_depth_ = 20;
 }
 
 void CompiledMap::emulate(const uint8_t *in, uint8_t *out, int64_t len, bool via_unions) const {
@@ -494,7 +500,8 @@ void CompiledMap::emulate_wide(const HostPlan &p, const uint8_t *in, uint8_t *ou
     }
 }
 
-void CompiledMap::emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds) const {
+void CompiledMap::emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds,
+                                 int depth) const {
     auto table_byte = [](uint32_t lo, uint32_t hi, int idx) {
         return (uint8_t)((idx < 4 ? lo : hi) >> (8 * (idx & 3)));
     };
@@ -502,7 +509,7 @@ void CompiledMap::emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *
     for (int t = 0; t < n_tiles_; ++t) {
         const uint32_t *tile = p.tiles.data() + (size_t)t * kTileDwords;
         std::fill(acc.begin(), acc.end(), 0);
-        if (tile[1] % 4) throw Error(ECX_E_ILLEGAL_ARGUMENT, "tile entry count not padded to the ring depth");
+        if (tile[1] % depth) throw Error(ECX_E_ILLEGAL_ARGUMENT, "tile entry count not padded to the ring depth");
         for (uint32_t e = 0; e < tile[1]; ++e) {
             const size_t ei = (size_t)tile[0] + e;
             const uint32_t *rec = p.entries.data() + ei * kEntryDwords;

@@ -119,7 +119,7 @@ public:
     // Host interpretation of a padded plan as k_gf_apply reads it: padding entries
     // read zeros, and with `tlds` the low dword of each 8-entry table comes from
     // HostPlan::atab (the LDS copy) instead of the entry.
-    void emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds) const;
+    void emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds, int depth) const;
     // The same for the padded wide-tile arrays (k_gf_apply_wide).
     void emulate_wide(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const;
     CompiledMap &compact();

@@ -238,8 +238,11 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     if (rows < kTileRows) {
         if (depth != 4 && depth != 8 && depth != 12) depth = 4;
     } else {
-        if (depth == 12) depth = 8;
         if (depth == 2 && (waves || threads != kBlockThreads || nts != 1)) depth = 4;
+        // deep rings (10-24) exist for single-tile maps with NT loads and stores and SGPR tables
+        if (depth > 8 && (cm.n_tiles() != 1 || threads != kBlockThreads || ntmode != 2 || nts != 1 ||
+                          tu.lds_tables == 2))
+            depth = 8;
     }
     // Wide tiles (pairs of 8-row tiles) for multi-tile maps: auto (1) when pairing
     // saves at least 1/6 of the input reads (Clay(4,2) encode / repair {0,3}: 40 reads

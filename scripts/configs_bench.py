@@ -104,13 +104,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--sweep", action="store_true", help="also the non-default launch shapes of SWEEP")
+    ap.add_argument("--depths", default=None, help="comma list of ring depths to sweep (nt 1), e.g. 0,8,12,20")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
     lib = ecx.lib()
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
     cs = cases(ecx, torch)
-    for depth, nt in (SWEEP if args.sweep else SWEEP[:1]):
+    shapes = SWEEP if args.sweep else SWEEP[:1]
+    if args.depths:
+        shapes = [(int(d), 1) for d in args.depths.split(",")]
+    for depth, nt in shapes:
         lib.ecx_tune(b"depth", depth)
         lib.ecx_tune(b"nontemporal", nt)
         times = {i: [] for i in range(len(cs))}

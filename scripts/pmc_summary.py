@@ -14,7 +14,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNEL = "k_gf_apply<false, true, 1, 8, false, 256, 8>"
+KERNEL = "k_gf_apply<false, true, 1, 20, false, 256, 8>"
 POOL, B = 1 << 15, 32768
 GRID = POOL * 8 * 256  # threads of one pool launch (8 chunks x 256 lanes per stripe)
 
@@ -30,7 +30,7 @@ def main():
     wr = statistics.median(write) * 1024
     algo_rd, algo_wr = POOL * 20 * B, POOL * 8 * B
     out = {
-        "kernel": "k_gf_apply<false,true,1,8,false,256,8>",
+        "kernel": "k_gf_apply<false,true,1,20,false,256,8>",
         "pool_stripes": POOL,
         "launches_sampled": [len(fetch), len(write)],
         "FETCH_SIZE_KB_median": statistics.median(fetch),

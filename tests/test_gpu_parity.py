@@ -788,7 +788,7 @@ def test_per_call_concurrent_threads(ecx):
 def test_random_maps_on_device(ecx, torch_dev, seed):
     """Random GF(256) maps of every shape class (single- and multi-tile, sparse and
     dense, coefficient-1 entries, scattered slots) applied by the device batch path at
-    ring depths 2, 4 and 8, with and without the LDS table copy, with 256- and 64-thread
+    ring depths 2 to 24 (deep rings: single-tile maps), with and without the LDS table copy, with 256- and 64-thread
     workgroups, on wide tiles and with the skewed chunk order, on a ragged byte count
     over several stripes: each equals the oracle's table-driven product."""
     from conftest import gf_apply_numpy
@@ -809,7 +809,9 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
     for depth, lt, bt, wd, sk in ((4, 0, 256, 0, 0), (4, 2, 256, 0, 0), (8, 0, 256, 0, 0), (8, 2, 256, 0, 0),
                                   (8, 2, 64, 0, 0), (4, 0, 64, 0, 0), (2, 0, 256, 0, 0), (2, 2, 256, 0, 0),
-                                  (4, 0, 256, 2, 0), (8, 0, 256, 2, 0), (8, 0, 256, 0, 2), (4, 0, 256, 0, 4)):
+                                  (4, 0, 256, 2, 0), (8, 0, 256, 2, 0), (8, 0, 256, 0, 2), (4, 0, 256, 0, 4),
+                                  (10, 0, 256, 0, 0), (12, 0, 256, 0, 0), (16, 0, 256, 0, 0), (20, 0, 256, 0, 0),
+                                  (24, 0, 256, 0, 0), (20, 2, 256, 0, 0)):
         ecx.tune("depth", depth)
         ecx.tune("lds_tables", lt)
         ecx.tune("block_threads", bt)
