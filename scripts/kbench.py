@@ -62,18 +62,21 @@ def main():
 
     variants = []
     for v in args.variants.split(","):
-        depth, nt = map(int, v.split(":"))
-        variants.append((f"clay depth={depth} nt={nt}", clay, depth, nt, P * ALGO))
-    variants.append(("xor-only depth=4 nt=1", xor_only, 4, 1, P * ALGO))
-    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE))
-    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE))
-    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE))
-    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE))
-    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B))
+        f = list(map(int, v.split(":")))
+        depth, nt = f[0], f[1]
+        threads = f[2] if len(f) > 2 else 256
+        variants.append((f"clay depth={depth} nt={nt} threads={threads}", clay, depth, nt, P * ALGO, threads))
+    variants.append(("xor-only depth=0 nt=1", xor_only, 0, 1, P * ALGO, 256))
+    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE, 256))
+    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE, 256))
+    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE, 256))
+    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE, 256))
+    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B, 256))
 
     res = {name: [] for name, *_ in variants}
     for r in range(args.rounds):
-        for name, fn, depth, nt, nbytes in variants:
+        for name, fn, depth, nt, nbytes, threads in variants:
+            lib.ecx_tune(b"block_threads", threads)
             lib.ecx_tune(b"depth", depth)
             lib.ecx_tune(b"nontemporal", nt)
             fn()
@@ -88,6 +91,7 @@ def main():
             res[name].append(nbytes / (ms * 1e-3) / 1e9)
     lib.ecx_tune(b"depth", 0)
     lib.ecx_tune(b"nontemporal", 1)
+    lib.ecx_tune(b"block_threads", 256)
     for name, *_ in variants:
         v = res[name]
         print(json.dumps({"variant": name, "GBps_median": round(statistics.median(v), 1),
