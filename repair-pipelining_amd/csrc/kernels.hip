@@ -240,7 +240,8 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     } else {
         if (depth == 2 && (waves || threads != kBlockThreads || nts != 1)) depth = 4;
         // deep rings (10-24) exist for single-tile maps with NT loads and stores and SGPR tables
-        if (depth > 8 && (cm.n_tiles() != 1 || threads != kBlockThreads || ntmode != 2 || nts != 1 ||
+        if (depth > 8 && (cm.n_tiles() != 1 || threads != kBlockThreads || ntmode != 2 ||
+                          (nts != 1 && !(nts == 2 && depth == 20)) ||
                           tu.lds_tables == 2))
             depth = 8;
     }

@@ -65,18 +65,21 @@ def main():
         f = list(map(int, v.split(":")))
         depth, nt = f[0], f[1]
         threads = f[2] if len(f) > 2 else 256
-        variants.append((f"clay depth={depth} nt={nt} threads={threads}", clay, depth, nt, P * ALGO, threads))
-    variants.append(("xor-only depth=0 nt=1", xor_only, 0, 1, P * ALGO, 256))
-    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE, 256))
-    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE, 256))
-    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE, 256))
-    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE, 256))
-    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B, 256))
+        scope = f[3] if len(f) > 3 else 0
+        variants.append((f"clay depth={depth} nt={nt} threads={threads} store_scope={scope}", clay, depth, nt,
+                         P * ALGO, threads, scope))
+    variants.append(("xor-only depth=0 nt=1", xor_only, 0, 1, P * ALGO, 256, 0))
+    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE, 256, 0))
+    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE, 256, 0))
+    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE, 256, 0))
+    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE, 256, 0))
+    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B, 256, 0))
 
     res = {name: [] for name, *_ in variants}
     for r in range(args.rounds):
-        for name, fn, depth, nt, nbytes, threads in variants:
+        for name, fn, depth, nt, nbytes, threads, scope in variants:
             lib.ecx_tune(b"block_threads", threads)
+            lib.ecx_tune(b"store_scope", scope)
             lib.ecx_tune(b"depth", depth)
             lib.ecx_tune(b"nontemporal", nt)
             fn()
@@ -92,6 +95,7 @@ def main():
     lib.ecx_tune(b"depth", 0)
     lib.ecx_tune(b"nontemporal", 1)
     lib.ecx_tune(b"block_threads", 256)
+    lib.ecx_tune(b"store_scope", 0)
     for name, *_ in variants:
         v = res[name]
         print(json.dumps({"variant": name, "GBps_median": round(statistics.median(v), 1),
