@@ -4,8 +4,10 @@
  * results are bit-identical for every setting, only speed changes.
  *
  *   "depth"            16-B loads per lane in the kernel's load ring: 0 = per map (default:
- *                      8 when every tile has >= 12 entries, else 4), or force 2 / 4 / 8 / 12
- *                      (2: 8-row tiles only; 12: small tiles only; otherwise clamped)
+ *                      20 for a single full tile of 17-20 entries, 8 when every tile has >= 12
+ *                      entries, else 4), or force 2 / 4 / 8 / 10 / 12 / 16 / 20 / 24 (2: 8-row
+ *                      tiles only; 10-24: single-tile maps with non-temporal loads; otherwise
+ *                      clamped)
  *   "nontemporal"      0 = plain loads/stores; 1 = auto (default): non-temporal stores, and
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous

@@ -165,7 +165,7 @@ struct ApplyArgs {
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
 struct Tuning {
     // Defaults are the fastest shape measured on MI355X (profiles/r01_kbench.txt).
-    int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or 4 / 8
+    int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or forced
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
     // Multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS), 2 =
