@@ -62,24 +62,31 @@ def main():
 
     variants = []
     for v in args.variants.split(","):
+        extra = {}
+        if "@" in v:  # depth:nt[:threads[:scope]]@key=value;key=value (any ecx_tune key)
+            v, kv = v.split("@", 1)
+            extra = {k: int(x) for k, x in (p.split("=") for p in kv.split(";"))}
         f = list(map(int, v.split(":")))
         depth, nt = f[0], f[1]
         threads = f[2] if len(f) > 2 else 256
         scope = f[3] if len(f) > 3 else 0
-        variants.append((f"clay depth={depth} nt={nt} threads={threads} store_scope={scope}", clay, depth, nt,
-                         P * ALGO, threads, scope))
-    variants.append(("xor-only depth=0 nt=1", xor_only, 0, 1, P * ALGO, 256, 0))
-    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE, 256, 0))
-    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE, 256, 0))
-    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE, 256, 0))
-    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE, 256, 0))
-    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B, 256, 0))
+        tag = "".join(f" {k}={x}" for k, x in extra.items())
+        variants.append((f"clay depth={depth} nt={nt} threads={threads} store_scope={scope}{tag}", clay, depth, nt,
+                         P * ALGO, threads, scope, extra))
+    variants.append(("xor-only depth=0 nt=1", xor_only, 0, 1, P * ALGO, 256, 0, {}))
+    variants.append(("probe read nt=0", probe(0, 0), 4, 0, PROBE, 256, 0, {}))
+    variants.append(("probe read nt=1", probe(0, 1), 4, 0, PROBE, 256, 0, {}))
+    variants.append(("probe copy nt=0", probe(1, 0), 4, 0, 2 * PROBE, 256, 0, {}))
+    variants.append(("probe copy nt=1", probe(1, 1), 4, 0, 2 * PROBE, 256, 0, {}))
+    variants.append(("d2d copy (torch)", copy, 4, 0, 2 * P * ALPHA * B, 256, 0, {}))
 
     res = {name: [] for name, *_ in variants}
     for r in range(args.rounds):
-        for name, fn, depth, nt, nbytes, threads, scope in variants:
+        for name, fn, depth, nt, nbytes, threads, scope, extra in variants:
             lib.ecx_tune(b"block_threads", threads)
             lib.ecx_tune(b"store_scope", scope)
+            for k, x in extra.items():
+                lib.ecx_tune(k.encode(), x)
             lib.ecx_tune(b"depth", depth)
             lib.ecx_tune(b"nontemporal", nt)
             fn()
@@ -92,6 +99,8 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.launches
             res[name].append(nbytes / (ms * 1e-3) / 1e9)
+            for k in extra:  # back to the library default
+                lib.ecx_tune(k.encode(), {"xcd_group": 0, "chunk_major": 0}.get(k, 0))
     lib.ecx_tune(b"depth", 0)
     lib.ecx_tune(b"nontemporal", 1)
     lib.ecx_tune(b"block_threads", 256)
