@@ -181,9 +181,28 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
     const int ebeg = (int)tile[0];
     const int ecnt = (int)tile[1];
     const int nrows = (int)tile[2];
+    // TLDS kernels (multi-tile maps, where the multiply keeps the vector pipe busy)
+    // load through a buffer descriptor over this workgroup's stripe chunk: the slot's
+    // byte offset is a scalar soffset (s_mul of the plan's slot by the slot stride)
+    // and the lane's 16 bytes the voffset, so an entry costs no VALU address
+    // arithmetic (launch_apply checks that every offset fits 32 bits).  Padding
+    // entries re-read the tile's first input (coefficient 0, an L2 hit) instead of
+    // selecting the zero page.  Other kernels use 64-bit global addresses.
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t first_soff = 0;
+    if constexpr (TLDS && !SAFE) {
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(in_base), 0, 0x7FFFFFFF, 0x00020000);
+        if (ecnt > 0) first_soff = plan_ptr(a.entries)[(int64_t)ebeg * kEntryDwords] * (uint32_t)a.in_slot_stride;
+    }
     auto load = [&](uint32_t slot) -> u32x4 {  // padding entries read the zero page
-        const uint8_t *p = slot == kDummySlot ? a.zero_page + zoff : ib + (int64_t)slot * a.in_slot_stride;
-        return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
+        if constexpr (TLDS && !SAFE) {
+            const uint32_t soff = slot == kDummySlot ? first_soff : slot * (uint32_t)a.in_slot_stride;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)zoff, (int)soff, NTL ? 2 : 0);
+            return (u32x4){(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]};
+        } else {
+            const uint8_t *p = slot == kDummySlot ? a.zero_page + zoff : ib + (int64_t)slot * a.in_slot_stride;
+            return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
+        }
     };
 
     u32x4 acc[ROWS];

@@ -137,11 +137,26 @@ __global__ void __launch_bounds__(kBlockThreads, 4) k_gf_apply_wide(ApplyArgs a)
         valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
     }
     cu32 *rec = plan_ptr(a.wtiles) + __builtin_amdgcn_readfirstlane(w) * kWideTileDwords;
-    const uint8_t *ib = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase))) +
-                        lane16;
+    const uint64_t in_base = uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase));
+    const uint8_t *ib = reinterpret_cast<const uint8_t *>(in_base) + lane16;
+    // Buffer-descriptor addressing as in apply_tile's TLDS kernels (apply.hpp): the
+    // slot offset is a scalar soffset, padding re-reads the pair's first input.
+    cu32 *went = plan_ptr(a.wentries) + (int64_t)rec[0] * kWideEntryDwords;
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t first_soff = 0;
+    if constexpr (!SAFE) {
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(in_base), 0, 0x7FFFFFFF, 0x00020000);
+        if (rec[1] > 0) first_soff = went[0] * (uint32_t)a.in_slot_stride;  // a pair with no inputs loads nothing
+    }
     auto load = [&](uint32_t slot) -> u32x4 {
-        const uint8_t *p = slot == kDummySlot ? a.zero_page + lane16 : ib + (int64_t)slot * a.in_slot_stride;
-        return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
+        if constexpr (!SAFE) {
+            const uint32_t soff = slot == kDummySlot ? first_soff : slot * (uint32_t)a.in_slot_stride;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)lane16, (int)soff, NTL ? 2 : 0);
+            return (u32x4){(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]};
+        } else {
+            const uint8_t *p = slot == kDummySlot ? a.zero_page + lane16 : ib + (int64_t)slot * a.in_slot_stride;
+            return load_partial(p, valid);
+        }
     };
     u32x4 acc_a[kTileRows], acc_b[kTileRows];
 #pragma unroll
@@ -249,8 +264,10 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // saves at least 1/6 of the input reads (Clay(4,2) encode / repair {0,3}: 40 reads
     // over a 32-column union, +7-10 %; Clay(10,4) shortened: 80 over 76, where the
     // 16-row workgroup is 2x slower -- profiles/r01_wide.jsonl), forced (2), off (0).
+    const bool offsets32 = in_slot_stride >= 0 &&
+                           (int64_t)cm.max_in_slot() * in_slot_stride + kChunkBytes <= 0x7FFFFFFF;
     const bool wide = (tu.wide_tiles == 2 || (tu.wide_tiles == 1 && cm.wide_sharing() >= 1.2)) && !waves &&
-                      cm.n_wide_tiles() > 0 && threads == kBlockThreads && rows == kTileRows;
+                      cm.n_wide_tiles() > 0 && threads == kBlockThreads && rows == kTileRows && offsets32;
     if (wide) depth = tu.depth == 8 || tu.depth == 4 ? tu.depth : cm.wide_depth();
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
@@ -340,7 +357,9 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             s.ntl = ntmode == 2;
             s.nts = nts;
             s.depth = depth;
-            s.tlds = !safe && rows == kTileRows && plan.max_tile_entries > 0 &&
+            // TLDS kernels address inputs through a buffer descriptor with 32-bit slot
+            // offsets (apply.hpp): every slot's chunk must lie within 2 GiB of the stripe chunk.
+            s.tlds = !safe && rows == kTileRows && plan.max_tile_entries > 0 && offsets32 &&
                      plan.max_tile_entries <= kMaxLdsTileEntries &&
                      (tu.lds_tables == 2 || (tu.lds_tables == 1 && a.n_tiles > 1));
             s.threads = threads;
