@@ -10,10 +10,15 @@ scaling); the only collectives are the timing barrier and the max-over-ranks.
 Metric: algorithmic bytes per stripe = 20 helper
 sub-chunks read + 8 repaired sub-chunks written = 917,504 B; GiB/s = bytes
 * stripes / time / 2^30, whole job.  ``roofline`` prices the dominant kernel
-(k_gf_apply<false,true,1,20,false,256,8>: the whole 20-entry tile in flight) against the MI355X HBM peak from per-launch HIP events;
+(the k_gf_apply instance the library reports it launched, ecx_last_kernel) against
+the MI355X HBM peak from per-launch HIP events;
 ``cpu_baseline`` times the oracle (the C restatement of the reference's JVM
 path, stage by stage) on this host for a bounded sample: one thread, then one
-thread per host core (oracle/orc_bench.c).
+thread per CPU of the lease, over a working set of >= 2x the host L3 (oracle/orc_bench.c).
+
+``--gpus N`` runs N ranks, one process per GPU: under torch.distributed.run (the
+driver's launch) each process is one rank; without a launcher, bench.py starts
+torch.distributed.run itself as a child process.
 
 ``--workload`` runs the other multi-GPU BASELINE configs with the same
 contract (same launch, timing and JSON line; the default is the headline):
@@ -45,7 +50,6 @@ READ_BYTES = 20 * B                          # helper sub-chunks read by one rep
 WRITE_BYTES = ALPHA * B                      # repaired sub-chunks written
 ALGO_BYTES = READ_BYTES + WRITE_BYTES        # 917,504 B per stripe
 HBM_PEAK_GBS = 8000.0                        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL = "k_gf_apply<false,true,1,20,false,256,8>"  # dominant kernel (SAFE=false, NT loads, NT stores, 20-deep ring, SGPR tables)
 METRIC = "GiB/s repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU"
 
 # workload -> (metric, default resident pool per GPU, default stripes per step per GPU)
@@ -70,6 +74,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample; 0 = skip")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-probes", action="store_true", help="skip the in-run memory ceiling probes")
+    ap.add_argument("--meta", default=None, help="write the launch metadata (kernel, pool, bytes per launch, "
+                                                 "kernel-source hash) as JSON here (scripts/pmc.sh)")
     args = ap.parse_args()
     _metric, pool, per_step = WORKLOADS[args.workload]
     args.pool = args.pool or pool
@@ -89,14 +95,60 @@ def _cpu_model() -> str:
     return "unknown CPU"
 
 
+def _size_bytes(text: str) -> int:
+    t = text.strip().upper()
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(t[-1:], 1)
+    return int(t.rstrip("KMG")) * mult
+
+
+def host_cpu_info() -> dict:
+    """What the CPU baseline may use on this host: CPUs present, the affinity mask, the
+    cgroup CPU quota (the lease's share; os.cpu_count() shows the whole machine), and
+    the L3 capacity of the whole machine and of the CPUs in the affinity mask (sum over
+    distinct L3 instances, /sys/devices/system/cpu/*/cache/index3)."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    l3_all, l3_aff, seen = 0, 0, set()
+    for cpu in range(os.cpu_count() or 1):
+        d = "/sys/devices/system/cpu/cpu%d/cache/index3" % cpu
+        try:
+            shared = open(d + "/shared_cpu_list").read().strip()
+            size = _size_bytes(open(d + "/size").read())
+        except (OSError, ValueError):
+            continue
+        if shared in seen:
+            continue
+        seen.add(shared)
+        l3_all += size
+        members = set()
+        for part in shared.split(","):
+            lo, _, hi = part.partition("-")
+            members.update(range(int(lo), int(hi or lo) + 1))
+        if members & set(aff):
+            l3_aff += size
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"model": _cpu_model(), "cpus_present": os.cpu_count(), "affinity_cpus": len(aff),
+            "cgroup_quota_cpus": quota, "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "l3_bytes_machine": l3_all or None, "l3_bytes_affinity": l3_aff or None}
+
+
 def cpu_baseline(seconds: float, erased: int, sample=None):
     """Oracle (C restatement of the reference JVM path: InputOutputByteTableCodingLoop
     + the ClayCodeErasureDecodingStep.doDecodeSingle stage sequence), timed by
-    oracle/orc_bench.c on one host thread and then on one thread per host core
-    (independent stripes per thread).  ``value`` is the
-    all-cores figure; the 1-thread figure rides along.  `sample` = (stripe, GPU repair
-    output) of one pool stripe: the oracle repairs it too, and ``oracle_check`` says
-    whether the bytes agree (the sampled byte-compare of SURVEY.md 8(d))."""
+    oracle/orc_bench.c on one host thread and then on one thread per CPU the lease
+    allows (the cgroup quota, else the affinity mask; independent stripes per thread,
+    SURVEY.md section 8(d)).  Following ReedSolomonBenchmark.java:25-33, the stripes
+    cycled through span at least twice the machine's L3, so the repairs stream from
+    DRAM as the reference's benchmark does.  ``value`` is the all-threads figure; the
+    1-thread figure rides along.  `sample` = (stripe, GPU repair output) of one pool
+    stripe: the oracle repairs it too, and ``oracle_check`` says whether the bytes
+    agree (the sampled byte-compare of SURVEY.md 8(d))."""
     import numpy as np
     import oracle as O
 
@@ -108,23 +160,36 @@ def cpu_baseline(seconds: float, erased: int, sample=None):
         O.Clay(K, M, [erased]).perform_coding(inputs, ref, B)
         oracle_check = all(bool((got[z] == ref[z]).all()) for z in range(ALPHA))
 
-    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
-    threads = max(1, min(threads, len(os.sched_getaffinity(0)), 64))
-    per_thread = 2
+    info = host_cpu_info()
+    threads = info["cgroup_quota_cpus"] or info["omp_num_threads"] or info["affinity_cpus"]
+    threads = max(1, min(threads, info["affinity_cpus"], 256))
+    # Working set: the helper + output bytes a repair touches (ALGO_BYTES), summed over
+    # every stripe cycled through, >= 2x the machine's L3 (32 MiB assumed if unknown).
+    l3 = info["l3_bytes_machine"] or (32 << 20)
+    n_stripes = max(2 * threads, -(-2 * l3 // ALGO_BYTES))
+    per_thread = -(-n_stripes // threads)
+    n_stripes = per_thread * threads
     rng = np.random.default_rng(0)
 
-    def stripe():
+    # 8 distinct valid stripes (random data + oracle encode), tiled through one host
+    # arena of n_stripes stripes: every stripe has its own memory (the cache sees the
+    # whole working set), the bytes repeat every 8 stripes.
+    distinct = []
+    for _ in range(8):
         data = [rng.integers(0, 256, B, dtype=np.uint8) if (i % N_NODES) < K else None
                 for i in range(N_NODES * ALPHA)]
         par = O.clay_encode(K, M, data, B)
-        full = [data[i] if (i % N_NODES) < K else par[(i // N_NODES) * M + (i % N_NODES) - K]
-                for i in range(N_NODES * ALPHA)]
-        return [None if (i % N_NODES) == erased else full[i] for i in range(N_NODES * ALPHA)]
-
-    stripes = [stripe() for _ in range(per_thread * threads)]
-    n1, el1 = O.bench_clay_repair(K, M, erased, B, stripes[:per_thread], 1, seconds / 2)
+        distinct.append(np.stack([data[i] if (i % N_NODES) < K else par[(i // N_NODES) * M + (i % N_NODES) - K]
+                                  for i in range(N_NODES * ALPHA)]))
+    arena = np.empty((n_stripes, N_NODES * ALPHA, B), np.uint8)
+    for s in range(n_stripes):
+        arena[s] = distinct[s % 8]
+    stripes = [[None if (i % N_NODES) == erased else arena[s, i] for i in range(N_NODES * ALPHA)]
+               for s in range(n_stripes)]
+    n1, el1 = O.bench_clay_repair(K, M, erased, B, stripes, 1, seconds / 2)
     nn, eln = O.bench_clay_repair(K, M, erased, B, stripes, threads, seconds)
     one = n1 * ALGO_BYTES / el1 / 2**30
+    ws = n_stripes * ALGO_BYTES
     return {
         "value": round(nn * ALGO_BYTES / eln / 2**30, 3),
         "unit": "GiB/s",
@@ -132,24 +197,52 @@ def cpu_baseline(seconds: float, erased: int, sample=None):
         "kind": "port",
         "single_thread_value": round(one, 3),
         "oracle_check": oracle_check,
+        "working_set_bytes": ws,
+        "host": info,
         "sample": f"Clay(4,2) single repairs (e={erased}, B=32 KiB), stage-by-stage C restatement of the "
-                  f"reference JVM path (oracle/): {nn} repairs on {threads} threads x {per_thread} host-resident "
-                  f"valid stripes each in {eln:.1f} s; single thread {n1} repairs in {el1:.1f} s; {_cpu_model()}",
+                  f"reference JVM path (oracle/): {nn} repairs on {threads} threads (lease quota "
+                  f"{info['cgroup_quota_cpus']}, affinity {info['affinity_cpus']} of {info['cpus_present']} CPUs) "
+                  f"x {per_thread} host-resident valid stripes each, {ws / 2**20:.0f} MiB touched "
+                  f"(>= 2x the {l3 / 2**20:.0f} MiB L3), in {eln:.1f} s; single thread {n1} repairs over "
+                  f"all {n_stripes} stripes in {el1:.1f} s; {info['model']}",
     }
 
 
-def pmc_traffic(pool: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (if it matches)."""
+# Sources that define what the device executes for a given map: the kernels, their
+# launch selection and the plan format / compiler.  Their hash is stored with every PMC
+# profile (profiles/pmc_traffic.json); a profile taken on other kernel code is stale.
+KERNEL_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
+                  "apply_skew.hip", "engine.hpp", "engine.cpp"]
+
+
+def kernel_source_hash() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        h.update(name.encode() + b"\0" + (ROOT / "repair-pipelining_amd" / "csrc" / name).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(workload: str, pool: int, kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (scripts/pmc.sh + scripts/pmc_summary.py), used only if it was taken on this
+    workload, pool size and kernel instance AND on the current kernel sources.
+    Returns (bytes or None, why-not)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
-        return None
+        return None, "no PMC profile"
     try:
         d = json.loads(f.read_text())
-        if d.get("pool_stripes") == pool and d.get("kernel") == KERNEL:
-            return d["hbm_bytes_per_launch"]
-    except Exception:
-        return None
-    return None
+        w = d.get("workloads", {}).get(workload)
+        if w is None:
+            return None, "no PMC profile for this workload"
+        if d.get("kernel_source_hash") != kernel_source_hash():
+            return None, "stale: PMC profile taken on other kernel sources"
+        if w.get("pool_stripes") != pool or w.get("kernel") != kernel:
+            return None, "stale: PMC profile taken on another pool size or kernel instance"
+        return w["hbm_bytes_per_launch"], None
+    except Exception as e:  # noqa: BLE001 - a malformed profile is reported, not fatal
+        return None, "unreadable PMC profile: %s" % e
 
 
 def memory_probes(ecx, torch, region, reads: int, writes: int, reps: int = 5):
@@ -186,7 +279,6 @@ class Workload:
     unit_bytes = ALGO_BYTES           # algorithmic bytes per stripe
     write_bytes = WRITE_BYTES         # of which written
     reads, writes = 20, 8             # equal-sized streams read / written per unit (mix model)
-    kernel = KERNEL
     description = ""
 
     def launch(self):
@@ -224,7 +316,6 @@ class Clay104(Workload):
     """Config 4: shortened Clay(10,4) (Clay(12,4) with 2 virtual zero data nodes),
     1 MiB node blocks = 256 planes x 4 KiB sub-chunks, single-node repair."""
     k, m, v, b, alpha = 10, 4, 2, 4096, 256
-    kernel = "k_gf_apply<false,false,1,8,true,256,8>"
 
     def __init__(self, ecx, torch, dev, P, erased, seed):
         k, m, v, b, a = self.k, self.m, self.v, self.b, self.alpha
@@ -263,7 +354,6 @@ class RS124(Workload):
     reads, writes = 12, 2
     unit_bytes = 14 * (4 << 20)
     write_bytes = 2 * (4 << 20)
-    kernel = "k_gf_apply<false,true,1,8,false,256,8>"
 
     def __init__(self, ecx, torch, dev, P, pad, seed):
         self.P, self.torch, self.pitch = P, torch, self.L + pad
@@ -294,7 +384,6 @@ class LRC(Workload):
     reads, writes = 3, 1
     unit_bytes = 4 * 65536
     write_bytes = 65536
-    kernel = "k_gf_apply<false,true,1,4,false,256,8>"
 
     def __init__(self, ecx, torch, dev, P, seed):
         import numpy as np
@@ -322,21 +411,47 @@ class LRC(Workload):
         return bool(self.torch.equal(self.out[:, 0], self.pool[:, 2]))
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N fresh rank processes through
+    torch.distributed.run as a CHILD process (this process never touches the GPU and
+    never execs), with the same arguments.  Rank 0's JSON line reaches stdout through
+    the inherited stream; the exit status is the launcher's, non-zero if any rank failed."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:  # a free rendezvous port on the loopback interface
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d: launch one rank per GPU" % (args.gpus, world))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
     import torch
     import torch.distributed as dist
 
     import rpamd
     ecx = rpamd.load()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # ECX_BENCH_BACKEND=gloo rehearses the multi-process path on a box with fewer
-    # GPUs than ranks (ranks share devices round-robin); the default is RCCL.
+    # GPUs than ranks (ranks share devices round-robin); the default is RCCL, which
+    # needs one GPU per rank.
     backend = os.environ.get("ECX_BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > max(1, ndev):
+        raise SystemExit("bench.py: %d ranks but %d visible GPUs (RCCL needs one GPU per rank; "
+                         "ECX_BENCH_BACKEND=gloo shares devices for a rehearsal)" % (world, ndev))
+    local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -364,6 +479,7 @@ def main():
 
     wl.launch()
     torch.cuda.synchronize()
+    kernel = ecx.last_kernel()  # the instance launch_apply actually chose for this map and layout
     verified = None
     if not args.no_verify:
         verified = wl.verify()
@@ -403,7 +519,7 @@ def main():
     achieved = per_launch_bytes / (launch_ms * 1e-3) / 1e9
     total_stripes = stripes_per_step * args.steps * world
     value = total_stripes * wl.unit_bytes / el / 2**30
-    traffic = pmc_traffic(P) if args.workload == "clay42" else None
+    traffic, traffic_note = pmc_traffic(args.workload, P, kernel)
 
     sample = None
     if args.workload == "clay42" and rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -414,6 +530,11 @@ def main():
     if sample is not None:
         cpu = cpu_baseline(args.cpu_seconds, args.erased, sample)
 
+    if rank == 0 and args.meta:
+        Path(args.meta).write_text(json.dumps({
+            "workload": args.workload, "kernel": kernel, "pool_stripes": P, "unit_bytes": wl.unit_bytes,
+            "write_bytes_per_unit": wl.write_bytes, "algorithmic_bytes_per_launch": per_launch_bytes,
+            "kernel_source_hash": kernel_source_hash(), "avg_launch_ms": launch_ms}) + "\n")
     if rank == 0:
         line = {
             "metric": WORKLOADS[args.workload][0],
@@ -441,7 +562,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": wl.kernel,
+                "traffic_note": traffic_note,
+                "kernel": kernel,
+                "kernel_source_hash": kernel_source_hash(),
                 "avg_launch_ms": round(launch_ms, 4),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "measured_ceilings": probes,

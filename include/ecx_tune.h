@@ -65,6 +65,11 @@ int ecx_map_selftest(const struct ecx_map *map, uint64_t seed);
 /* Plan shape: row tiles, tile entries (= input loads of the one-workgroup-per-tile
  * kernel), tile groups, and the summed group unions (= input loads of the LDS kernel). */
 int ecx_map_plan_stats(const struct ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total);
+/* The kernel instance of the last full-chunk launch this thread enqueued, named as
+ * rocprofv3 names it (e.g. "k_gf_apply<false, true, 1, 20, false, 256, 8>"), copied
+ * NUL-terminated into buf.  Returns its length (0 = no launch yet), or
+ * ECX_E_ILLEGAL_ARGUMENT if buf is null or shorter than length + 1. */
+int ecx_last_kernel(char *buf, int len);
 #ifdef __cplusplus
 }
 #endif

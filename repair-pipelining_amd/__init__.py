@@ -211,6 +211,15 @@ def tune(key: str, value: int) -> None:
     check(f(key.encode(), int(value)))
 
 
+def last_kernel() -> str:
+    """The kernel instance of this thread's last full-chunk launch, as rocprofv3 names it
+    (ecx_last_kernel, include/ecx_tune.h); "" before the first launch."""
+    f = lib().ecx_last_kernel
+    f.argtypes, f.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+    buf = ctypes.create_string_buffer(256)
+    return buf.value.decode() if check(f(buf, len(buf))) > 0 else ""
+
+
 def probe_bandwidth(kind: int, src, dst, nbytes: int, nontemporal: bool = True, stream=None) -> None:
     """Pure-bandwidth probe kernels (include/ecx_tune.h): kind 0 = read-only stream of
     `src`, kind 1 = copy src -> dst; nbytes a multiple of 16 KiB.  Diagnostics only."""

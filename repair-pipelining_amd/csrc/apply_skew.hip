@@ -93,6 +93,7 @@ void launch_skew(int k, int rows, int depth, bool ntl, dim3 grid, hipStream_t st
     const dim3 blk(kBlockThreads);
 #define ECX_SKEW(NTL, D, R, KK)                                                                 \
     if (ntl == NTL && depth == D && rows == R && k == KK) {                                     \
+        note_kernel("k_gf_apply_skew", NTL, D, R, KK);                                          \
         hipLaunchKernelGGL((k_gf_apply_skew<NTL, D, R, KK>), grid, blk, 0, stream, a);          \
         return;                                                                                 \
     }

@@ -907,6 +907,13 @@ int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_
     });
 }
 
+int ecx_last_kernel(char *buf, int len) {
+    const std::string &k = last_kernel();
+    if (!buf || len < (int)k.size() + 1) return ECX_E_ILLEGAL_ARGUMENT;
+    std::memcpy(buf, k.c_str(), k.size() + 1);
+    return (int)k.size();
+}
+
 int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
     return guarded([&]() -> int {
         const CompiledMap &cm = map->cm;

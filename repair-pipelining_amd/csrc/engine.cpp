@@ -11,6 +11,10 @@ Tuning &tuning() {
     return t;
 }
 
+static thread_local std::string g_last_kernel;
+void set_last_kernel(std::string name) { g_last_kernel = std::move(name); }
+const std::string &last_kernel() { return g_last_kernel; }
+
 void check_hip(hipError_t e, const char *what) {
     if (e != hipSuccess) throw Error(ECX_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }

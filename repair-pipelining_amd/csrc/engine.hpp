@@ -22,6 +22,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "codes.hpp"
@@ -208,6 +209,23 @@ struct Tuning {
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();
+
+// The kernel instance of the last full-chunk (non-byte-safe) launch enqueued on this
+// thread, as rocprofv3 names it ("k_gf_apply<false, true, 1, 20, false, 256, 8>").
+// Diagnostics: bench.py's roofline.kernel and its PMC-profile match (ecx_last_kernel).
+void set_last_kernel(std::string name);
+const std::string &last_kernel();
+inline std::string kernel_param(bool v) { return v ? "true" : "false"; }
+inline std::string kernel_param(int v) { return std::to_string(v); }
+template <typename... P>
+void note_kernel(const char *name, P... params) {
+    std::string s = name;
+    s += '<';
+    const char *sep = "";
+    ((s += sep, s += kernel_param(params), sep = ", "), ...);
+    s += '>';
+    set_last_kernel(std::move(s));
+}
 
 // Enqueue out = M * in over nstripes stripes (kernels.hip).
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,

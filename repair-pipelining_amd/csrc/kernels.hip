@@ -328,6 +328,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             const dim3 grid((unsigned)(ns * per_stripe));
             if (waves) {
                 const dim3 blk(64 * cm.group_size());
+                if (!safe) note_kernel(tu.wave_groups == 2 ? "k_gf_apply_grp" : "k_gf_apply_lds", false, depth == 8 ? 8 : 4);
                 if (tu.wave_groups == 2) {  // direct loads, no LDS staging
                     if (safe) hipLaunchKernelGGL((k_gf_apply_grp<true, 4>), grid, blk, 0, stream, a);
                     else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_grp<false, 8>), grid, blk, 0, stream, a);
@@ -342,6 +343,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             if (wide) {
                 const dim3 blk(kBlockThreads);
                 const bool ntl = ntmode == 2 || (ntmode == 1 && a.n_wide == 1);  // one pair: no re-reads
+                if (!safe) note_kernel("k_gf_apply_wide", false, ntl, 1, depth);
                 if (safe) hipLaunchKernelGGL((k_gf_apply_wide<true, false, 0, 4>), grid, blk, 0, stream, a);
                 else if (depth == 8) {
                     if (ntl) hipLaunchKernelGGL((k_gf_apply_wide<false, true, 1, 8>), grid, blk, 0, stream, a);

@@ -1,17 +1,33 @@
 #!/bin/bash
-# HBM traffic of the headline kernel from rocprofv3 PMC counters, one counter
-# per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950).
+# HBM traffic and shader counters of the bench's dominant kernel, per --workload
+# (default: all four), from rocprofv3 PMC passes: FETCH_SIZE and WRITE_SIZE in passes
+# of their own (they do not fit one TCC pass on gfx950), then one SQ pass (VALU
+# instructions, wave/busy/wait cycles, GRBM clock).  Every pass runs the bench for one
+# step over its resident pool and writes its launch metadata (--meta: kernel instance,
+# pool, algorithmic bytes, kernel-source hash) next to the counters;
+# scripts/pmc_summary.py turns them into profiles/pmc_traffic.json.
+# A pass that fails stops the script (no retries).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o run \
-      -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 --stripes-per-step 32768 --no-verify --no-probes \
-      > "$OUT/pmc_$C.log" 2>&1
-  rc=$?; echo "pmc $C rc=$rc"; [ $rc -ne 0 ] && exit $rc
+WORKLOADS="${*:-clay42 clay104 rs124 lrc}"
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+for W in $WORKLOADS; do
+  case $W in
+    clay42) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; lrc) POOL=32768 ;;
+    *) echo "unknown workload $W"; exit 2 ;;
+  esac
+  i=0
+  for C in FETCH_SIZE WRITE_SIZE "$SQ"; do
+    D="$OUT/pmc_${W}_$i"; mkdir -p "$D"
+    timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
+        -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 \
+           --stripes-per-step "$POOL" --no-probes --meta "$D/meta.json" > "$D.log" 2>&1
+    rc=$?; echo "pmc $W pass$i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D.log"; exit $rc; }
+    i=$((i + 1))
+  done
 done
-find "$OUT" -path '*pmc_*' -name '*.csv' | head
 exit 0

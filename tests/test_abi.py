@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(ecx):
     assert headers == ["ecx.h", "ecx_tune.h"]
     missing = [s for h in headers for s in declared_symbols(h) if not hasattr(lib, s)]
     assert not missing, missing
-    assert len(declared_symbols("ecx_tune.h")) == 4
+    assert len(declared_symbols("ecx_tune.h")) == 5
 
 
 def test_binding_table_matches_header(ecx):
@@ -144,3 +144,13 @@ def test_tuning_keys(ecx):
         assert tune(key.encode(), bad) == -1, key
     for key, val in defaults.items():  # restore
         tune(key.encode(), val)
+
+
+def test_last_kernel_label_before_any_launch(ecx):
+    """ecx_last_kernel (include/ecx_tune.h): empty before any launch on this thread,
+    and a too-short buffer is refused rather than truncated."""
+    import ctypes as C
+    f = ecx.lib().ecx_last_kernel
+    f.argtypes, f.restype = [C.c_char_p, C.c_int], C.c_int
+    assert f(C.create_string_buffer(8), 8) == 0
+    assert f(None, 0) == -1

@@ -1039,3 +1039,35 @@ def test_batch_empty_calls_are_noops(ecx, torch_dev):
     rs.encodeParityBatch(pool, 48 * B, B, 2, 0, 0)
     torch.cuda.synchronize()
     assert (out == 9).all() and (pool == 7).all()
+
+
+@pytest.mark.parametrize("stride", [(1 << 31) - 8192, (1 << 31) + 4096])
+def test_multitile_slot_offset_near_2gib(ecx, torch_dev, stride):
+    """launch_apply's offsets32 gate (kernels.hip): the buffer-descriptor kernels
+    (multi-tile maps with LDS tables, wide tiles) address an input slot by a 32-bit
+    scalar offset, valid only while max_in_slot * in_slot_stride + 4 KiB < 2^31.  A
+    16 x 2 map (two 8-row tiles sharing both inputs) with slot 1 just under and just
+    over 2 GiB from slot 0 -- the descriptor path, and the 64-bit fallback -- equals
+    the oracle's table product, with wide tiles on and off."""
+    from conftest import gf_apply_numpy
+    torch = torch_dev
+    rng = np.random.default_rng(stride & 0xFFFF)
+    m = rng.integers(1, 256, (16, 2)).astype(np.uint8)
+    L = 8192
+    gm = ecx.GfMap.from_matrix(m, in_slot=[0, 1], out_slot=list(range(16)))
+    buf = torch.empty(stride + L, dtype=torch.uint8, device="cuda")
+    ecx.fill_random(buf[:L], L, 7)
+    ecx.fill_random(buf[stride:], L, 8)
+    x0, x1 = buf[:L].cpu().numpy(), buf[stride:].cpu().numpy()
+    ref = gf_apply_numpy(m, [x0, x1])
+    try:
+        for wide in (0, 2):
+            ecx.tune("wide_tiles", wide)
+            out = torch.full((16, L), 0x5A, dtype=torch.uint8, device="cuda")
+            gm.apply_batch(buf, stride + L, stride, out, 16 * L, L, 1, L)
+            torch.cuda.synchronize()
+            assert (out.cpu().numpy() == ref).all(), (stride, wide, ecx.last_kernel())
+    finally:
+        ecx.tune("wide_tiles", 1)
+    del buf
+    torch.cuda.empty_cache()

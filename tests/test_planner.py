@@ -98,6 +98,43 @@ def test_clay42_map_shape(ecx):
     assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (16, 32, 144)
 
 
+A3_E1_COEFFS = {143, 104, 208, 52, 187, 210, 107, 92, 105, 184, 109, 189, 185, 214}
+
+
+def _probe_oracle_repair_map(k, m, e, ins):
+    """The oracle's single-repair map, read off by unit vectors: byte position j of
+    input slot ins[j] is 1, every other helper byte 0 (GF linearity per byte
+    position), so output byte j of row o is the coefficient M[o][j]."""
+    n, nin = k + m, len(ins)
+    c = O.Clay(k, m, [e])
+    inputs = [None if (i % n) == e else np.zeros(nin, np.uint8) for i in range(n * c.alpha)]
+    for j, slot in enumerate(ins):
+        inputs[slot][j] = 1
+    outs = [np.zeros(nin, np.uint8) for _ in range(c.alpha)]
+    c.perform_coding(inputs, outs, nin)
+    return np.stack(outs)
+
+
+def test_clay42_repair_map_pinned_to_survey_a3(ecx):
+    """SURVEY.md A.3, the survey's independent scratch restatement of
+    ClayCodeErasureDecodingStep.java:435-492,630-666 (the non-codeword repair map, H2):
+    the e=1 Clay(4,2) single repair has exactly the 14 distinct coefficients
+    {143,104,208,52,187,210,107,92,105,184,109,189,185,214}, and every e has 52
+    non-zeros with 6-7 per row.  Asserted on the planner's composed map
+    (ecx_clay_map) and on the oracle probed with unit vectors; the two must also be
+    the same matrix."""
+    for e in range(6):
+        mat, ins, outs = ecx.ClayCodeErasureDecodingStep([e], 4, 2).map().matrix()
+        probed = _probe_oracle_repair_map(4, 2, e, ins.tolist())
+        assert (probed == mat).all(), e
+        for mm in (mat, probed):
+            nnz = (mm != 0).sum(1)
+            assert mm.shape == (8, 20) and int(nnz.sum()) == 52 and set(nnz.tolist()) <= {6, 7}, e
+        if e == 1:
+            assert set(mat[mat != 0].tolist()) == A3_E1_COEFFS
+            assert set(probed[probed != 0].tolist()) == A3_E1_COEFFS
+
+
 def test_clay124_map_shape(ecx):
     inf = ecx.ClayCodeErasureDecodingStep([5], 12, 4).map().info()
     assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (256, 960, 5568)
