@@ -1,30 +1,46 @@
 #!/bin/bash
-# One GPU session on the MI355X box: smoke, GPU parity tests, bench, rocprofv3.
+# One GPU session on the MI355X box.  Modes (any of, in order): test bench gloo2 pmc prof
 # Every GPU step has its own time limit; a fault/abort/timeout stops the script.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 cd "$ROOT"
-MODE="${1:-all}"
+MODES="${*:-test bench}"
+has() { [[ " $MODES " == *" $1 "* ]]; }
+stop() { echo "step '$1' exited with $2: stopping"; exit "$2"; }
 
-fatal() { case "$1" in 0|1) return 1;; *) echo "step exited with $1: stopping" ; return 0;; esac; }
-
-if [[ "$MODE" == all || "$MODE" == test ]]; then
+if has test; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
-  rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; fatal $rc && exit $rc
-  timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
-  rc=$?; echo "pytest gpu rc=$rc"; tail -15 "$OUT/pytest_gpu.log"; fatal $rc && exit $rc
+  rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke.log"; [ $rc -ne 0 ] && stop smoke $rc
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread \
+      > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?; echo "pytest gpu rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && stop pytest $rc
 fi
-if [[ "$MODE" == all || "$MODE" == bench ]]; then
-  timeout -k 10 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 > "$OUT/bench.log" 2>&1
-  rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; fatal $rc && exit $rc
+if has bench; then
+  timeout -k 10 600 python bench.py --steps 5 --warmup 2 > "$OUT/bench.log" 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; [ $rc -ne 0 ] && stop bench $rc
 fi
-if [[ "$MODE" == all || "$MODE" == prof ]]; then
+if has gloo2; then
+  # the multi-rank path without an external launcher, 2 ranks sharing the one GPU
+  ECX_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --pool 4096 --steps 2 --warmup 1 \
+      --cpu-seconds 0 --no-probes > "$OUT/bench_gloo2.log" 2>&1
+  rc=$?; echo "bench gloo2 rc=$rc"; tail -2 "$OUT/bench_gloo2.log"; [ $rc -ne 0 ] && stop gloo2 $rc
+fi
+if has workloads; then
+  for W in clay104 rs124 lrc; do
+    timeout -k 10 300 python bench.py --workload $W --steps 3 --warmup 1 > "$OUT/bench_$W.log" 2>&1
+    rc=$?; echo "bench $W rc=$rc"; tail -1 "$OUT/bench_$W.log"; [ $rc -ne 0 ] && stop "bench $W" $rc
+  done
+fi
+if has pmc; then
+  bash "$ROOT/scripts/pmc.sh" || stop pmc $?
+fi
+if has prof; then
   export TMPDIR=/tmp
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
       -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0) > "$OUT/prof.log" 2>&1
-  rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; fatal $rc && exit $rc
-  find "$OUT/prof" -name '*stats*' | head
+  rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/prof.log"; [ $rc -ne 0 ] && stop prof $rc
+  find "$OUT/prof" -name '*stats*'
 fi
 exit 0
