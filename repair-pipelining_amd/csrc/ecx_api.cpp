@@ -881,6 +881,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_gather_max = (int64_t)value << 10;
     }
+    else if (k == "bitslice") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.bitslice = value;
+    }
     else if (k == "host_buffers") {
         if (value < 1 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_buffers = value;
@@ -961,6 +965,31 @@ int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
                 cm.emulate_padded(hp, in.data(), got.data(), len, tlds, depth);
                 check(got, tlds ? "padded plan (LDS tables) differs from the map" : "padded plan differs from the map");
             }
+        }
+        // The bit-sliced kernel's arithmetic (bits.hpp, shared with apply_bits.hip) over
+        // its padded entries at both of its ring depths, on one whole 4 KiB chunk.
+        const int64_t blen = kChunkBytes;
+        std::vector<uint8_t> bin((size_t)std::max(1, nin) * blen), bref((size_t)std::max(1, nout) * blen, 0);
+        for (uint8_t &b : bin) {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            b = (uint8_t)x;
+        }
+        for (int o = 0; o < m.n_out; ++o)
+            for (int j = 0; j < m.n_in; ++j) {
+                const uint8_t c = m.at(o, j);
+                if (!c) continue;
+                for (int64_t i = 0; i < blen; ++i)
+                    bref[(size_t)m.out_slot[o] * blen + i] ^= f.mul(c, bin[(size_t)m.in_slot[j] * blen + i]);
+            }
+        for (int depth : {2, 4}) {
+            std::vector<uint8_t> got(bref.size(), 0);
+            cm.emulate_bits(cm.padded_plan(depth), bin.data(), got.data(), blen);
+            for (int o = 0; o < m.n_out; ++o)
+                if (!std::equal(got.begin() + (size_t)m.out_slot[o] * blen, got.begin() + (size_t)(m.out_slot[o] + 1) * blen,
+                                bref.begin() + (size_t)m.out_slot[o] * blen))
+                    throw Error(ECX_E_ILLEGAL_ARGUMENT, "bit-sliced plan differs from the map");
         }
         return ECX_OK;
     });

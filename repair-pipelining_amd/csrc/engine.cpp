@@ -1,5 +1,6 @@
 // engine.cpp -- plan compilation, device contexts, host-pointer execution.
 #include "engine.hpp"
+#include "bits.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -397,6 +398,7 @@ CompiledMap::~CompiledMap() {
         (void)hipFree(kv.second.atab);
         (void)hipFree(kv.second.wentries);
         (void)hipFree(kv.second.wtiles);
+        (void)hipFree(kv.second.bentries);
         (void)hipSetDevice(cur);
     }
 }
@@ -427,6 +429,20 @@ HostPlan CompiledMap::padded_plan(int depth) const {
             p.atab.push_back(p.entries[e * kEntryDwords + 4 + 5 * r]);      // T0a
             p.atab.push_back(p.entries[e * kEntryDwords + 4 + 5 * r + 2]);  // T1a
         }
+    // Bit-sliced entries: the coefficient of each row, recovered from its table
+    // (T0a byte 1 = c * 1), or 1 for a plain-XOR row.
+    for (size_t e = 0; e < p.entries.size() / kEntryDwords; ++e) {
+        const uint32_t *rec = p.entries.data() + e * kEntryDwords;
+        uint32_t coef[2] = {0u, 0u};
+        for (int r = 0; r < kTileRows; ++r) {
+            const uint32_t c = (rec[2] >> r) & 1u ? 1u : ((rec[1] >> r) & 1u ? (rec[4 + 5 * r] >> 8) & 0xFFu : 0u);
+            coef[r >> 2] |= c << (8 * (r & 3));
+        }
+        p.bentries.push_back(rec[0]);
+        p.bentries.push_back(rec[1] | rec[2]);
+        p.bentries.push_back(coef[0]);
+        p.bentries.push_back(coef[1]);
+    }
     // Unions: each group's list padded with zero-page entries to a multiple of
     // group_size * depth, i.e. whole stages of the LDS kernel's load ring.
     p.groups = groups_;
@@ -541,6 +557,38 @@ void CompiledMap::emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *
     }
 }
 
+void CompiledMap::emulate_bits(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const {
+    if (len % kChunkBytes) throw Error(ECX_E_ILLEGAL_ARGUMENT, "bit-sliced emulation needs whole 4 KiB chunks");
+    const bits::Masks mk{0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+    auto get = [](const uint8_t *b) { return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24; };
+    for (int t = 0; t < n_tiles_; ++t) {
+        const uint32_t *tile = p.tiles.data() + (size_t)t * kTileDwords;
+        for (int64_t c = 0; c < len; c += kChunkBytes)
+            for (int lane = 0; lane < kBitsThreads; ++lane) {
+                // the lane's 32 bytes: [16 l, 16 l + 16) and [2048 + 16 l, ...) of the chunk
+                const int64_t off[2] = {c + 16 * lane, c + kChunkBytes / 2 + 16 * lane};
+                uint32_t acc[8][8] = {};
+                for (uint32_t e = 0; e < tile[1]; ++e) {
+                    const uint32_t *r = p.bentries.data() + ((size_t)tile[0] + e) * kBitsEntryDwords;
+                    if (!r[1]) continue;
+                    if (r[0] == kDummySlot) throw Error(ECX_E_ILLEGAL_ARGUMENT, "padding entry with coefficients");
+                    uint32_t x[8];
+                    for (int h = 0; h < 2; ++h)
+                        for (int d = 0; d < 4; ++d) x[4 * h + d] = get(in + (int64_t)r[0] * len + off[h] + 4 * d);
+                    bits::transpose8(x, mk);
+                    bits::apply_entry_bits(acc, x, r[1], r[2], r[3]);
+                }
+                for (int o = 0; o < (int)tile[2]; ++o) {
+                    bits::untranspose8(acc[o], mk);
+                    for (int h = 0; h < 2; ++h)
+                        for (int d = 0; d < 4; ++d)
+                            for (int b = 0; b < 4; ++b)
+                                out[(int64_t)tile[4 + o] * len + off[h] + 4 * d + b] = (uint8_t)(acc[o][4 * h + d] >> (8 * b));
+                }
+            }
+    }
+}
+
 const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     int dev = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
@@ -561,6 +609,7 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     upload(&p.atab, h.atab, "hipMalloc(plan atab)");
     upload(&p.wentries, h.wentries, "hipMalloc(plan wide entries)");
     upload(&p.wtiles, h.wtiles, "hipMalloc(plan wide tiles)");
+    upload(&p.bentries, h.bentries, "hipMalloc(plan bit-sliced entries)");
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;
 }
 

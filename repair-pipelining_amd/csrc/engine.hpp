@@ -53,6 +53,7 @@ struct DevicePlan {
     uint32_t *atab = nullptr;
     uint32_t *wentries = nullptr;  // wide tiles (k_gf_apply_wide)
     uint32_t *wtiles = nullptr;
+    uint32_t *bentries = nullptr;  // bit-sliced kernel (k_gf_bits): kBitsEntryDwords per padded entry
     int max_tile_entries = 0;  // padded
 };
 constexpr int kAtabDwords = 2 * kTileRows;
@@ -64,12 +65,18 @@ constexpr int kAtabDwords = 2 * kTileRows;
 constexpr int kWideEntryDwords = 2 * kEntryDwords;
 constexpr int kWideTileDwords = 32;
 constexpr int kMaxLdsTileEntries = 512;  // 32 KiB of LDS per workgroup at most
+// Bit-sliced kernel (k_gf_bits, apply_bits.hip): per padded entry [0] input slot
+// [1] rows with a non-zero coefficient (bitmask) [2] coefficients of rows 0-3 (one
+// byte each) [3] coefficients of rows 4-7.  Parallel to the padded `entries` array,
+// so the padded `tiles` index both.
+constexpr int kBitsEntryDwords = 4;
+constexpr int kBitsThreads = 128;  // 128 lanes x 32 bytes = one 4 KiB chunk (kChunkBytes)
 
 // The padded plan exactly as uploaded to a device for one load-ring depth
 // (CompiledMap::padded_plan): entries/tiles padded to multiples of `depth`,
 // group unions padded to whole LDS stages, and the TLDS low-table array.
 struct HostPlan {
-    std::vector<uint32_t> entries, tiles, groups, unions, atab, wentries, wtiles;
+    std::vector<uint32_t> entries, tiles, groups, unions, atab, wentries, wtiles, bentries;
     int max_tile_entries = 0;
 };
 
@@ -123,6 +130,10 @@ public:
     void emulate_padded(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len, bool tlds, int depth) const;
     // The same for the padded wide-tile arrays (k_gf_apply_wide).
     void emulate_wide(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const;
+    // k_gf_bits on the host: the bit-sliced arithmetic of apply_bits.hip (the same
+    // __host__ __device__ transpose / xtime / nibble code) over the padded
+    // `bentries`, for `len` a multiple of kChunkBytes (the kernel's chunk).
+    void emulate_bits(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const;
     CompiledMap &compact();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
@@ -151,6 +162,7 @@ struct ApplyArgs {
     const uint32_t *atab;
     const uint32_t *wentries;
     const uint32_t *wtiles;
+    const uint32_t *bentries;
     const uint8_t *zero_page;
     int64_t in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride;
     int64_t nbytes, chunk_begin, n_chunks, stripe_begin;
@@ -202,6 +214,9 @@ struct Tuning {
     int skew_chunks = 1;
     // Per-call CodingLoop entry points: compiled plans kept, by map content (0 = none).
     int plan_cache = 256;
+    // 1 = the bit-sliced kernel (k_gf_bits) for maps it is measured faster on (auto),
+    // 2 = for every map it can run (aligned layout, 32-bit slot offsets), 0 = never.
+    int bitslice = 1;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -266,7 +266,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // 16-row workgroup is 2x slower -- profiles/r01_wide.jsonl), forced (2), off (0).
     const bool offsets32 = in_slot_stride >= 0 &&
                            (int64_t)cm.max_in_slot() * in_slot_stride + kChunkBytes <= 0x7FFFFFFF;
-    const bool wide = (tu.wide_tiles == 2 || (tu.wide_tiles == 1 && cm.wide_sharing() >= 1.2)) && !waves &&
+    bool wide = (tu.wide_tiles == 2 || (tu.wide_tiles == 1 && cm.wide_sharing() >= 1.2)) && !waves &&
                       cm.n_wide_tiles() > 0 && threads == kBlockThreads && rows == kTileRows && offsets32;
     if (wide) depth = tu.depth == 8 || tu.depth == 4 ? tu.depth : cm.wide_depth();
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
@@ -284,6 +284,18 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
           nbytes >= skew * kChunkBytes))
         skew = 0;
     if (skew) depth = depth == 4 || skew_rows == kTileRows ? 4 : 8;
+    // Bit-sliced kernel (k_gf_bits, apply_bits.hip) for the full 4 KiB chunks: forced (2)
+    // wherever it can run, or auto (1) for multi-tile maps that do not pair into wide
+    // tiles -- the maps with many coefficients per input, where the split-table
+    // kernel is bound by vector issue (Clay(10,4)).  Its ring is 4
+    // deep (2 on request); the byte-safe tail then runs on the same padded plan.
+    const bool bits_ok = aligned && offsets32 && !waves && ntmode != 0 && nbytes >= kChunkBytes;
+    const bool bits = bits_ok && !skew &&
+                      (tu.bitslice == 2 || (tu.bitslice == 1 && cm.n_tiles() > 1 && !wide));
+    if (bits) {
+        depth = tu.depth == 2 ? 2 : 4;
+        wide = false;  // the byte-safe tail runs k_gf_apply over the same padded tiles
+    }
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
     // one workgroup per (stripe, chunk, tile) with 4 KiB (256 threads) or 1 KiB (64) chunks.
@@ -301,6 +313,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.atab = plan.atab;
     a.wentries = plan.wentries;
     a.wtiles = plan.wtiles;
+    a.bentries = plan.bentries;
     a.n_wide = cm.n_wide_tiles();
     a.lane_zero = 0;
     a.chunk_major = tu.chunk_major;
@@ -338,6 +351,10 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                 if (safe) hipLaunchKernelGGL((k_gf_apply_lds<true, 4>), grid, blk, 0, stream, a);
                 else if (depth == 8) hipLaunchKernelGGL((k_gf_apply_lds<false, 8>), grid, blk, 0, stream, a);
                 else hipLaunchKernelGGL((k_gf_apply_lds<false, 4>), grid, blk, 0, stream, a);
+                continue;
+            }
+            if (bits && !safe) {
+                launch_bits(ntmode == 2, depth, grid, stream, a);
                 continue;
             }
             if (wide) {

@@ -811,7 +811,10 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
                                   (8, 2, 64, 0, 0), (4, 0, 64, 0, 0), (2, 0, 256, 0, 0), (2, 2, 256, 0, 0),
                                   (4, 0, 256, 2, 0), (8, 0, 256, 2, 0), (8, 0, 256, 0, 2), (4, 0, 256, 0, 4),
                                   (10, 0, 256, 0, 0), (12, 0, 256, 0, 0), (16, 0, 256, 0, 0), (20, 0, 256, 0, 0),
-                                  (24, 0, 256, 0, 0), (20, 2, 256, 0, 0)):
+                                  (24, 0, 256, 0, 0), (20, 2, 256, 0, 0), (4, 0, 256, 0, -2), (2, 0, 256, 0, -2)):
+        # sk < 0: the bit-sliced kernel forced (ecx_tune "bitslice" 2), at ring depth 4 / 2
+        ecx.tune("bitslice", 2 if sk < 0 else 0)
+        sk = max(sk, 0)
         ecx.tune("depth", depth)
         ecx.tune("lds_tables", lt)
         ecx.tune("block_threads", bt)
@@ -829,6 +832,7 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.tune("block_threads", 256)
     ecx.tune("wide_tiles", 1)
     ecx.tune("skew_chunks", 1)
+    ecx.tune("bitslice", 1)
 
 
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
