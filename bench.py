@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample; 0 = skip")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-probes", action="store_true", help="skip the in-run memory ceiling probes")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="launch-shape knob (include/ecx_tune.h), for A/B runs; repeatable")
     ap.add_argument("--meta", default=None, help="write the launch metadata (kernel, pool, bytes per launch, "
                                                  "kernel-source hash) as JSON here (scripts/pmc.sh)")
     args = ap.parse_args()
@@ -461,6 +463,9 @@ def main():
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     ecx.set_device(local)
+    for kv in args.tune:
+        key, _, val = kv.partition("=")
+        ecx.tune(key, int(val))
 
     P = args.pool
     passes = max(1, args.stripes_per_step // P)
