@@ -27,10 +27,12 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 #endif
 }
 
-// m ? a : b, bitwise: one v_bitop3_b32 (truth table 0xE4 over (a, b, m)).
+// m ? a : b, bitwise: one v_bfi_b32 (D = S0 & S1 | ~S0 & S2).
 __host__ __device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_bitop3_b32(a, b, m, 0xE4);
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
 #else
     return (a & m) | (b & ~m);
 #endif
@@ -60,7 +62,7 @@ __host__ __device__ __forceinline__ void xor2_into(uint32_t &acc, uint32_t a, ui
 // One delta-swap stage between dwords a and b at bit distance s over mask m: the
 // bits of a outside m and the bits of b inside m (shifted by s) trade places.  An
 // involution, so the inverse transpose runs the stages in reverse order.  With m in
-// a VGPR each select is one full-rate v_bitop3_b32 (a literal mask would become an
+// a VGPR each select is one full-rate v_bfi_b32 (a literal mask would become an
 // SGPR operand, which gfx950 issues at half rate).
 __host__ __device__ __forceinline__ void swap_stage(uint32_t &a, uint32_t &b, int s, uint32_t m) {
     const uint32_t na = sel(m, a, b << s);

@@ -289,7 +289,9 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // tiles -- the maps with many coefficients per input, where the split-table
     // kernel is bound by vector issue (Clay(10,4)).  Its ring is 4
     // deep (2 on request); the byte-safe tail then runs on the same padded plan.
-    const bool bits_ok = aligned && offsets32 && !waves && ntmode != 0 && nbytes >= kChunkBytes;
+    // (the chunk accounting below is in 4 KiB chunks only for 256-thread shapes)
+    const bool bits_ok = aligned && offsets32 && !waves && threads == kBlockThreads && ntmode != 0 &&
+                         nbytes >= kChunkBytes;
     const bool bits = bits_ok && !skew &&
                       (tu.bitslice == 2 || (tu.bitslice == 1 && cm.n_tiles() > 1 && !wide));
     if (bits) {
@@ -354,6 +356,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                 continue;
             }
             if (bits && !safe) {
+                if (chunk != kChunkBytes) throw Error(ECX_E_ILLEGAL_ARGUMENT, "k_gf_bits needs 4 KiB chunks");
                 launch_bits(ntmode == 2, depth, grid, stream, a);
                 continue;
             }

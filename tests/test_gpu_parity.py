@@ -1075,3 +1075,49 @@ def test_multitile_slot_offset_near_2gib(ecx, torch_dev, stride):
         ecx.tune("wide_tiles", 1)
     del buf
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case", ["clay104", "clay42", "rs124", "dense40x24", "ones"])
+@pytest.mark.parametrize("depth", [2, 4])
+def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
+    """k_gf_bits (apply_bits.hip, forced by ecx_tune "bitslice" 2) equals the oracle's
+    table-driven product of the map on every stripe: maps with 32 tiles (Clay(10,4)),
+    one tile (Clay(4,2), RS(12,4)), a dense random map and an all-ones map, over
+    whole 4 KiB chunks plus a byte-safe tail."""
+    from conftest import gf_apply_numpy
+    torch = torch_dev
+    rng = np.random.default_rng(77)
+    if case == "clay104":
+        m, ins, outs = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2).map().matrix()
+    elif case == "clay42":
+        m, ins, outs = ecx.ClayCodeErasureDecodingStep([1], 4, 2).map().matrix()
+    elif case == "rs124":
+        m, ins, outs = ecx.ReedSolomon.create(12, 4).decode_map([False, False] + [True] * 14).matrix()
+    elif case == "dense40x24":
+        m = rng.integers(0, 256, (40, 24)).astype(np.uint8)
+        ins, outs = np.arange(24), np.arange(40)
+    else:
+        m = np.ones((16, 20), np.uint8)
+        ins, outs = np.arange(20), np.arange(16)
+    gm = ecx.GfMap.from_matrix(m, in_slot=[int(i) for i in ins], out_slot=[int(o) for o in outs])
+    ni, no = int(max(ins)) + 1, int(max(outs)) + 1
+    S, L = 3, 4096 * 2 + 112  # 16-B aligned rows (the bit-sliced kernel's layout) with a tail
+    inp = torch.empty((S, ni, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(inp, inp.numel(), 5)
+    host = inp.cpu().numpy()
+    try:
+        ecx.tune("bitslice", 2)
+        ecx.tune("depth", depth)
+        out = torch.full((S, no, L), 0x5A, dtype=torch.uint8, device="cuda")
+        gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
+        torch.cuda.synchronize()
+        assert ecx.last_kernel() == "k_gf_bits<%s, %d>" % ("true" if len(m) <= 8 else "false", depth)
+    finally:
+        ecx.tune("bitslice", 1)
+        ecx.tune("depth", 0)
+    got = out.cpu().numpy()
+    for s in range(S):
+        ref = gf_apply_numpy(m, [host[s, j] for j in ins])
+        for o, slot in enumerate(outs):
+            bad = np.nonzero(got[s, slot] != ref[o])[0]
+            assert bad.size == 0, (case, s, o, bad[:8], got[s, slot][bad[:8]], ref[o][bad[:8]])
