@@ -41,7 +41,8 @@
  *   "bitslice"         the bit-sliced kernel (k_gf_bits: 32 bytes per lane as 8 bit planes, GF
  *                      multiplies as XORs of the planes of 2^k x) for the full 4 KiB chunks of
  *                      aligned layouts whose slot offsets fit 31 bits: 1 = for multi-tile maps
- *                      that do not run as wide tiles (default), 2 = for every such map, 0 = never
+ *                      that do not run as wide tiles, 2 = for every such map, 0 = never (default;
+ *                      measured slower, bound by its scalar branches)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -214,9 +214,11 @@ struct Tuning {
     int skew_chunks = 1;
     // Per-call CodingLoop entry points: compiled plans kept, by map content (0 = none).
     int plan_cache = 256;
-    // 1 = the bit-sliced kernel (k_gf_bits) for maps it is measured faster on (auto),
-    // 2 = for every map it can run (aligned layout, 32-bit slot offsets), 0 = never.
-    int bitslice = 1;
+    // Bit-sliced kernel (k_gf_bits): 2 = for every map it can run (aligned layout, 32-bit
+    // slot offsets, 4 KiB chunks), 1 = for multi-tile maps that do not pair into wide
+    // tiles, 0 = never (default: it measured 4-10 % slower on every BASELINE map, bound
+    // by its scalar branches -- profiles/r02_bits_ab.jsonl, r02_bits_sq_ab.json).
+    int bitslice = 0;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

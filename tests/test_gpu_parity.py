@@ -832,7 +832,7 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.tune("block_threads", 256)
     ecx.tune("wide_tiles", 1)
     ecx.tune("skew_chunks", 1)
-    ecx.tune("bitslice", 1)
+    ecx.tune("bitslice", 0)
 
 
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
@@ -1113,7 +1113,7 @@ def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
         torch.cuda.synchronize()
         assert ecx.last_kernel() == "k_gf_bits<%s, %d>" % ("true" if len(m) <= 8 else "false", depth)
     finally:
-        ecx.tune("bitslice", 1)
+        ecx.tune("bitslice", 0)
         ecx.tune("depth", 0)
     got = out.cpu().numpy()
     for s in range(S):
