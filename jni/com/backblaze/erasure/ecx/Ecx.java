@@ -1,0 +1,69 @@
+package com.backblaze.erasure.ecx;
+
+/**
+ * Status codes of libecx.so (include/ecx.h:40-50) mapped back onto the exceptions the
+ * reference throws for the same conditions, with the library's thread-local message.
+ */
+public final class Ecx {
+    public static final int OK = 0;
+    public static final int E_ILLEGAL_ARGUMENT = -1; // IllegalArgumentException (sizes, offsets, counts)
+    public static final int E_NOT_ENOUGH_SHARDS = -2; // "Not enough shards present", ReedSolomon.java:211-213
+    public static final int E_SINGULAR = -3;          // "Matrix is singular", Matrix.java:311-313
+    public static final int E_TOO_MANY_SHARDS = -4;   // "too many shards - max is 256", ReedSolomon.java:48-50
+    public static final int E_INDEX = -5;             // ArrayIndexOutOfBoundsException (Clay (k+m)%m != 0)
+    public static final int E_NULL = -6;              // NullPointerException (decodeMissingSingle, bug B3)
+    public static final int E_NOMEM = -7;             // host or device allocation failed
+    public static final int E_DEVICE = -10;           // no HIP device / HIP runtime error
+
+    private Ecx() {
+    }
+
+    /** Returns {@code status} if it is not an error, else throws the reference's exception. */
+    public static int check(int status) {
+        if (status >= 0) {
+            return status;
+        }
+        String detail = EcxNative.lastError();
+        String msg = EcxNative.statusString(status) + (detail == null || detail.isEmpty() ? "" : ": " + detail);
+        switch (status) {
+            case E_ILLEGAL_ARGUMENT:
+            case E_NOT_ENOUGH_SHARDS:
+            case E_SINGULAR:
+            case E_TOO_MANY_SHARDS:
+                throw new IllegalArgumentException(msg);
+            case E_INDEX:
+                throw new ArrayIndexOutOfBoundsException(msg);
+            case E_NULL:
+                throw new NullPointerException(msg);
+            case E_NOMEM:
+                throw new OutOfMemoryError(msg);
+            default:
+                throw new IllegalStateException(msg);
+        }
+    }
+
+    /** Flattens row-major coefficient rows (the CodingLoop matrixRows argument). */
+    public static byte[] flatten(byte[][] rows, int rowCount, int rowLength) {
+        byte[] flat = new byte[rowCount * rowLength];
+        for (int r = 0; r < rowCount; r++) {
+            System.arraycopy(rows[r], 0, flat, r * rowLength, rowLength);
+        }
+        return flat;
+    }
+
+    /** boolean[] shard-present flags as the byte flags the C ABI takes. */
+    public static byte[] flags(boolean[] present) {
+        byte[] f = new byte[present.length];
+        for (int i = 0; i < present.length; i++) {
+            f[i] = (byte) (present[i] ? 1 : 0);
+        }
+        return f;
+    }
+
+    /** Creates the codec handle of ReedSolomon.create(k, m) (ReedSolomon.java:34-61). */
+    public static long createReedSolomon(int dataShards, int parityShards) {
+        long[] h = new long[1];
+        check(EcxNative.rsCreate(dataShards, parityShards, h));
+        return h[0];
+    }
+}

@@ -1,0 +1,103 @@
+package distributed.erasure.coding.clay;
+
+import com.backblaze.erasure.ecx.Ecx;
+import com.backblaze.erasure.ecx.EcxNative;
+
+import java.nio.ByteBuffer;
+
+/**
+ * ClayCodeErasureDecodingStep (ClayCodeErasureDecodingStep.java:28-107) on libecx.so:
+ * the same constructor arguments (erased indexes, and the code's k and m instead of
+ * the two ReedSolomon objects, which the library builds identically), the same
+ * performCoding(ECChunk[], ECChunk[]) contract (inputs n*alpha plane-major, null =
+ * erased or absent; outputs |E|*alpha), and a batched form over many stripes for the
+ * coordinator (ClayCoordinator.kt:96-97) -- device-resident or in (direct) host memory.
+ * Results are those of the reference's decode/encode stage sequence; deviations
+ * affect only caller-visible side effects (DESIGN.md section 5).
+ */
+public class EcxClayCodeErasureDecodingStep {
+    private final long clay;
+    private final int numErased;
+
+    public EcxClayCodeErasureDecodingStep(int[] erasedIndexes, int numDataUnits, int numParityUnits) {
+        long[] h = new long[1];
+        Ecx.check(EcxNative.clayCreate(numDataUnits, numParityUnits, erasedIndexes, erasedIndexes.length, h));
+        this.clay = h[0];
+        this.numErased = erasedIndexes.length;
+    }
+
+    /** Sub-packetization alpha (ClayCodeUtil, ClayCodeErasureDecodingStep.java:690-695). */
+    public int subPacketSize() {
+        int[] q = new int[1], t = new int[1], alpha = new int[1];
+        Ecx.check(EcxNative.clayGeometry(clay, q, t, alpha));
+        return alpha[0];
+    }
+
+    /**
+     * performCoding(ECChunk[], ECChunk[]) (ClayCodeErasureDecodingStep.java:53-107).  Heap
+     * buffers are passed by array and position; as the reference, input positions
+     * advance by the buffer size and output positions are left where they were.
+     */
+    public void performCoding(ECChunk[] inputChunks, ECChunk[] outputChunks) {
+        ByteBuffer[] in = ECChunk.toBuffers(inputChunks);
+        ByteBuffer[] out = ECChunk.toBuffers(outputChunks);
+        int bufSize = -1;
+        for (ByteBuffer b : in) {
+            if (b != null) {
+                bufSize = b.remaining();
+                break;
+            }
+        }
+        if (bufSize < 0) {
+            throw new IllegalArgumentException("Invalid buffer, all null");
+        }
+        byte[][] inArrays = new byte[in.length][];
+        int[] inPos = new int[in.length];
+        for (int i = 0; i < in.length; i++) {
+            if (in[i] != null) {
+                inArrays[i] = in[i].array();
+                inPos[i] = in[i].arrayOffset() + in[i].position();
+            }
+        }
+        byte[][] outArrays = new byte[out.length][];
+        int[] outPos = new int[out.length];
+        for (int i = 0; i < out.length; i++) {
+            outArrays[i] = out[i].array();
+            outPos[i] = out[i].arrayOffset() + out[i].position();
+        }
+        Ecx.check(EcxNative.clayPerformCoding(clay, inArrays, inPos, outArrays, outPos, bufSize));
+        for (ByteBuffer b : in) {
+            if (b != null) {
+                b.position(b.position() + bufSize);
+            }
+        }
+    }
+
+    /**
+     * Batched performCoding over {@code nstripes} device-resident stripes (HBM addresses):
+     * stripe s's sub-chunk slot z*n+node at in + s*inStripeStride + slot*inSubStride, its
+     * repaired sub-chunk z*|E|+j at out + s*outStripeStride + slot*outSubStride.  Enqueued on
+     * {@code stream} (a hipStream_t, 0 = the default stream).
+     */
+    public void performCodingBatch(long in, long inStripeStride, long inSubStride, long out, long outStripeStride,
+                                   long outSubStride, long nstripes, long bufSize, long stream) {
+        Ecx.check(EcxNative.clayPerformCodingBatch(clay, in, inStripeStride, inSubStride, out, outStripeStride,
+                outSubStride, nstripes, bufSize, stream));
+    }
+
+    /** The same from direct host ByteBuffers (pipelined over PCIe; synchronous). */
+    public void performCodingBatchHost(ByteBuffer in, long inStripeStride, long inSubStride, ByteBuffer out,
+                                       long outStripeStride, long outSubStride, long nstripes, long bufSize) {
+        Ecx.check(EcxNative.clayPerformCodingBatchHost(clay, EcxNative.directAddress(in), inStripeStride,
+                inSubStride, EcxNative.directAddress(out), outStripeStride, outSubStride, nstripes, bufSize));
+    }
+
+    public int numErased() {
+        return numErased;
+    }
+
+    /** Releases the native decoding step. */
+    public void close() {
+        EcxNative.clayDestroy(clay);
+    }
+}

@@ -8,8 +8,13 @@ N=1, everything is on rank 0.  Each rank holds its nodes' sub-chunks node-major 
 --stripes stripes.  Slices of --slice stripes flow along the chain as partial sums,
 over RCCL P2P ("nccl") or, with ECX_CHAIN_BACKEND=gloo, staged through the host
 (a rehearsal on a box with fewer GPUs than ranks).
-Prints one JSON line on the destination rank: the stripes repaired per second through
-the chain, and the algorithmic GiB/s (917,504 B per stripe, as in bench.py).
+Prints one driver-style JSON line on the destination rank (the bench.py fields: metric,
+value, unit, n_gpus, ...): the algorithmic GiB/s of stripes repaired through the chain
+(917,504 B per stripe, as in bench.py), the per-hop partial-sum rate in GB/s, the slice
+size and the chain of ranks.  `--gpus N` without a launcher starts the N ranks itself
+(torch.distributed.run as a child process, as bench.py does).  The reference's shape
+is ClayCoordinator.kt:265-319 (decodeDecoupledData: the partial-sum chain along
+nodesPath) and ClayCodeNode.kt:165-233 (each hop's decodeMissingSingle and forward).
 """
 import json
 import os
@@ -28,7 +33,17 @@ def main():
     ap.add_argument("--slice", type=int, default=128)
     ap.add_argument("--buffers", type=int, default=3)
     ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+               "--master-addr=127.0.0.1", "--master-port=%d" % port, str(Path(__file__).resolve())] + sys.argv[1:]
+        raise SystemExit(subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode)
     import torch
     import torch.distributed as dist
     import rpamd
@@ -82,12 +97,23 @@ def main():
         best = el if best is None else min(best, el)
     if rank == dest:
         print(json.dumps({
-            "what": "pipelined partial-sum repair chain, Clay(4,2) e=1, B=32 KiB",
-            "world": world, "backend": backend if world > 1 else "none", "chain": order, "dest": dest,
-            "stripes": S, "slice_stripes": args.slice, "seconds": round(best, 4),
+            "metric": "GiB/s pipelined partial-sum repair chain (device-resident), Clay(4,2) 32 KiB blocks",
+            "value": round(S * 917504 / best / 2**30, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "higher_is_better": True,
+            "dtype": "u8",
+            "data": "synthetic (device splitmix64 sub-chunks)",
+            "config": {"workload": "Clay(4,2) repair of node 1 through a chain of %d rank(s), helpers node-major "
+                                   "per rank, destination rank %d" % (len(order), dest),
+                       "stripes": S, "slice_stripes": args.slice, "buffers": args.buffers},
+            "backend": backend if world > 1 else "none",
+            "chain": order,
+            "dest": dest,
+            "seconds": round(best, 4),
             "stripes_per_s": round(S / best, 1),
-            "GiB_per_s_algorithmic": round(S * 917504 / best / 2**30, 2),
             "per_hop_GB_per_s": round(S * A * B / best / 1e9, 2),
+            "per_hop_bytes_per_stripe": A * B,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -14,6 +14,8 @@
 #include <random>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "ecx.h"
 #include "ecx_tune.h"
 
@@ -96,6 +98,37 @@ int main() {
             }
         }
         ecx_tune("plan_cache", 256);
+    }
+    // The LRC chain hop (NodeHelper.kt:86-97): the reference calls
+    // LRCErasureCode.encodeParitySingle (RS(3,1), ReedSolomon.java:110-118) once per 34-B
+    // word, 1024 words per 34,816-B block (PipelineUtil.kt:10-11).  The same partial sums
+    // for the whole block: one host call over 34,816 B, or one device-resident
+    // ecx_rs_encode_partial_batch (block already in HBM; includes the stream sync).
+    {
+        ecx_rs *rs31 = nullptr;
+        if (ecx_rs_create(3, 1, &rs31)) return 1;
+        const int W = 34, NW = 1024, BLK = W * NW;
+        std::vector<uint8_t> block(BLK), acc(BLK);
+        fill(block);
+        const double word = median_us([&] { return ecx_rs_encode_parity_single(rs31, block.data(), acc.data(), 1, 0, 0, W); });
+        const double blk = median_us([&] { return ecx_rs_encode_parity_single(rs31, block.data(), acc.data(), 1, 0, 0, BLK); });
+        uint8_t *d_in = nullptr, *d_acc = nullptr;
+        if (hipMalloc(&d_in, BLK) != hipSuccess || hipMalloc(&d_acc, BLK) != hipSuccess) return 1;
+        if (hipMemcpy(d_in, block.data(), BLK, hipMemcpyHostToDevice) != hipSuccess) return 1;
+        const double dev = median_us([&] {
+            int st = ecx_rs_encode_partial_batch(rs31, 1, d_in, BLK, d_acc, BLK, BLK, 1, BLK, 0, nullptr);
+            return st ? st : ecx_synchronize(nullptr);
+        });
+        printf("{\"case\": \"LRC chain hop, encodeParitySingle per 34-B word (NodeHelper.kt:89)\", \"us_per_call\": %.1f, "
+               "\"calls_per_block\": %d, \"us_per_block\": %.1f}\n", word, NW, word * NW);
+        printf("{\"case\": \"LRC chain hop, one encodeParitySingle over the 34,816-B block (host buffers)\", "
+               "\"us_per_call\": %.1f, \"calls_per_block\": 1, \"us_per_block\": %.1f}\n", blk, blk);
+        printf("{\"case\": \"LRC chain hop, ecx_rs_encode_partial_batch over the block in HBM (+ sync)\", "
+               "\"us_per_call\": %.1f, \"calls_per_block\": 1, \"us_per_block\": %.1f}\n", dev, dev);
+        fflush(stdout);
+        (void)hipFree(d_in);
+        (void)hipFree(d_acc);
+        ecx_rs_destroy(rs31);
     }
     ecx_clay_destroy(clay);
     ecx_rs_destroy(rs);
