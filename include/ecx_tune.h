@@ -43,6 +43,10 @@
  *                      aligned layouts whose slot offsets fit 31 bits: 1 = for multi-tile maps
  *                      that do not run as wide tiles, 2 = for every such map, 0 = never (default;
  *                      measured slower, bound by its scalar branches)
+ *   "clay_rtc"         Clay single-node repair batches (ecx_clay_perform_coding_batch): 1 = the
+ *                      per-helper-plane kernel generated for the repair and compiled with hiprtc, for
+ *                      the whole 4 KiB chunks of 16-B-aligned layouts (default); 0 = the composed-map
+ *                      kernel only
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered
@@ -75,6 +79,16 @@ int ecx_map_plan_stats(const struct ecx_map *map, int *n_tiles, int *n_entries, 
  * NUL-terminated into buf.  Returns its length (0 = no launch yet), or
  * ECX_E_ILLEGAL_ARGUMENT if buf is null or shorter than length + 1. */
 int ecx_last_kernel(char *buf, int len);
+/* The per-helper-plane Clay repair kernel (ecx_tune "clay_rtc"): builds the clay
+ * step's repair program (checked against the composed reference map), generates the
+ * kernel source and compiles it with hiprtc for gfx950 -- no device needed.  Returns
+ * the code-object size, ECX_E_ILLEGAL_ARGUMENT if the step has no such program (not a
+ * single-node repair), ECX_E_DEVICE if hiprtc is missing or fails. */
+struct ecx_clay;
+int ecx_clay_rtc_compile_check(struct ecx_clay *clay);
+/* The generated kernel source: copied NUL-terminated into buf when len exceeds its
+ * length; returns the length. */
+int ecx_clay_rtc_source(struct ecx_clay *clay, char *buf, int len);
 #ifdef __cplusplus
 }
 #endif

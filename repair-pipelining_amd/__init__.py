@@ -629,6 +629,23 @@ class ClayCodeErasureDecodingStep:
             lib().ecx_clay_destroy(self._h)
             self._h = None
 
+    def rtcCompileCheck(self) -> int:
+        """Build this single-node repair's per-helper-plane program (checked against the
+        composed reference map), generate its kernel and compile it with hiprtc for
+        gfx950; returns the code-object size (ecx_clay_rtc_compile_check, include/ecx_tune.h)."""
+        f = lib().ecx_clay_rtc_compile_check
+        f.argtypes, f.restype = [ctypes.c_void_p], ctypes.c_int
+        return check(f(self._h))
+
+    def rtcSource(self) -> str:
+        """The generated k_clay_repair source (ecx_clay_rtc_source)."""
+        f = lib().ecx_clay_rtc_source
+        f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+        n = check(f(self._h, None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        check(f(self._h, buf, n + 1))
+        return buf.value.decode()
+
     def getHelperPlanesIndexes(self, erasedIndex: int):
         out = np.zeros(self.subPacketSize, np.int32)
         n = check(lib().ecx_clay_helper_planes(self._h, erasedIndex, out.ctypes.data))

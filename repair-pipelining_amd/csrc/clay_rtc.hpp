@@ -1,0 +1,53 @@
+// clay_rtc.hpp -- the per-helper-plane Clay repair kernel, generated for one repair
+// program (ClayRepairProgram, codes.hpp) and compiled at run time with hiprtc.
+//
+// The composed-map kernels (k_gf_apply) spend 3 half-rate v_perm_b32 + 2 v_bitop3 per
+// dword and coefficient: Clay(10,4)'s 4,672 coefficients per byte position keep the
+// vector pipe busy.  This kernel executes the repair in its stage
+// structure instead, in bit planes (bits.hpp's transpose), with every coefficient a
+// compile-time constant: a multiply is a fixed XOR network over the 8 planes, chosen
+// by the generator, with no table operands and no scalar branches.  The plane-decode
+// matrix is the same for every helper plane, so one loop body (one helper plane per
+// workgroup) serves all of them and the code stays small.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+
+#include "codes.hpp"
+
+namespace ecx {
+
+constexpr int kRtcThreads = 128;  // 128 lanes x 32 bytes = one 4 KiB chunk
+
+// HIP source of the kernel `k_clay_repair` for this program (exposed for tests).
+std::string clay_rtc_source(const ClayRepairProgram &pg);
+
+class ClayRtc {
+public:
+    explicit ClayRtc(ClayRepairProgram pg);
+    ~ClayRtc();
+    const ClayRepairProgram &program() const { return pg_; }
+    // Compile (hiprtc, once per process) and load (once per device).  Throws
+    // ECX_E_DEVICE when hiprtc or the module load fails.
+    void prepare();
+    // Enqueue the repair of `nchunks` whole 4 KiB chunks (bytes [0, nchunks * 4 KiB) of
+    // every sub-chunk) over nstripes stripes, in the performCoding batch layout.
+    void launch(const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
+                int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nchunks,
+                hipStream_t stream);
+
+private:
+    struct Impl;
+    ClayRepairProgram pg_;
+    std::unique_ptr<Impl> impl_;
+};
+
+// Compile `source` with hiprtc for gfx950 (diagnostics / tests: no device needed).
+// Returns the code object size, throws ECX_E_DEVICE with the compiler log on failure.
+size_t rtc_compile_check(const std::string &source);
+
+}  // namespace ecx

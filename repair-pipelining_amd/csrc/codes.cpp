@@ -377,6 +377,145 @@ void ClayPlanner::decode_multi(std::vector<SymBuf> in, std::vector<SymBuf> &outp
     }
 }
 
+LinearMap ClayRepairProgram::compose(int n_in_slots, int n_out_slots) const {
+    const Field &f = Field::get();
+    LinearMap mp;
+    mp.n_in = n_in_slots;
+    mp.n_out = n_out_slots;
+    for (int j = 0; j < n_in_slots; ++j) mp.in_slot.push_back(j);
+    for (int o = 0; o < n_out_slots; ++o) mp.out_slot.push_back(o);
+    mp.a.assign((size_t)n_in_slots * n_out_slots, 0);
+    auto axpy = [&](std::vector<uint8_t> &y, uint8_t c, const std::vector<uint8_t> &x) {
+        for (size_t i = 0; i < y.size(); ++i) y[i] ^= f.mul(c, x[i]);
+    };
+    auto unit = [&](int slot) {
+        std::vector<uint8_t> v(n_in_slots, 0);
+        if (slot >= 0) v[slot] = 1;
+        return v;
+    };
+    for (int p = 0; p < n_planes; ++p) {
+        const int32_t *t = table.data() + (size_t)p * stride;
+        std::vector<std::vector<uint8_t>> ucol(q, std::vector<uint8_t>(n_in_slots, 0));
+        for (int j = 0; j < n_noncol; ++j) {
+            std::vector<uint8_t> u(n_in_slots, 0);
+            axpy(u, pair_a, unit(t[j]));
+            axpy(u, pair_b, unit(t[n_noncol + j]));
+            for (int r = 0; r < q; ++r) axpy(ucol[r], dmat[(size_t)r * n_noncol + j], u);
+        }
+        const int32_t *mates = t + 2 * n_noncol, *outs = mates + (q - 1);
+        auto put = [&](int slot, const std::vector<uint8_t> &row) {
+            if (slot < 0 || slot >= n_out_slots) throw Error(ECX_E_ILLEGAL_ARGUMENT, "program output slot out of range");
+            std::copy(row.begin(), row.end(), mp.a.begin() + (size_t)slot * n_in_slots);
+        };
+        put(outs[0], ucol[e_row]);
+        for (int i = 0; i < q - 1; ++i) {
+            std::vector<uint8_t> row(n_in_slots, 0);
+            axpy(row, rc_c, unit(mates[i]));
+            axpy(row, rc_u, ucol[mate_row[i]]);
+            put(outs[1 + i], row);
+        }
+    }
+    return mp;
+}
+
+ClayRepairProgram ClayPlanner::repair_program(int erased_index) const {
+    const int nr = n_real(), nn = n();
+    if (erased_real_.size() != 1 || erased_real_[0] != erased_index)
+        throw Error(ECX_E_ILLEGAL_ARGUMENT, "repair program: the planner's erasure set must be {erased_index}");
+    const int e = erased_[0], ey = ny(e);
+    if (e < 0 || e >= nn || ey >= t_) throw Error(ECX_E_INDEX, "erased node outside the q x t grid");
+    ClayRepairProgram pg;
+    pg.q = q_;
+    // the pair transform's two directions (getPairWiseCouple :630-666 as the two callers use it)
+    {
+        const LinearMap dec = pair_.decode_map({true, true, false, false});  // U from (C, C')
+        const LinearMap rec = pair_.decode_map({false, true, false, true});  // C(z',e) from (C(z,x), U(z,x))
+        auto coef = [](const LinearMap &m, int out_slot, int in_slot) -> uint8_t {
+            for (int o = 0; o < m.n_out; ++o)
+                if (m.out_slot[o] == out_slot)
+                    for (int j = 0; j < m.n_in; ++j)
+                        if (m.in_slot[j] == in_slot) return m.at(o, j);
+            return 0;
+        };
+        pg.pair_a = coef(dec, 2, 0);
+        pg.pair_b = coef(dec, 2, 1);
+        pg.rc_c = coef(rec, 0, 1);
+        pg.rc_u = coef(rec, 0, 3);
+    }
+    if ((pg.pair_a ^ pg.pair_b) != 1) throw Error(ECX_E_ILLEGAL_ARGUMENT, "pair transform without the dot identity");
+    std::vector<int> noncol, column;
+    for (int j = 0; j < q_ * t_; ++j) (ny(j) == ey ? column : noncol).push_back(j);
+    pg.n_noncol = (int)noncol.size();
+    // the plane decode: column rows from the non-column nodes (decodeMissing's map)
+    std::vector<bool> present(nn, true);
+    for (int j : column) present[j] = false;
+    const LinearMap dm = rs_.decode_map(present);
+    pg.dmat.assign((size_t)q_ * pg.n_noncol, 0);
+    for (int r = 0; r < q_; ++r)
+        for (int o = 0; o < dm.n_out; ++o)
+            if (dm.out_slot[o] == column[r])
+                for (int jj = 0; jj < dm.n_in; ++jj) {
+                    const auto it = std::find(noncol.begin(), noncol.end(), dm.in_slot[jj]);
+                    if (it == noncol.end()) throw Error(ECX_E_ILLEGAL_ARGUMENT, "plane decode reads a column node");
+                    pg.dmat[(size_t)r * pg.n_noncol + (it - noncol.begin())] = dm.at(o, jj);
+                }
+    for (int r = 0; r < q_; ++r) {
+        if (column[r] == e) pg.e_row = r;
+        else pg.mate_row.push_back(r);
+    }
+    // real slot of (plane z, underlying node u), -1 for a virtual node
+    auto slot = [&](int z, int u) -> int {
+        if (is_virtual(u)) return -1;
+        const int real = u < k_ - v_ ? u : u - v_;
+        return z * nr + real;
+    };
+    const std::vector<int> hidx = helper_planes(erased_real_[0]);
+    pg.n_planes = (int)hidx.size();
+    pg.stride = 2 * pg.n_noncol + 2 * q_ - 1;
+    for (int z : hidx) {
+        const std::vector<int> v = zvec(z);
+        std::vector<int32_t> rec(pg.stride, -1);
+        for (int jj = 0; jj < pg.n_noncol; ++jj) {
+            const int j = noncol[jj], x = nx(j), y = ny(j);
+            rec[jj] = slot(z, j);
+            // a dot pairs with itself: pair_a C + pair_b C = C
+            rec[pg.n_noncol + jj] = v[y] == x ? slot(z, j) : slot(couple_plane(x, y, z), node(v[y], y));
+        }
+        int mi = 0;
+        for (int r = 0; r < q_; ++r) {
+            const int nd = column[r];
+            if (nd == e) {
+                rec[2 * pg.n_noncol + (q_ - 1)] = z;  // output slot z * |E| + 0 (single erasure)
+            } else {
+                rec[2 * pg.n_noncol + mi] = slot(z, nd);
+                rec[2 * pg.n_noncol + (q_ - 1) + 1 + mi] = couple_plane(nx(nd), ey, z);
+                ++mi;
+            }
+        }
+        pg.table.insert(pg.table.end(), rec.begin(), rec.end());
+    }
+    for (int p = 0; p < pg.n_planes; ++p) {
+        const int32_t *t = pg.table.data() + (size_t)p * pg.stride;
+        for (int i = 0; i < 2 * pg.n_noncol + q_ - 1; ++i) pg.max_in_slot = std::max(pg.max_in_slot, (int)t[i]);
+        for (int i = 0; i < q_; ++i) pg.max_out_slot = std::max(pg.max_out_slot, (int)t[2 * pg.n_noncol + q_ - 1 + i]);
+    }
+    // The program must be the reference's map exactly (standard null pattern: the
+    // erased node absent, every other sub-chunk present).
+    std::vector<bool> pres((size_t)nr * alpha_, true);
+    for (int z = 0; z < alpha_; ++z) pres[(size_t)z * nr + erased_index] = false;
+    const LinearMap ref = perform_coding_map(pres);
+    const LinearMap got = pg.compose(nr * alpha_, alpha_);
+    if (ref.n_out != alpha_ || got.nnz() != ref.nnz())
+        throw Error(ECX_E_ILLEGAL_ARGUMENT, "repair program differs from the reference map");
+    for (int o = 0; o < ref.n_out; ++o) {
+        if (ref.out_slot[o] != o) throw Error(ECX_E_ILLEGAL_ARGUMENT, "unexpected output order");
+        for (int j = 0; j < ref.n_in; ++j)
+            if (ref.at(o, j) != got.at(o, ref.in_slot[j]))
+                throw Error(ECX_E_ILLEGAL_ARGUMENT, "repair program differs from the reference map");
+    }
+    return pg;
+}
+
 LinearMap ClayPlanner::perform_coding_map(const std::vector<bool> &input_present) const {
     const int nn = n(), nr = n_real(), ne = (int)erased_.size();
     const int width = nr * alpha_;  // symbolic inputs = the real slots

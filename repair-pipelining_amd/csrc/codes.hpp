@@ -76,6 +76,31 @@ private:
     RsCode group_;
 };
 
+// Single-node Clay repair (doDecodeSingle, ClayCodeErasureDecodingStep.java:118-221) as a
+// program over its helper planes, the stage structure the per-plane kernel
+// (clay_rtc.cpp) executes.  For helper plane p (plane z = helper_planes(e)[p]):
+//   decouple (:435-492)   U_j = pair_a * C(z, j) + pair_b * C(z', j') for every node j
+//                         outside e's column (a dot, j' = j and z' = z, gives U_j = C(z, j)
+//                         because pair_a ^ pair_b == 1; virtual nodes read zeros)
+//   plane decode (:542-597)  U(column row r) = sum_j dmat[r][j] * U_j
+//   re-couple (:180-200)  out(z) = U(e's row); for each column mate x at row r,
+//                         out(z'_x) = rc_c * C(z, x) + rc_u * U(r)
+// `table` holds, per helper plane, kClayTab ints: own slot of each non-column node,
+// its partner slot, the mates' slots (q - 1, column order without e) and the q output
+// slots (e's plane, then the mates'), real slot numbers or -1 (= zeros).
+struct ClayRepairProgram {
+    int q = 0, n_planes = 0, n_noncol = 0, stride = 0;  // stride = ints per plane in `table`
+    uint8_t pair_a = 0, pair_b = 0, rc_c = 0, rc_u = 0;
+    int e_row = 0;
+    std::vector<int> mate_row;     // q - 1 column rows
+    std::vector<uint8_t> dmat;     // q x n_noncol
+    std::vector<int32_t> table;    // n_planes x stride
+    int max_in_slot = -1, max_out_slot = -1;
+    // The program composed into a dense map over (out slot, in slot); tests compare it
+    // with perform_coding_map (the reference's stage sequence).
+    LinearMap compose(int n_in_slots, int n_out_slots) const;
+};
+
 // ClayCodeErasureDecodingStep.java + ClayCodeUtil (:676-944), symbolically.
 //
 // virtual_units > 0 builds a SHORTENED code: Clay(k + v, m) whose data nodes
@@ -105,6 +130,11 @@ public:
     // planes this helper plane writes are non-empty; `written` marks them).
     LinearMap decode_single_helper_map(const std::vector<bool> &helper_present, int helper_i, int erased_index,
                                        std::vector<bool> *written) const;
+    // Single-node repair of real node `erased_index` as a per-helper-plane program
+    // (ClayRepairProgram).  Throws ECX_E_ILLEGAL_ARGUMENT when the code's pair
+    // transform does not allow the dot trick (pair_a ^ pair_b != 1) or when the
+    // program does not compose to perform_coding_map exactly.
+    ClayRepairProgram repair_program(int erased_index) const;
 
 private:
     int k_, m_, v_, q_, t_, alpha_;

@@ -8,6 +8,7 @@
 #include <mutex>
 #include <string>
 
+#include "clay_rtc.hpp"
 #include "engine.hpp"
 
 using namespace ecx;
@@ -30,6 +31,10 @@ struct ecx_clay {
     ClayPlanner pl;
     std::mutex mu;
     std::map<std::string, std::unique_ptr<ecx_map>> maps;
+    // Single-node repair as the per-helper-plane kernel (clay_rtc.hpp), built on first use.
+    std::unique_ptr<ClayRtc> rtc;
+    int rtc_state = 0;  // 0 = not tried, 1 = available, -1 = not representable
+    std::string rtc_why;
 };
 
 namespace {
@@ -695,6 +700,26 @@ int ecx_clay_map(ecx_clay *clay, const ecx_map **out) {
     });
 }
 
+namespace {
+// The per-helper-plane repair kernel of a single-erasure step, or nullptr when the
+// step's repair has no such program (ClayPlanner::repair_program throws; the reason is
+// kept for ecx_clay_rtc_compile_check).
+ClayRtc *clay_rtc(ecx_clay *clay) {
+    std::lock_guard<std::mutex> lk(clay->mu);
+    if (clay->rtc_state == 0) {
+        try {
+            if (clay->pl.erased().size() != 1) throw Error(ECX_E_ILLEGAL_ARGUMENT, "not a single-node repair");
+            clay->rtc.reset(new ClayRtc(clay->pl.repair_program(clay->pl.erased()[0])));
+            clay->rtc_state = 1;
+        } catch (const Error &e) {
+            clay->rtc_state = -1;
+            clay->rtc_why = e.what();
+        }
+    }
+    return clay->rtc_state == 1 ? clay->rtc.get() : nullptr;
+}
+}  // namespace
+
 int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride, int64_t in_sub_stride,
                                   uint8_t *out, int64_t out_stripe_stride, int64_t out_sub_stride, int64_t nstripes,
                                   int64_t buf_size, void *stream) {
@@ -703,9 +728,44 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
         if (nstripes < 0 || buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
         ecx_map *m = clay_standard_map(clay);
-        launch_apply(m->cm, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
-                     buf_size, (hipStream_t)stream);
+        // Single-node repair: the per-helper-plane kernel (clay_rtc.hpp) for the whole
+        // 4 KiB chunks of 16-B-aligned layouts whose slot offsets fit 31 bits; the
+        // composed-map kernel takes any tail and every other layout.
+        int64_t done = 0;
+        if (tuning().clay_rtc && buf_size >= kChunkBytes && ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+            in_stripe_stride % 16 == 0 && in_sub_stride % 16 == 0 && out_stripe_stride % 16 == 0 &&
+            out_sub_stride % 16 == 0 && in_sub_stride >= 0 && out_sub_stride >= 0) {
+            if (ClayRtc *r = clay_rtc(clay)) {
+                if ((int64_t)r->program().max_in_slot * in_sub_stride + kChunkBytes <= 0x7FFFFFFF) {
+                    done = buf_size / kChunkBytes * kChunkBytes;
+                    r->launch(in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
+                              done / kChunkBytes, (hipStream_t)stream);
+                }
+            }
+        }
+        if (done < buf_size)
+            launch_apply(m->cm, in + done, in_stripe_stride, in_sub_stride, out + done, out_stripe_stride,
+                         out_sub_stride, nstripes, buf_size - done, (hipStream_t)stream);
+        if (done > 0) set_last_kernel("k_clay_repair");
         return ECX_OK;
+    });
+}
+
+int ecx_clay_rtc_compile_check(ecx_clay *clay) {
+    return guarded([&]() -> int {
+        ClayRtc *r = clay_rtc(clay);
+        if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
+        return (int)rtc_compile_check(clay_rtc_source(r->program()));
+    });
+}
+
+int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
+    return guarded([&]() -> int {
+        ClayRtc *r = clay_rtc(clay);
+        if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
+        const std::string src = clay_rtc_source(r->program());
+        if (buf && len > (int)src.size()) std::memcpy(buf, src.c_str(), src.size() + 1);
+        return (int)src.size();
     });
 }
 
@@ -881,6 +941,7 @@ int ecx_tune(const char *key, int value) {
         if (value < 0) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_gather_max = (int64_t)value << 10;
     }
+    else if (k == "clay_rtc") t.clay_rtc = value != 0;
     else if (k == "bitslice") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.bitslice = value;

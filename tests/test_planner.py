@@ -276,3 +276,22 @@ def test_compiled_plan_selftest_random_maps(ecx):
         ecx.GfMap.from_matrix(m, in_slot=in_slot, out_slot=out_slot).selftest(seed & 0xFFFF)
 
     check()
+
+
+@pytest.mark.parametrize("k,m,v,e", [(4, 2, 0, 1), (4, 2, 0, 5), (10, 4, 2, 3), (10, 4, 2, 13), (12, 4, 0, 0),
+                                     (6, 3, 0, 7), (2, 2, 0, 0)])
+def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
+    """The single-node repair as a per-helper-plane program (ClayPlanner::repair_program:
+    decouple with the dot identity pair_a ^ pair_b = 1, plane decode, re-couple) composes
+    to exactly the reference stage sequence's map (checked inside the builder), and its
+    generated kernel compiles with hiprtc for gfx950 without a device."""
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    assert step.rtcCompileCheck() > 0
+    src = step.rtcSource()
+    assert "k_clay_repair" in src and "__launch_bounds__" in src
+
+
+def test_clay_rtc_refuses_multi_erasure(ecx):
+    step = ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2)
+    with pytest.raises(ecx.EcxError):
+        step.rtcCompileCheck()
