@@ -1155,3 +1155,32 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B):
         ref = [np.zeros(B, np.uint8) for _ in range(a)]
         O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
         assert all((outs[1][0][S - 1, z] == ref[z]).all() for z in range(a))
+
+
+def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):
+    """Stripe bases beyond 2 and 4 GiB from the allocation start (a 2.25 GiB stripe
+    pitch): the generated kernel's 64-bit stripe addressing (a sign-extended low half
+    would corrupt the buffer descriptor) matches the composed-map kernel on every stripe."""
+    torch = torch_dev
+    k, m, v, e, B = 10, 4, 2, 3, 4096
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    n, a = k + m, step.subPacketSize
+    pitch, S = (9 << 28) + 4096, 3
+    used = n * a * B
+    buf = torch.empty((S - 1) * pitch + used, dtype=torch.uint8, device="cuda")
+    for s in range(S):
+        ecx.fill_random(buf[s * pitch:s * pitch + used], used, 90 + s)
+    outs = []
+    try:
+        for rtc in (0, 1):
+            ecx.tune("clay_rtc", rtc)
+            o = torch.full((S, a, B), 0x33, dtype=torch.uint8, device="cuda")
+            step.performCodingBatch(buf, pitch, B, o, a * B, B, S, B)
+            torch.cuda.synchronize()
+            outs.append((o.cpu().numpy(), ecx.last_kernel()))
+    finally:
+        ecx.tune("clay_rtc", 1)
+    assert outs[1][1] == "k_clay_repair"
+    assert (outs[0][0] == outs[1][0]).all()
+    del buf
+    torch.cuda.empty_cache()
