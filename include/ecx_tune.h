@@ -43,10 +43,11 @@
  *                      aligned layouts whose slot offsets fit 31 bits: 1 = for multi-tile maps
  *                      that do not run as wide tiles, 2 = for every such map, 0 = never (default;
  *                      measured slower, bound by its scalar branches)
- *   "clay_rtc"         Clay single-node repair batches (ecx_clay_perform_coding_batch): 1 = the
+ *   "clay_rtc"         Clay single-node repair batches (ecx_clay_perform_coding_batch): the
  *                      per-helper-plane kernel generated for the repair and compiled with hiprtc, for
- *                      the whole 4 KiB chunks of 16-B-aligned layouts (default); 0 = the composed-map
- *                      kernel only
+ *                      the whole 4 KiB chunks of 16-B-aligned layouts: 1 = when the composed map spans
+ *                      several 8-row tiles (alpha > 8: Clay(10,4), Clay(12,4); default), 2 = always,
+ *                      0 = never (the composed-map kernel only)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -732,7 +732,13 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
         // 4 KiB chunks of 16-B-aligned layouts whose slot offsets fit 31 bits; the
         // composed-map kernel takes any tail and every other layout.
         int64_t done = 0;
-        if (tuning().clay_rtc && buf_size >= kChunkBytes && ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+        // auto (1): repairs whose composed map spans several 8-row tiles (alpha > 8), where
+        // the composed kernel is bound by vector issue (Clay(10,4): 0.61 -> 0.70 of HBM);
+        // Clay(4,2)'s single-tile map is memory-bound and stays on the composed kernel
+        // (0.83 there vs 0.63 per plane: profiles/r02_clay_rtc_ab.jsonl).
+        const int rtc_mode = tuning().clay_rtc;
+        const bool rtc_want = rtc_mode == 2 || (rtc_mode == 1 && m->cm.n_tiles() > 1);
+        if (rtc_want && buf_size >= kChunkBytes && ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
             in_stripe_stride % 16 == 0 && in_sub_stride % 16 == 0 && out_stripe_stride % 16 == 0 &&
             out_sub_stride % 16 == 0 && in_sub_stride >= 0 && out_sub_stride >= 0) {
             if (ClayRtc *r = clay_rtc(clay)) {
@@ -941,7 +947,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_gather_max = (int64_t)value << 10;
     }
-    else if (k == "clay_rtc") t.clay_rtc = value != 0;
+    else if (k == "clay_rtc") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.clay_rtc = value;
+    }
     else if (k == "bitslice") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.bitslice = value;

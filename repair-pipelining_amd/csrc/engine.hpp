@@ -219,9 +219,9 @@ struct Tuning {
     // tiles, 0 = never (default: it measured 4-10 % slower on every BASELINE map, bound
     // by its scalar branches -- profiles/r02_bits_ab.jsonl, r02_bits_sq_ab.json).
     int bitslice = 0;
-    // Clay single-node repair batches: 1 = the per-helper-plane kernel generated for the
-    // repair and compiled with hiprtc (clay_rtc.hpp) for whole 4 KiB chunks, 0 = the
-    // composed-map kernel only.
+    // Clay single-node repair batches: the per-helper-plane kernel generated for the
+    // repair and compiled with hiprtc (clay_rtc.hpp) for whole 4 KiB chunks -- 1 = when
+    // the composed map spans several tiles (auto), 2 = always, 0 = never.
     int clay_rtc = 1;
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight

@@ -1139,7 +1139,7 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B):
     ecx.fill_random(pool, pool.numel(), 41 + e)
     outs = {}
     try:
-        for rtc in (0, 1):
+        for rtc in (0, 2):
             ecx.tune("clay_rtc", rtc)
             o = torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
@@ -1147,14 +1147,14 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B):
             outs[rtc] = (o.cpu().numpy(), ecx.last_kernel())
     finally:
         ecx.tune("clay_rtc", 1)
-    assert outs[1][1] == "k_clay_repair", outs[1][1]
-    assert (outs[0][0] == outs[1][0]).all()
+    assert outs[2][1] == "k_clay_repair", outs[2][1]
+    assert (outs[0][0] == outs[2][0]).all()
     if v == 0:
         host = pool[S - 1].cpu().numpy()
         inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
         ref = [np.zeros(B, np.uint8) for _ in range(a)]
         O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
-        assert all((outs[1][0][S - 1, z] == ref[z]).all() for z in range(a))
+        assert all((outs[2][0][S - 1, z] == ref[z]).all() for z in range(a))
 
 
 def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):
@@ -1172,7 +1172,7 @@ def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):
         ecx.fill_random(buf[s * pitch:s * pitch + used], used, 90 + s)
     outs = []
     try:
-        for rtc in (0, 1):
+        for rtc in (0, 2):
             ecx.tune("clay_rtc", rtc)
             o = torch.full((S, a, B), 0x33, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(buf, pitch, B, o, a * B, B, S, B)
