@@ -48,6 +48,9 @@
  *                      the whole 4 KiB chunks of 16-B-aligned layouts: 1 = when the composed map spans
  *                      several 8-row tiles (alpha > 8: Clay(10,4), Clay(12,4); default), 2 = always,
  *                      0 = never (the composed-map kernel only)
+ *   "rtc_lookahead"    that kernel's generated load schedule: items (non-column nodes, mates) whose
+ *                      loads are issued ahead of the one being computed, 0..3 (default 1)
+ *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -23,8 +23,16 @@ namespace ecx {
 
 constexpr int kRtcThreads = 128;  // 128 lanes x 32 bytes = one 4 KiB chunk
 
+// Code-generation shape (ecx_tune "rtc_lookahead" / "rtc_waves"): items whose loads are
+// issued ahead of the one being computed, and the minimum waves per SIMD the register
+// budget is set for.
+struct RtcShape {
+    int lookahead = 1;
+    int waves = 3;
+};
+
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).
-std::string clay_rtc_source(const ClayRepairProgram &pg);
+std::string clay_rtc_source(const ClayRepairProgram &pg, const RtcShape &shape = RtcShape());
 
 class ClayRtc {
 public:

@@ -951,6 +951,14 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.clay_rtc = value;
     }
+    else if (k == "rtc_lookahead") {
+        if (value < 0 || value > 3) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_lookahead = value;
+    }
+    else if (k == "rtc_waves") {
+        if (value < 2 || value > 4) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_waves = value;
+    }
     else if (k == "bitslice") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.bitslice = value;

@@ -223,6 +223,8 @@ struct Tuning {
     // repair and compiled with hiprtc (clay_rtc.hpp) for whole 4 KiB chunks -- 1 = when
     // the composed map spans several tiles (auto), 2 = always, 0 = never.
     int clay_rtc = 1;
+    int rtc_lookahead = 1;  // the generated kernel's load lookahead (items), 0..3
+    int rtc_waves = 3;      // its __launch_bounds__ minimum waves per SIMD, 2..4
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -1,0 +1,74 @@
+"""Sweep the generated per-helper-plane Clay kernel's code shape (ecx_tune
+"rtc_lookahead" x "rtc_waves") on BASELINE config 4 (shortened Clay(10,4), 1 MiB node
+blocks = 256 x 4 KiB sub-chunks, repair of node 3) in one process: one resident pool,
+every shape verified against the composed-map kernel, interleaved rounds, median
+per-launch time -> algorithmic GB/s and fraction of the 8 TB/s HBM peak.
+
+    python scripts/rtc_sweep.py [--pool 2048 --reps 10 --rounds 2]
+"""
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import rpamd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pool", type=int, default=2048)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--erased", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    ecx = rpamd.load()
+    k, m, v, b, a = 10, 4, 2, 4096, 256
+    n, P = k + m, args.pool
+    pool = torch.empty((P, n * a, b), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 11)
+    step = ecx.ClayCodeErasureDecodingStep([args.erased], k, m, virtualUnits=v)
+    info = step.map().info()
+    unit = (info["n_in"] + info["n_out"]) * b
+    ref = torch.empty((P, a, b), dtype=torch.uint8, device="cuda")
+    ecx.tune("clay_rtc", 0)
+    step.performCodingBatch(pool, n * a * b, b, ref, a * b, b, P, b)
+    torch.cuda.synchronize()
+    shapes = [("composed", None, None)] + [("rtc", la, w) for w in (2, 3, 4) for la in (0, 1, 2, 3)]
+    out = torch.empty_like(ref)
+    times = {s: [] for s in shapes}
+    for _ in range(args.rounds):
+        for s in shapes:
+            if s[0] == "composed":
+                ecx.tune("clay_rtc", 0)
+            else:
+                ecx.tune("clay_rtc", 2)
+                ecx.tune("rtc_lookahead", s[1])
+                ecx.tune("rtc_waves", s[2])
+            out.fill_(0)
+            step.performCodingBatch(pool, n * a * b, b, out, a * b, b, P, b)
+            torch.cuda.synchronize()
+            if not torch.equal(out, ref):
+                raise SystemExit("shape %s differs from the composed kernel" % (s,))
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
+            for e0, e1 in evs:
+                e0.record()
+                step.performCodingBatch(pool, n * a * b, b, out, a * b, b, P, b)
+                e1.record()
+            torch.cuda.synchronize()
+            times[s].extend(e0.elapsed_time(e1) for e0, e1 in evs)
+    for s in shapes:
+        ms = statistics.median(times[s])
+        gbs = P * unit / (ms * 1e-3) / 1e9
+        print(json.dumps({"kernel": s[0], "rtc_lookahead": s[1], "rtc_waves": s[2], "launch_ms": round(ms, 4),
+                          "GBps": round(gbs, 1), "frac": round(gbs / 8000.0, 4)}), flush=True)
+    ecx.tune("clay_rtc", 1)
+    ecx.tune("rtc_lookahead", 1)
+    ecx.tune("rtc_waves", 3)
+
+
+if __name__ == "__main__":
+    main()
