@@ -214,7 +214,8 @@ def cpu_baseline(seconds: float, erased: int, sample=None):
 # launch selection and the plan format / compiler.  Their hash is stored with every PMC
 # profile (profiles/pmc_traffic.json); a profile taken on other kernel code is stale.
 KERNEL_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
-                  "apply_skew.hip", "engine.hpp", "engine.cpp"]
+                  "apply_skew.hip", "apply_bits.hip", "bits.hpp", "engine.hpp", "engine.cpp", "clay_rtc.hpp",
+                  "clay_rtc.cpp", "codes.cpp", "codes.hpp"]
 
 
 def kernel_source_hash() -> str:

@@ -23,12 +23,13 @@ namespace ecx {
 
 constexpr int kRtcThreads = 128;  // 128 lanes x 32 bytes = one 4 KiB chunk
 
-// Code-generation shape (ecx_tune "rtc_lookahead" / "rtc_waves"): items whose loads are
-// issued ahead of the one being computed, and the minimum waves per SIMD the register
-// budget is set for.
+// Code-generation shape (ecx_tune "rtc_lookahead" / "rtc_waves" / "rtc_xcd"): items whose
+// loads are issued ahead of the one being computed, the minimum waves per SIMD the
+// register budget is set for, and the block order.
 struct RtcShape {
     int lookahead = 1;
     int waves = 3;
+    int xcd_local = 0;  // 1: the helper planes of one (stripe, chunk) run on one XCD (shared L2)
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

@@ -955,6 +955,7 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 3) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_lookahead = value;
     }
+    else if (k == "rtc_xcd") t.rtc_xcd = value != 0;
     else if (k == "rtc_waves") {
         if (value < 2 || value > 4) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_waves = value;

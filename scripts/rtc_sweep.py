@@ -1,5 +1,5 @@
 """Sweep the generated per-helper-plane Clay kernel's code shape (ecx_tune
-"rtc_lookahead" x "rtc_waves") on BASELINE config 4 (shortened Clay(10,4), 1 MiB node
+"rtc_lookahead" x "rtc_waves" x "rtc_xcd") on BASELINE config 4 (shortened Clay(10,4), 1 MiB node
 blocks = 256 x 4 KiB sub-chunks, repair of node 3) in one process: one resident pool,
 every shape verified against the composed-map kernel, interleaved rounds, median
 per-launch time -> algorithmic GB/s and fraction of the 8 TB/s HBM peak.
@@ -37,7 +37,7 @@ def main():
     ecx.tune("clay_rtc", 0)
     step.performCodingBatch(pool, n * a * b, b, ref, a * b, b, P, b)
     torch.cuda.synchronize()
-    shapes = [("composed", None, None)] + [("rtc", la, w) for w in (2, 3, 4) for la in (0, 1, 2, 3)]
+    shapes = [("composed", None, None, 0)] + [("rtc", la, w, x) for x in (0, 1) for w in (2, 3) for la in (0, 1, 2)]
     out = torch.empty_like(ref)
     times = {s: [] for s in shapes}
     for _ in range(args.rounds):
@@ -48,6 +48,7 @@ def main():
                 ecx.tune("clay_rtc", 2)
                 ecx.tune("rtc_lookahead", s[1])
                 ecx.tune("rtc_waves", s[2])
+                ecx.tune("rtc_xcd", s[3])
             out.fill_(0)
             step.performCodingBatch(pool, n * a * b, b, out, a * b, b, P, b)
             torch.cuda.synchronize()
@@ -63,11 +64,13 @@ def main():
     for s in shapes:
         ms = statistics.median(times[s])
         gbs = P * unit / (ms * 1e-3) / 1e9
-        print(json.dumps({"kernel": s[0], "rtc_lookahead": s[1], "rtc_waves": s[2], "launch_ms": round(ms, 4),
+        print(json.dumps({"kernel": s[0], "rtc_lookahead": s[1], "rtc_waves": s[2], "rtc_xcd": s[3],
+                          "launch_ms": round(ms, 4),
                           "GBps": round(gbs, 1), "frac": round(gbs / 8000.0, 4)}), flush=True)
     ecx.tune("clay_rtc", 1)
     ecx.tune("rtc_lookahead", 1)
     ecx.tune("rtc_waves", 3)
+    ecx.tune("rtc_xcd", 0)
 
 
 if __name__ == "__main__":

@@ -1123,10 +1123,10 @@ def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
             assert bad.size == 0, (case, s, o, bad[:8], got[s, slot][bad[:8]], ref[o][bad[:8]])
 
 
-@pytest.mark.parametrize("k,m,v,e,B", [(4, 2, 0, 1, 4096 * 2 + 112), (4, 2, 0, 4, 4096), (4, 2, 0, 0, 8192),
-                                       (10, 4, 2, 3, 4096), (10, 4, 2, 13, 4096 + 16), (10, 4, 2, 9, 4096),
-                                       (12, 4, 0, 5, 4096), (6, 3, 0, 2, 4096 * 2), (2, 2, 0, 3, 4096)])
-def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B):
+@pytest.mark.parametrize("k,m,v,e,B,S", [(4, 2, 0, 1, 4096 * 2 + 112, 3), (4, 2, 0, 4, 4096, 9), (4, 2, 0, 0, 8192, 3),
+                                         (10, 4, 2, 3, 4096, 3), (10, 4, 2, 13, 4096 + 16, 3), (10, 4, 2, 9, 4096, 17),
+                                         (12, 4, 0, 5, 4096, 3), (6, 3, 0, 2, 4096 * 2, 5), (2, 2, 0, 3, 4096, 3)])
+def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S):
     """The per-helper-plane repair kernel (clay_rtc.hpp: generated for the repair
     program and compiled with hiprtc) over whole 4 KiB chunks, the composed-map kernel
     over the tail: every stripe equals the composed-map kernel alone (ecx_tune
@@ -1134,21 +1134,22 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B):
     torch = torch_dev
     step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
     n, a = k + m, step.subPacketSize
-    S = 3
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 41 + e)
     outs = {}
     try:
-        for rtc in (0, 2):
+        for rtc, xcd in ((0, 0), (2, 0), (2, 1)):  # composed; per-plane kernel, plane-fastest / XCD-local order
             ecx.tune("clay_rtc", rtc)
+            ecx.tune("rtc_xcd", xcd)
             o = torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
             torch.cuda.synchronize()
-            outs[rtc] = (o.cpu().numpy(), ecx.last_kernel())
+            outs[rtc + xcd] = (o.cpu().numpy(), ecx.last_kernel())
     finally:
         ecx.tune("clay_rtc", 1)
-    assert outs[2][1] == "k_clay_repair", outs[2][1]
-    assert (outs[0][0] == outs[2][0]).all()
+        ecx.tune("rtc_xcd", 0)
+    assert outs[2][1] == "k_clay_repair" and outs[3][1] == "k_clay_repair", outs[2][1]
+    assert (outs[0][0] == outs[2][0]).all() and (outs[0][0] == outs[3][0]).all()
     if v == 0:
         host = pool[S - 1].cpu().numpy()
         inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
