@@ -52,7 +52,7 @@
  *                      loads are issued ahead of the one being computed, 0..3 (default 1)
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_xcd"          that kernel's block order: 1 = the helper planes of one (stripe, chunk) on one
- *                      XCD (their shared partner loads meet in its L2), 0 = plane-fastest (default 0)
+ *                      XCD (their shared partner loads meet in its L2; default), 0 = plane-fastest
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -225,7 +225,8 @@ struct Tuning {
     int clay_rtc = 1;
     int rtc_lookahead = 1;  // the generated kernel's load lookahead (items), 0..3
     int rtc_waves = 3;      // its __launch_bounds__ minimum waves per SIMD, 2..4
-    int rtc_xcd = 0;        // its block order: 1 = the helper planes of a (stripe, chunk) on one XCD
+    int rtc_xcd = 1;        // its block order: 1 = the helper planes of a (stripe, chunk) on one XCD
+                            // (+1.1 % on Clay(10,4), profiles/r02_rtc_sweep.jsonl)
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

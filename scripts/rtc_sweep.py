@@ -70,7 +70,7 @@ def main():
     ecx.tune("clay_rtc", 1)
     ecx.tune("rtc_lookahead", 1)
     ecx.tune("rtc_waves", 3)
-    ecx.tune("rtc_xcd", 0)
+    ecx.tune("rtc_xcd", 1)
 
 
 if __name__ == "__main__":

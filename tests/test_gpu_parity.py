@@ -1147,7 +1147,7 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
             outs[rtc + xcd] = (o.cpu().numpy(), ecx.last_kernel())
     finally:
         ecx.tune("clay_rtc", 1)
-        ecx.tune("rtc_xcd", 0)
+        ecx.tune("rtc_xcd", 1)
     assert outs[2][1] == "k_clay_repair" and outs[3][1] == "k_clay_repair", outs[2][1]
     assert (outs[0][0] == outs[2][0]).all() and (outs[0][0] == outs[3][0]).all()
     if v == 0:
