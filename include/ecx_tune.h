@@ -49,8 +49,16 @@
  *                      several 8-row tiles (alpha > 8: Clay(10,4), Clay(12,4); default), 2 = always,
  *                      0 = never (the composed-map kernel only)
  *   "rtc_lookahead"    that kernel's generated load schedule: items (non-column nodes, mates) whose
- *                      loads are issued ahead of the one being computed, 0..3 (default 1)
+ *                      loads are issued ahead of the one being computed, 0..3 (default 1); for the
+ *                      plane-group kernel bit 0 = partner and mate loads after row ya, bit 1 = skip
+ *                      the dot's and virtual partners' transposes by uniform branches
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
+ *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
+ *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes
+ *                      per workgroup, partners exchanged in registers and LDS; default), 0 = one
+ *                      helper plane per workgroup
+ *   "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
+ *                      a persistent grid of that many workgroups per CU walking the units
  *   "rtc_xcd"          that kernel's block order: 1 = the helper planes of one (stripe, chunk) on one
  *                      XCD (their shared partner loads meet in its L2; default), 0 = plane-fastest
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)

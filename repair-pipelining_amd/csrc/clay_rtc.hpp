@@ -30,10 +30,21 @@ struct RtcShape {
     int lookahead = 1;
     int waves = 3;
     int xcd_local = 0;  // 1: the helper planes of one (stripe, chunk) run on one XCD (shared L2)
+    int group = 0;      // 1: the plane-group kernel (k_clay_repair_grp) where the program allows it
+    int persist = 0;    // plane-group kernel: > 0 = a persistent grid of this many workgroups per CU
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).
 std::string clay_rtc_source(const ClayRepairProgram &pg, const RtcShape &shape = RtcShape());
+
+// The plane-group kernel `k_clay_repair_grp` (clay_rtc.cpp): one 256-thread workgroup
+// per (stripe, 512-B slice, q x q square of helper planes), partners exchanged on chip.
+// Supported for q == 4 codes with at least two free plane digits (Clay(12,4), the
+// shortened Clay(10,4), Clay(8,4), ...); `why` gets the reason otherwise.
+bool clay_grp_supported(const ClayRepairProgram &pg, std::string *why = nullptr);
+std::string clay_grp_source(const ClayRepairProgram &pg, const RtcShape &shape = RtcShape());
+// The source of the kernel the current tuning (ecx_tune "rtc_group", ...) selects.
+std::string clay_rtc_selected_source(const ClayRepairProgram &pg);
 
 class ClayRtc {
 public:
@@ -45,6 +56,9 @@ public:
     void prepare();
     // Enqueue the repair of `nchunks` whole 4 KiB chunks (bytes [0, nchunks * 4 KiB) of
     // every sub-chunk) over nstripes stripes, in the performCoding batch layout.
+    // The kernel the current tuning selects for this program: "k_clay_repair_grp" or
+    // "k_clay_repair".
+    const char *kernel_name() const;
     void launch(const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                 int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nchunks,
                 hipStream_t stream);

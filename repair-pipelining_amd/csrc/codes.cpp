@@ -463,6 +463,13 @@ ClayRepairProgram ClayPlanner::repair_program(int erased_index) const {
         if (column[r] == e) pg.e_row = r;
         else pg.mate_row.push_back(r);
     }
+    pg.t = t_;
+    pg.ex = nx(e);
+    pg.ey = ey;
+    pg.n_real = nr;
+    pg.noncol = noncol;
+    pg.column = column;
+    for (int u = 0; u < q_ * t_; ++u) pg.real_of.push_back(is_virtual(u) ? -1 : (u < k_ - v_ ? u : u - v_));
     // real slot of (plane z, underlying node u), -1 for a virtual node
     auto slot = [&](int z, int u) -> int {
         if (is_virtual(u)) return -1;

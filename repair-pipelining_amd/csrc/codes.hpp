@@ -96,6 +96,13 @@ struct ClayRepairProgram {
     std::vector<uint8_t> dmat;     // q x n_noncol
     std::vector<int32_t> table;    // n_planes x stride
     int max_in_slot = -1, max_out_slot = -1;
+    // Grid geometry, for the plane-group kernel (clay_rtc.cpp), which derives slots from
+    // the plane digits instead of `table`: node u = x + q*y of the q x t grid, plane
+    // z = sum_y zvec[y] * q^(t-1-y), the erased node at (ex, ey), `real_of[u]` the real
+    // slot index of underlying node u (-1 = virtual), `noncol[jj]` the node of column jj
+    // of dmat, `column[r]` the node of dmat row r.
+    int t = 0, ex = 0, ey = 0, n_real = 0;
+    std::vector<int> real_of, noncol, column;
     // The program composed into a dense map over (out slot, in slot); tests compare it
     // with perform_coding_map (the reference's stage sequence).
     LinearMap compose(int n_in_slots, int n_out_slots) const;

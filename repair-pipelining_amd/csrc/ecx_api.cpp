@@ -752,7 +752,7 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
         if (done < buf_size)
             launch_apply(m->cm, in + done, in_stripe_stride, in_sub_stride, out + done, out_stripe_stride,
                          out_sub_stride, nstripes, buf_size - done, (hipStream_t)stream);
-        if (done > 0) set_last_kernel("k_clay_repair");
+        if (done > 0) set_last_kernel(clay_rtc(clay)->kernel_name());
         return ECX_OK;
     });
 }
@@ -761,7 +761,7 @@ int ecx_clay_rtc_compile_check(ecx_clay *clay) {
     return guarded([&]() -> int {
         ClayRtc *r = clay_rtc(clay);
         if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
-        return (int)rtc_compile_check(clay_rtc_source(r->program()));
+        return (int)rtc_compile_check(clay_rtc_selected_source(r->program()));
     });
 }
 
@@ -769,7 +769,7 @@ int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
     return guarded([&]() -> int {
         ClayRtc *r = clay_rtc(clay);
         if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
-        const std::string src = clay_rtc_source(r->program());
+        const std::string src = clay_rtc_selected_source(r->program());
         if (buf && len > (int)src.size()) std::memcpy(buf, src.c_str(), src.size() + 1);
         return (int)src.size();
     });
@@ -956,6 +956,11 @@ int ecx_tune(const char *key, int value) {
         t.rtc_lookahead = value;
     }
     else if (k == "rtc_xcd") t.rtc_xcd = value != 0;
+    else if (k == "rtc_group") t.rtc_group = value != 0;
+    else if (k == "rtc_persist") {
+        if (value < 0 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_persist = value;
+    }
     else if (k == "rtc_waves") {
         if (value < 2 || value > 4) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_waves = value;

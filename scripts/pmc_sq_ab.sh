@@ -9,7 +9,9 @@ cd /tmp
 WL="${WL:-clay104}"
 case $WL in clay42) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; lrc) POOL=32768 ;; esac
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA"
-      "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE")
+      "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
+      "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
+      "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS")
 for TAG in A B; do
   TUNE="${!TAG}"
   i=0

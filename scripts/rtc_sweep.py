@@ -1,5 +1,6 @@
 """Sweep the generated per-helper-plane Clay kernel's code shape (ecx_tune
-"rtc_lookahead" x "rtc_waves" x "rtc_xcd") on BASELINE config 4 (shortened Clay(10,4), 1 MiB node
+"rtc_lookahead" x "rtc_waves" x "rtc_xcd", and the plane-group kernel "rtc_group" 1 x
+"rtc_waves" x "rtc_xcd") on BASELINE config 4 (shortened Clay(10,4), 1 MiB node
 blocks = 256 x 4 KiB sub-chunks, repair of node 3) in one process: one resident pool,
 every shape verified against the composed-map kernel, interleaved rounds, median
 per-launch time -> algorithmic GB/s and fraction of the 8 TB/s HBM peak.
@@ -23,6 +24,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--erased", type=int, default=3)
+    ap.add_argument("--grp", default=None, help="plane-group shapes as la:waves:persist,... (XCD-local order)")
+    ap.add_argument("--group-only", action="store_true", help="composed, the default per-plane shape and the "
+                    "plane-group kernel shapes only")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
@@ -37,7 +41,17 @@ def main():
     ecx.tune("clay_rtc", 0)
     step.performCodingBatch(pool, n * a * b, b, ref, a * b, b, P, b)
     torch.cuda.synchronize()
-    shapes = [("composed", None, None, 0)] + [("rtc", la, w, x) for x in (0, 1) for w in (2, 3) for la in (0, 1, 2)]
+    shapes = [("composed", None, None, 0)]
+    if args.group_only:
+        shapes += [("rtc", 1, 3, 1)]
+    else:
+        shapes += [("rtc", la, w, x) for x in (0, 1) for w in (2, 3) for la in (0, 1, 2)]
+    if args.grp:
+        shapes += [("grp", int(a), int(b), 1, int(c)) for a, b, c in (t.split(":") for t in args.grp.split(","))]
+    elif args.group_only:
+        shapes += [("grp", la, w, 1) for la in (0, 1, 2, 3) for w in (2, 3)]
+    else:
+        shapes += [("grp", la, w, x) for x in (0, 1) for w in (2, 3) for la in (0, 1, 2, 3)]
     out = torch.empty_like(ref)
     times = {s: [] for s in shapes}
     for _ in range(args.rounds):
@@ -46,14 +60,20 @@ def main():
                 ecx.tune("clay_rtc", 0)
             else:
                 ecx.tune("clay_rtc", 2)
-                ecx.tune("rtc_lookahead", s[1])
+                ecx.tune("rtc_group", 1 if s[0] == "grp" else 0)
+                ecx.tune("rtc_lookahead", s[1] if s[1] is not None else 1)
                 ecx.tune("rtc_waves", s[2])
                 ecx.tune("rtc_xcd", s[3])
+                ecx.tune("rtc_persist", s[4] if len(s) > 4 else 0)
             out.fill_(0)
             step.performCodingBatch(pool, n * a * b, b, out, a * b, b, P, b)
             torch.cuda.synchronize()
             if not torch.equal(out, ref):
                 raise SystemExit("shape %s differs from the composed kernel" % (s,))
+            if s[0] != "composed":
+                want = "k_clay_repair_grp" if s[0] == "grp" else "k_clay_repair"
+                if ecx.last_kernel() != want:
+                    raise SystemExit("shape %s ran %s" % (s, ecx.last_kernel()))
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
             for e0, e1 in evs:
                 e0.record()
@@ -65,12 +85,15 @@ def main():
         ms = statistics.median(times[s])
         gbs = P * unit / (ms * 1e-3) / 1e9
         print(json.dumps({"kernel": s[0], "rtc_lookahead": s[1], "rtc_waves": s[2], "rtc_xcd": s[3],
+                          "rtc_persist": s[4] if len(s) > 4 else 0,
                           "launch_ms": round(ms, 4),
                           "GBps": round(gbs, 1), "frac": round(gbs / 8000.0, 4)}), flush=True)
     ecx.tune("clay_rtc", 1)
     ecx.tune("rtc_lookahead", 1)
     ecx.tune("rtc_waves", 3)
     ecx.tune("rtc_xcd", 1)
+    ecx.tune("rtc_group", 1)
+    ecx.tune("rtc_persist", 0)
 
 
 if __name__ == "__main__":

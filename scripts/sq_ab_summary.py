@@ -29,6 +29,11 @@ def main(src=None, wl="clay104"):
                   "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_INST_CYCLES_SALU"):
             if k in d:
                 d[k + "_per_wave"] = d[k] / w
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d and "algorithmic_bytes_per_launch" in meta:
+            hbm = 2 * d["FETCH_SIZE"] * 1024 + d["WRITE_SIZE"] * 1024  # gfx950 FETCH_SIZE half-count
+            d["hbm_over_algorithmic"] = hbm / meta["algorithmic_bytes_per_launch"]
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
         out[tag] = d
     print(json.dumps(out, indent=1))
     return out

@@ -1125,7 +1125,8 @@ def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
 
 @pytest.mark.parametrize("k,m,v,e,B,S", [(4, 2, 0, 1, 4096 * 2 + 112, 3), (4, 2, 0, 4, 4096, 9), (4, 2, 0, 0, 8192, 3),
                                          (10, 4, 2, 3, 4096, 3), (10, 4, 2, 13, 4096 + 16, 3), (10, 4, 2, 9, 4096, 17),
-                                         (12, 4, 0, 5, 4096, 3), (6, 3, 0, 2, 4096 * 2, 5), (2, 2, 0, 3, 4096, 3)])
+                                         (12, 4, 0, 5, 4096, 3), (12, 4, 0, 15, 8192 + 512, 5), (8, 4, 0, 0, 4096, 3),
+                                         (6, 3, 0, 2, 4096 * 2, 5), (2, 2, 0, 3, 4096, 3)])
 def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S):
     """The per-helper-plane repair kernel (clay_rtc.hpp: generated for the repair
     program and compiled with hiprtc) over whole 4 KiB chunks, the composed-map kernel
@@ -1136,26 +1137,38 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
     n, a = k + m, step.subPacketSize
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 41 + e)
+    modes = [(0, 0, 0, 0), (2, 0, 0, 0), (2, 1, 0, 0)]  # composed; per-plane kernel, plane-fastest / XCD-local order
+    if m == 4:
+        # the plane-group kernel, both block orders, and its persistent grid
+        modes += [(2, 0, 1, 0), (2, 1, 1, 0), (2, 1, 1, 2)]
     outs = {}
     try:
-        for rtc, xcd in ((0, 0), (2, 0), (2, 1)):  # composed; per-plane kernel, plane-fastest / XCD-local order
+        for rtc, xcd, grp, persist in modes:
             ecx.tune("clay_rtc", rtc)
             ecx.tune("rtc_xcd", xcd)
+            ecx.tune("rtc_group", grp)
+            ecx.tune("rtc_persist", persist)
             o = torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
             torch.cuda.synchronize()
-            outs[rtc + xcd] = (o.cpu().numpy(), ecx.last_kernel())
+            outs[(rtc, xcd, grp, persist)] = (o.cpu().numpy(), ecx.last_kernel())
     finally:
         ecx.tune("clay_rtc", 1)
         ecx.tune("rtc_xcd", 1)
-    assert outs[2][1] == "k_clay_repair" and outs[3][1] == "k_clay_repair", outs[2][1]
-    assert (outs[0][0] == outs[2][0]).all() and (outs[0][0] == outs[3][0]).all()
+        ecx.tune("rtc_group", 1)
+        ecx.tune("rtc_persist", 0)
+    ref0 = outs[(0, 0, 0, 0)][0]
+    for mode in modes[1:]:
+        want = "k_clay_repair_grp" if mode[2] else "k_clay_repair"
+        assert outs[mode][1] == want, (mode, outs[mode][1])
+        assert (outs[mode][0] == ref0).all(), mode
     if v == 0:
         host = pool[S - 1].cpu().numpy()
         inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
         ref = [np.zeros(B, np.uint8) for _ in range(a)]
         O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
-        assert all((outs[2][0][S - 1, z] == ref[z]).all() for z in range(a))
+        assert all((ref0[S - 1, z] == ref[z]).all() for z in range(a))
+        assert all((outs[modes[-1]][0][S - 1, z] == ref[z]).all() for z in range(a))
 
 
 def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):
@@ -1173,15 +1186,17 @@ def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):
         ecx.fill_random(buf[s * pitch:s * pitch + used], used, 90 + s)
     outs = []
     try:
-        for rtc in (0, 2):
+        for rtc, grp in ((0, 0), (2, 0), (2, 1)):
             ecx.tune("clay_rtc", rtc)
+            ecx.tune("rtc_group", grp)
             o = torch.full((S, a, B), 0x33, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(buf, pitch, B, o, a * B, B, S, B)
             torch.cuda.synchronize()
             outs.append((o.cpu().numpy(), ecx.last_kernel()))
     finally:
         ecx.tune("clay_rtc", 1)
-    assert outs[1][1] == "k_clay_repair"
-    assert (outs[0][0] == outs[1][0]).all()
+        ecx.tune("rtc_group", 1)
+    assert outs[1][1] == "k_clay_repair" and outs[2][1] == "k_clay_repair_grp"
+    assert (outs[0][0] == outs[1][0]).all() and (outs[0][0] == outs[2][0]).all()
     del buf
     torch.cuda.empty_cache()

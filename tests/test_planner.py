@@ -278,17 +278,29 @@ def test_compiled_plan_selftest_random_maps(ecx):
     check()
 
 
-@pytest.mark.parametrize("k,m,v,e", [(4, 2, 0, 1), (4, 2, 0, 5), (10, 4, 2, 3), (10, 4, 2, 13), (12, 4, 0, 0),
-                                     (6, 3, 0, 7), (2, 2, 0, 0)])
+@pytest.mark.parametrize("k,m,v,e", [(4, 2, 0, 1), (4, 2, 0, 5), (10, 4, 2, 3), (10, 4, 2, 13), (10, 4, 2, 9),
+                                     (12, 4, 0, 0), (8, 4, 0, 11), (6, 3, 0, 7), (2, 2, 0, 0)])
 def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
     """The single-node repair as a per-helper-plane program (ClayPlanner::repair_program:
     decouple with the dot identity pair_a ^ pair_b = 1, plane decode, re-couple) composes
-    to exactly the reference stage sequence's map (checked inside the builder), and its
-    generated kernel compiles with hiprtc for gfx950 without a device."""
+    to exactly the reference stage sequence's map (checked inside the builder), and both
+    generated kernels compile with hiprtc for gfx950 without a device: the plane-group
+    kernel for q = 4 codes (the default, ecx_tune "rtc_group" 1), the one-plane-per-
+    workgroup kernel for every code."""
     step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
-    assert step.rtcCompileCheck() > 0
-    src = step.rtcSource()
-    assert "k_clay_repair" in src and "__launch_bounds__" in src
+    try:
+        for grp, persist in ((1, 0), (1, 2), (0, 0)):
+            ecx.tune("rtc_group", grp)
+            ecx.tune("rtc_persist", persist)
+            assert step.rtcCompileCheck() > 0
+            src = step.rtcSource()
+            name = "k_clay_repair_grp(" if grp and m == 4 else "k_clay_repair("
+            assert name in src and "__launch_bounds__" in src
+            if name == "k_clay_repair_grp(":
+                assert ("for (u32 b = blockIdx.x; b < n_units" in src) == (persist > 0)
+    finally:
+        ecx.tune("rtc_group", 1)
+        ecx.tune("rtc_persist", 0)
 
 
 def test_clay_rtc_refuses_multi_erasure(ecx):
