@@ -49,9 +49,10 @@
  *                      several 8-row tiles (alpha > 8: Clay(10,4), Clay(12,4); default), 2 = always,
  *                      0 = never (the composed-map kernel only)
  *   "rtc_lookahead"    that kernel's generated load schedule: items (non-column nodes, mates) whose
- *                      loads are issued ahead of the one being computed, 0..3 (default 1); for the
- *                      plane-group kernel bit 0 = partner and mate loads after row ya, bit 1 = skip
- *                      the dot's and virtual partners' transposes by uniform branches
+ *                      loads are issued ahead of the one being computed, 0..3 (bits 0-1; default 1);
+ *                      for the plane-group kernel bit 0 = partner and mate loads after row ya, bit 1
+ *                      = skip the dot's and virtual partners' transposes by uniform branches, bit 2
+ *                      = a second body for plane groups whose memory-row partner is virtual
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes

@@ -140,7 +140,7 @@ def test_tuning_keys(ecx):
     for key, val in defaults.items():
         assert tune(key.encode(), val) == 0, key
     assert tune(b"no_such_knob", 1) == -1
-    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("plan_cache", -1), ("bitslice", 3), ("clay_rtc", 3), ("rtc_lookahead", 4), ("rtc_waves", 1), ("rtc_persist", 9)):
+    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("plan_cache", -1), ("bitslice", 3), ("clay_rtc", 3), ("rtc_lookahead", 8), ("rtc_waves", 1), ("rtc_persist", 9)):
         assert tune(key.encode(), bad) == -1, key
     for key, val in defaults.items():  # restore
         tune(key.encode(), val)

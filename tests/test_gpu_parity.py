@@ -1137,27 +1137,31 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
     n, a = k + m, step.subPacketSize
     pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 41 + e)
-    modes = [(0, 0, 0, 0), (2, 0, 0, 0), (2, 1, 0, 0)]  # composed; per-plane kernel, plane-fastest / XCD-local order
+    # (clay_rtc, rtc_xcd, rtc_group, rtc_persist, rtc_lookahead)
+    modes = [(0, 0, 0, 0, 1), (2, 0, 0, 0, 1), (2, 1, 0, 0, 1)]  # composed; per-plane, both block orders
     if m == 4:
-        # the plane-group kernel, both block orders, and its persistent grid
-        modes += [(2, 0, 1, 0), (2, 1, 1, 0), (2, 1, 1, 2)]
+        # the plane-group kernel: both block orders, persistent grid, every schedule bit
+        modes += [(2, 0, 1, 0, 1), (2, 1, 1, 0, 1), (2, 1, 1, 2, 1), (2, 1, 1, 0, 0), (2, 1, 1, 0, 3),
+                  (2, 1, 1, 0, 5), (2, 1, 1, 0, 6)]
     outs = {}
     try:
-        for rtc, xcd, grp, persist in modes:
+        for rtc, xcd, grp, persist, la in modes:
             ecx.tune("clay_rtc", rtc)
             ecx.tune("rtc_xcd", xcd)
             ecx.tune("rtc_group", grp)
             ecx.tune("rtc_persist", persist)
+            ecx.tune("rtc_lookahead", la)
             o = torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
             torch.cuda.synchronize()
-            outs[(rtc, xcd, grp, persist)] = (o.cpu().numpy(), ecx.last_kernel())
+            outs[(rtc, xcd, grp, persist, la)] = (o.cpu().numpy(), ecx.last_kernel())
     finally:
         ecx.tune("clay_rtc", 1)
         ecx.tune("rtc_xcd", 1)
         ecx.tune("rtc_group", 1)
         ecx.tune("rtc_persist", 0)
-    ref0 = outs[(0, 0, 0, 0)][0]
+        ecx.tune("rtc_lookahead", 1)
+    ref0 = outs[(0, 0, 0, 0, 1)][0]
     for mode in modes[1:]:
         want = "k_clay_repair_grp" if mode[2] else "k_clay_repair"
         assert outs[mode][1] == want, (mode, outs[mode][1])
