@@ -52,7 +52,8 @@
  *                      loads are issued ahead of the one being computed, 0..3 (bits 0-1; default 1);
  *                      for the plane-group kernel bit 0 = partner and mate loads after row ya, bit 1
  *                      = skip the dot's and virtual partners' transposes by uniform branches, bit 2
- *                      = a second body for plane groups whose memory-row partner is virtual
+ *                      = a second body for plane groups whose memory-row partner is virtual, bit 3 =
+ *                      every load issued at the start
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes
@@ -61,7 +62,10 @@
  *   "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
  *                      a persistent grid of that many workgroups per CU walking the units
  *   "rtc_xcd"          that kernel's block order: 1 = the helper planes of one (stripe, chunk) on one
- *                      XCD (their shared partner loads meet in its L2; default), 0 = plane-fastest
+ *                      XCD (their shared partner loads meet in its L2), 0 = plane-fastest; 2 = the
+ *                      same, and for the plane-group kernel all slices and plane groups of one
+ *                      (stripe, chunk) on one XCD, plane-group-fastest (default); 3 = the same, slice-fastest; 4 = as 3
+ *                      with a contiguous range of (stripe, chunk) units per XCD
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -952,10 +952,13 @@ int ecx_tune(const char *key, int value) {
         t.clay_rtc = value;
     }
     else if (k == "rtc_lookahead") {
-        if (value < 0 || value > 7) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value < 0 || value > 15) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_lookahead = value;
     }
-    else if (k == "rtc_xcd") t.rtc_xcd = value != 0;
+    else if (k == "rtc_xcd") {
+        if (value < 0 || value > 4) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_xcd = value;
+    }
     else if (k == "rtc_group") t.rtc_group = value != 0;
     else if (k == "rtc_persist") {
         if (value < 0 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;

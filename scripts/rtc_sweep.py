@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--erased", type=int, default=3)
-    ap.add_argument("--grp", default=None, help="plane-group shapes as la:waves:persist,... (XCD-local order)")
+    ap.add_argument("--grp", default=None, help="plane-group shapes as la:waves:persist[:xcd],... (default XCD order 2)")
     ap.add_argument("--group-only", action="store_true", help="composed, the default per-plane shape and the "
                     "plane-group kernel shapes only")
     args = ap.parse_args()
@@ -47,7 +47,9 @@ def main():
     else:
         shapes += [("rtc", la, w, x) for x in (0, 1) for w in (2, 3) for la in (0, 1, 2)]
     if args.grp:
-        shapes += [("grp", int(a), int(b), 1, int(c)) for a, b, c in (t.split(":") for t in args.grp.split(","))]
+        for t in args.grp.split(","):
+            f = [int(v) for v in t.split(":")]
+            shapes.append(("grp", f[0], f[1], f[3] if len(f) > 3 else 2, f[2]))
     elif args.group_only:
         shapes += [("grp", la, w, 1) for la in (0, 1, 2, 3) for w in (2, 3)]
     else:
@@ -91,7 +93,7 @@ def main():
     ecx.tune("clay_rtc", 1)
     ecx.tune("rtc_lookahead", 1)
     ecx.tune("rtc_waves", 3)
-    ecx.tune("rtc_xcd", 1)
+    ecx.tune("rtc_xcd", 2)
     ecx.tune("rtc_group", 1)
     ecx.tune("rtc_persist", 0)
 

@@ -1141,8 +1141,8 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
     modes = [(0, 0, 0, 0, 1), (2, 0, 0, 0, 1), (2, 1, 0, 0, 1)]  # composed; per-plane, both block orders
     if m == 4:
         # the plane-group kernel: both block orders, persistent grid, every schedule bit
-        modes += [(2, 0, 1, 0, 1), (2, 1, 1, 0, 1), (2, 1, 1, 2, 1), (2, 1, 1, 0, 0), (2, 1, 1, 0, 3),
-                  (2, 1, 1, 0, 5), (2, 1, 1, 0, 6)]
+        modes += [(2, 0, 1, 0, 1), (2, 1, 1, 0, 1), (2, 2, 1, 0, 1), (2, 3, 1, 0, 1), (2, 4, 1, 0, 1), (2, 1, 1, 2, 1), (2, 1, 1, 0, 0),
+                  (2, 1, 1, 0, 3), (2, 1, 1, 0, 5), (2, 1, 1, 0, 6), (2, 1, 1, 0, 12)]
     outs = {}
     try:
         for rtc, xcd, grp, persist, la in modes:
@@ -1157,7 +1157,7 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
             outs[(rtc, xcd, grp, persist, la)] = (o.cpu().numpy(), ecx.last_kernel())
     finally:
         ecx.tune("clay_rtc", 1)
-        ecx.tune("rtc_xcd", 1)
+        ecx.tune("rtc_xcd", 2)
         ecx.tune("rtc_group", 1)
         ecx.tune("rtc_persist", 0)
         ecx.tune("rtc_lookahead", 1)
