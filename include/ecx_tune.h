@@ -12,7 +12,9 @@
  *                      non-temporal loads for single-tile maps (no input re-read); 2 = always
  *   "xcd_group"        multi-tile maps: 0 = identity block order; 1 = each XCD runs a contiguous
  *                      eighth of the grid; 2 = each XCD runs whole (stripe, chunk) units, all
- *                      tiles of a unit back to back (default: see engine.hpp Tuning)
+ *                      tiles of a unit back to back (default: see engine.hpp Tuning); 3 = (any
+ *                      map) each XCD runs runs of "xcd_run" consecutive units
+ *   "xcd_run"          xcd_group 3: consecutive (stripe, chunk) units per XCD run, 1..4096 (default 8)
  *   "wave_groups"      multi-tile maps: one workgroup per group of tiles sharing inputs, one
  *                      wave per tile, 1 KiB chunks: 1 = the group's input union staged once
  *                      through LDS; 2 = each wave loads its own entries (no LDS, no barriers);

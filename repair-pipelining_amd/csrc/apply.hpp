@@ -146,7 +146,9 @@ __device__ __forceinline__ void apply_entry(cu32 *r, const u32x4 x, u32x4 (&acc)
 //                back to back, so a unit's re-reads meet in one XCD's L2 while
 //                all XCDs stream neighbouring units.  Units past the last full
 //                group of 8 keep the identity mapping.
-__device__ __forceinline__ uint32_t logical_block(int xcd_group, uint32_t n_tiles) {
+//   xcd_group 3: as 2 with runs of `run` consecutive units (all their tiles) per XCD,
+//                for any map (single-tile maps: `run` neighbouring chunks per XCD).
+__device__ __forceinline__ uint32_t logical_block(int xcd_group, uint32_t n_tiles, uint32_t run) {
     const uint32_t b = blockIdx.x;
     if (xcd_group == 0) return b;
     const uint32_t g = gridDim.x, xcd = b % 8, j = b / 8;
@@ -154,9 +156,10 @@ __device__ __forceinline__ uint32_t logical_block(int xcd_group, uint32_t n_tile
         const uint32_t q = g / 8, r = g % 8;
         return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
-    const uint32_t full = (g / (8 * n_tiles)) * (8 * n_tiles);
+    const uint32_t R = xcd_group == 3 ? run * n_tiles : n_tiles;
+    const uint32_t full = (g / (8 * R)) * (8 * R);
     if (b >= full) return b;
-    return ((j / n_tiles) * 8 + xcd) * n_tiles + (j % n_tiles);
+    return ((j / R) * 8 + xcd) * R + (j % R);
 }
 
 // One output tile over the workgroup's (or wave's) lanes x 16 bytes of one stripe.
@@ -273,7 +276,7 @@ __global__ void __launch_bounds__(THREADS, ROWS < kTileRows ? (DEPTH >= 12 ? 5 :
                                                             : (DEPTH == 2 ? 8 : (DEPTH == 4 ? 6 : (DEPTH <= 8 ? 5 : (DEPTH <= 12 ? 4 : 3)))))
     k_gf_apply(ApplyArgs a) {
     extern __shared__ uint2 lds_tab[];
-    const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles);
+    const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles, (uint32_t)a.xcd_run);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
     // chunk_major: consecutive units take the same chunk of consecutive stripes

@@ -908,8 +908,12 @@ int ecx_tune(const char *key, int value) {
         t.nontemporal = value;
     }
     else if (k == "xcd_group") {
-        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value < 0 || value > 3) return ECX_E_ILLEGAL_ARGUMENT;
         t.xcd_group = value;
+    }
+    else if (k == "xcd_run") {
+        if (value < 1 || value > 4096) return ECX_E_ILLEGAL_ARGUMENT;
+        t.xcd_run = value;
     }
     else if (k == "wave_groups") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;

@@ -170,6 +170,7 @@ struct ApplyArgs {
     int n_wide;           // k_gf_apply_wide: wide tiles (workgroups per chunk)
     int n_groups;         // k_gf_apply_lds: tile groups (workgroups per chunk)
     int xcd_group;        // k_gf_apply: keep the tiles of one chunk on one XCD
+    int xcd_run;          // k_gf_apply, xcd_group 3: units (stripe, chunk) per XCD run
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
     int lane_zero;        // always 0 (keeps k_gf_apply's LDS table base in a VGPR)
     int chunk_major;      // k_gf_apply block order: 0 = stripe by stripe, 1 = chunk c of every stripe, then c + 1
@@ -181,6 +182,7 @@ struct Tuning {
     int depth = 0;            // k_gf_apply load ring depth: 0 = per map (preferred_depth), or forced
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
+    int xcd_run = 8;          // xcd_group 3 (any map): runs of this many consecutive units per XCD
     // Multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS), 2 =
     // k_gf_apply_grp (tile groups in one workgroup, direct loads).  Off by
     // default: Clay(10,4)'s 64-row groups still need 1.23x the unique inputs and the

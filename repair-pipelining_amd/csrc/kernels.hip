@@ -327,7 +327,8 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.out_slot_stride = out_slot_stride;
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
-    a.xcd_group = a.n_tiles > 1 ? tu.xcd_group : 0;
+    a.xcd_group = (a.n_tiles > 1 || tu.xcd_group == 3) ? tu.xcd_group : 0;
+    a.xcd_run = tu.xcd_run;
     a.accumulate = accumulate ? 1 : 0;
 
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {

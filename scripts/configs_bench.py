@@ -99,18 +99,55 @@ def cases(ecx, torch):
     return out
 
 
+def knob_variants(args, ecx, torch, cs):
+    """A/B/... of ecx_tune knob sets, interleaved: every round runs every variant over
+    every case.  Each variant sets only the knobs it names, so name every knob that
+    another variant changes (e.g. 'xcd_group=0;xcd_group=3,xcd_run=8')."""
+    variants = [dict(kv.split("=") for kv in v.split(",") if kv) for v in args.knobs.split(";")]
+    times = {(vi, i): [] for vi in range(len(variants)) for i in range(len(cs))}
+    for _ in range(args.rounds):
+        for vi, v in enumerate(variants):
+            for k, val in v.items():
+                ecx.tune(k, int(val))
+            for i, (_name, _ub, _u, fn, _x, _keep) in enumerate(cs):
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                times[(vi, i)].append(e0.elapsed_time(e1) / args.reps * 1e-3)
+    for vi, v in enumerate(variants):
+        for i, (name, unit_bytes, units, _fn, extra, _keep) in enumerate(cs):
+            sec = statistics.median(times[(vi, i)])
+            gbs = unit_bytes * units / sec / 1e9
+            d = {"config": name, "knobs": v, "ms_per_launch": round(sec * 1e3, 3), "GBps": round(gbs, 1),
+                 "frac_of_peak": round(gbs / PEAK, 4), "rounds": args.rounds, "reps": args.reps}
+            d.update(extra)
+            print(json.dumps(d), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--sweep", action="store_true", help="also the non-default launch shapes of SWEEP")
     ap.add_argument("--depths", default=None, help="comma list of ring depths to sweep (nt 1), e.g. 0,8,12,20")
+    ap.add_argument("--knobs", default=None, help="variants of ecx_tune knobs, interleaved inside every round: "
+                    "'k=v,k=v;k=v' (';' separates variants, '' = defaults)")
+    ap.add_argument("--only", default=None, help="substring filter on the config names")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
     lib = ecx.lib()
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
     cs = cases(ecx, torch)
+    if args.only:
+        cs = [c for c in cs if any(o in c[0] for o in args.only.split("|"))]
+    if args.knobs is not None:
+        return knob_variants(args, ecx, torch, cs)
     shapes = SWEEP if args.sweep else SWEEP[:1]
     if args.depths:
         shapes = [(int(d), 1) for d in args.depths.split(",")]
