@@ -137,6 +137,8 @@ def test_tuning_keys(ecx):
                 "chunk_major": 0, "block_threads": 256, "small_tiles": 0, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "plan_cache": 256, "bitslice": 0, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_persist": 0, "xcd_run": 8,
                 "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 256}
     assert sorted(documented) == sorted(defaults)
+    integration = (ROOT / "INTEGRATION.md").read_text()
+    assert all("`%s`" % k in integration for k in documented), "INTEGRATION.md must list every tuning key"
     for key, val in defaults.items():
         assert tune(key.encode(), val) == 0, key
     assert tune(b"no_such_knob", 1) == -1
