@@ -26,8 +26,9 @@
  *                      (system scope: written through, dropped from L2)
  *   "chunk_major"      block order of the one-workgroup-per-tile kernel: 0 = stripe-major
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
- *   "block_threads"    one-workgroup-per-tile kernel: 256 threads over 4 KiB chunks (default)
- *                      or 64 threads (one wave) over 1 KiB chunks
+ *   "block_threads"    one-workgroup-per-tile kernel: 256 threads over 4 KiB chunks or 64 threads
+ *                      (one wave) over 1 KiB chunks; 0 = auto (default): one wave for single-tile
+ *                      maps of <= 2 rows over >= 8 inputs on slot pitches that are not 4 MiB multiples
  *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
  *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel (default)
  *   "plan_cache"       per-call entry points that receive or derive their coefficients per call

@@ -936,7 +936,7 @@ int ecx_tune(const char *key, int value) {
         t.wide_tiles = value;
     }
     else if (k == "block_threads") {
-        if (value != 64 && value != 256) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value != 0 && value != 64 && value != 256) return ECX_E_ILLEGAL_ARGUMENT;
         t.block_threads = value;
     }
     else if (k == "lds_tables") {

@@ -199,7 +199,7 @@ struct Tuning {
     int chunk_major = 0;
     // k_gf_apply workgroup: 256 threads over 4 KiB chunks (default) or 64 threads (one
     // wave) over 1 KiB chunks.
-    int block_threads = kBlockThreads;
+    int block_threads = 0;  // 0 = auto (launch_apply), 256 or 64 forced
     // Single-tile maps of at most 2 / 4 rows: 1 = k_gf_apply variants with that many
     // accumulator rows (fewer VGPRs, depth-12 rings possible); 0 = the 8-row kernel.
     int small_tiles = 0;

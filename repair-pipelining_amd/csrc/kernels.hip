@@ -245,7 +245,15 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (cm.n_tiles() == 1 ? 2 : 1) : 0);
     const int nts = ntmode == 0 ? 0 : (tu.store_scope ? 2 : 1);
     // Launch shapes that exist (apply_launch.inc); anything else is clamped here.
-    int threads = tu.block_threads == 64 && nts == 1 ? 64 : kBlockThreads;
+    // Workgroup size: 256 threads over 4 KiB chunks; one wave over 1 KiB chunks when forced
+    // (64) or, in auto (0), for single-tile maps of <= 2 rows over >= 8 inputs whose slot
+    // pitch is not a 4 MiB multiple (RS(12,4) decode on its padded pitch: +2.4-2.8 %; every
+    // other BASELINE map is 3-8 % slower on one wave, profiles/r02_block_threads.jsonl).
+    const bool skew_pitch = in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4;
+    const bool one_wave = tu.block_threads == 64 ||
+                          (tu.block_threads == 0 && cm.n_tiles() == 1 && cm.max_tile_rows() <= 2 &&
+                           cm.map().n_in >= 8 && !skew_pitch);
+    int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     if (tu.small_tiles && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1)
         rows = cm.max_tile_rows() <= 2 ? 2 : (cm.max_tile_rows() <= 4 ? 4 : kTileRows);
@@ -276,7 +284,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // same-offset streams collide in HBM, where rotation recovers +10-17 %; on other
     // pitches it helps or costs by layout (profiles/r01_pitch_sweep.jsonl).  Auto needs
     // at least 4 input streams: one helper's partial sum (1 input) only loses.
-    const bool skew_auto = in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4;
+    const bool skew_auto = skew_pitch;
     int skew = tu.skew_chunks == 1 ? (skew_auto ? 4 : 0) : tu.skew_chunks;
     const int skew_rows = cm.max_tile_rows() <= 2 ? 2 : (cm.max_tile_rows() <= 4 ? 4 : kTileRows);
     if (skew == 4 && skew_rows == kTileRows) skew = 2;  // 8 rows x 4 chunks would not fit the VGPRs

@@ -103,7 +103,7 @@ def main():
                 lib.ecx_tune(k.encode(), {"xcd_group": 0, "chunk_major": 0}.get(k, 0))
     lib.ecx_tune(b"depth", 0)
     lib.ecx_tune(b"nontemporal", 1)
-    lib.ecx_tune(b"block_threads", 256)
+    lib.ecx_tune(b"block_threads", 0)
     lib.ecx_tune(b"store_scope", 0)
     for name, *_ in variants:
         v = res[name]

@@ -442,6 +442,39 @@ def test_rs124_two_erasure_batch_roundtrip(ecx, torch_dev):
     assert all((b[i] == host[i]).all() for i in range(12, 16))
 
 
+@pytest.mark.parametrize("L", [(1 << 20) + 1000, 4 << 20])
+def test_rs124_padded_pitch_one_wave_auto(ecx, torch_dev, L):
+    """RS(12,4) decode on a padded shard pitch (4 MiB + 4 KiB style) runs on one-wave
+    workgroups under the auto workgroup size (ecx_tune "block_threads" 0): same bytes as
+    the 256-thread kernel, ragged tail included, and the non-codeword decode equals the
+    oracle's decodeMissing on a sampled window."""
+    torch = torch_dev
+    k, m, S = 12, 4, 3
+    P = L + 4096
+    rs = ecx.ReedSolomon.create(k, m)
+    pool = torch.empty((S, 16, P), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 19)
+    present = [False, False] + [True] * 14
+    outs = []
+    try:
+        for bt in (0, 256):
+            ecx.tune("block_threads", bt)
+            o = pool.clone()
+            rs.decode_map(present).apply_batch(o, 16 * P, P, o, 16 * P, P, S, L)
+            torch.cuda.synchronize()
+            outs.append((o, ecx.last_kernel()))
+    finally:
+        ecx.tune("block_threads", 0)
+    assert ", 64, " in outs[0][1] and ", 256, " in outs[1][1], (outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], outs[1][0])
+    w0 = L - 5000  # a window that ends in the ragged tail
+    host = pool[1, :, w0:L].cpu().numpy()
+    b = [host[i].copy() for i in range(16)]
+    O.ReedSolomon(k, m).decode_missing(b, present, 0, L - w0)
+    got = outs[0][0][1, :, w0:L].cpu().numpy()
+    assert all((b[i] == got[i]).all() for i in range(16))
+
+
 def test_lrc_batch_config3(ecx, torch_dev):
     """BASELINE config 3 shape: LRC (12 data, 4 XOR groups), 64 KiB blocks, repair block 2."""
     torch = torch_dev
@@ -645,7 +678,7 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     ecx.tune("lds_tables", 1)
     ecx.tune("store_scope", 0)
     ecx.tune("chunk_major", 0)
-    ecx.tune("block_threads", 256)
+    ecx.tune("block_threads", 0)
     ecx.tune("wide_tiles", 1)
     for o in outs[1:]:
         assert (o == outs[0]).all()
@@ -829,7 +862,7 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
                 assert (got[s, slot] == ref[s][o]).all(), (depth, lt, bt, wd, sk, s, o)
     ecx.tune("depth", 0)
     ecx.tune("lds_tables", 1)
-    ecx.tune("block_threads", 256)
+    ecx.tune("block_threads", 0)
     ecx.tune("wide_tiles", 1)
     ecx.tune("skew_chunks", 1)
     ecx.tune("bitslice", 0)
