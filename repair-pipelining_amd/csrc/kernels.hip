@@ -252,7 +252,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool skew_pitch = in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4;
     const bool one_wave = tu.block_threads == 64 ||
                           (tu.block_threads == 0 && cm.n_tiles() == 1 && cm.max_tile_rows() <= 2 &&
-                           cm.map().n_in >= 8 && !skew_pitch);
+                           cm.map().n_in >= 8 && !skew_pitch && tu.bitslice != 2);
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     if (tu.small_tiles && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1)
