@@ -30,7 +30,8 @@
  *                      (one wave) over 1 KiB chunks; 0 = auto (default): one wave for single-tile
  *                      maps of <= 2 rows over >= 8 inputs on slot pitches that are not 4 MiB multiples
  *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
- *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel (default)
+ *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel; 2 = auto (default):
+ *                      the small variant for maps of <= 2 rows over <= 4 inputs (LRC block repair)
  *   "plan_cache"       per-call entry points that receive or derive their coefficients per call
  *                      (ecx_code_some_shards, ecx_check_some_shards, ecx_code_single,
  *                      ecx_rs_encode_parity_single, ecx_rs_decode_missing_single): compiled plans

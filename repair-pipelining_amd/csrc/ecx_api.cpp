@@ -921,7 +921,10 @@ int ecx_tune(const char *key, int value) {
     }
     else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "chunk_major") t.chunk_major = value != 0;
-    else if (k == "small_tiles") t.small_tiles = value != 0;
+    else if (k == "small_tiles") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.small_tiles = value;
+    }
     else if (k == "host_zero_copy") t.host_zero_copy = value != 0;
     else if (k == "plan_cache") {
         if (value < 0 || value > 4096) return ECX_E_ILLEGAL_ARGUMENT;

@@ -202,7 +202,7 @@ struct Tuning {
     int block_threads = 0;  // 0 = auto (launch_apply), 256 or 64 forced
     // Single-tile maps of at most 2 / 4 rows: 1 = k_gf_apply variants with that many
     // accumulator rows (fewer VGPRs, depth-12 rings possible); 0 = the 8-row kernel.
-    int small_tiles = 0;
+    int small_tiles = 2;  // 2 = auto (launch_apply), 1 = forced, 0 = the 8-row kernel
     // Per-call host APIs on the gather path: 1 = the kernel reads / writes the pinned
     // staging area directly over PCIe instead of one H2D and one D2H copy (20-40 % lower
     // latency per call, profiles/r01_percall_native.jsonl).

@@ -255,7 +255,12 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                            cm.map().n_in >= 8 && !skew_pitch && tu.bitslice != 2);
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
-    if (tu.small_tiles && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1)
+    // Small-row kernel variants: forced (1), or auto (2) for maps of <= 2 rows over <= 4
+    // inputs (LRC block repair: +2.5-3 %; wider narrow maps gain nothing or lose,
+    // profiles/r02_small_tiles_ab.jsonl).
+    const bool small = tu.small_tiles == 1 ||
+                       (tu.small_tiles == 2 && cm.max_tile_rows() <= 2 && cm.map().n_in <= 4 && cm.n_tiles() == 1);
+    if (small && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1)
         rows = cm.max_tile_rows() <= 2 ? 2 : (cm.max_tile_rows() <= 4 ? 4 : kTileRows);
     int depth = tu.depth ? tu.depth : cm.preferred_depth();
     if (rows < kTileRows) {

@@ -65,7 +65,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[(name, label)].append(nbytes / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
-    ecx.tune("small_tiles", 0)
+    ecx.tune("small_tiles", 2)
     ecx.tune("depth", 0)
     for (name, label), v in res.items():
         med = statistics.median(v)

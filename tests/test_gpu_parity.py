@@ -926,7 +926,7 @@ def test_small_tile_variants(ecx, torch_dev, n_out):
         ecx.fill_random(inp, inp.numel(), n_in)
         host = inp.cpu().numpy()
         ref = [gf_apply_numpy(m, [host[s, j] for j in range(n_in)]) for s in range(S)]
-        for st, depth in ((0, 0), (1, 4), (1, 8), (1, 12), (1, 0)):
+        for st, depth in ((0, 0), (2, 0), (1, 4), (1, 8), (1, 12), (1, 0)):
             ecx.tune("small_tiles", st)
             ecx.tune("depth", depth)
             out = torch.full((S, n_out, L), 0xA5, dtype=torch.uint8, device="cuda")
@@ -936,8 +936,37 @@ def test_small_tile_variants(ecx, torch_dev, n_out):
             for s in range(S):
                 for o in range(n_out):
                     assert (got[s, o] == ref[s][o]).all(), (n_in, st, depth, s, o)
-    ecx.tune("small_tiles", 0)
+    ecx.tune("small_tiles", 2)
     ecx.tune("depth", 0)
+
+
+def test_small_tiles_auto_picks_lrc_repair(ecx, torch_dev):
+    """ecx_tune "small_tiles" 2 (auto): an LRC block repair (1 row over 3 inputs, 16-B
+    aligned layout) runs the 2-row kernel variant, a 4-row LRC encode the 8-row kernel,
+    and both give the forced-off kernel's bytes."""
+    torch = torch_dev
+    S, L = 4, 4096 * 2 + 96
+    inp = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(inp, inp.numel(), 12)
+    enc = np.zeros((4, 16), np.uint8)
+    for g in range(4):
+        enc[g, 4 * g:4 * g + 3] = 1
+    cases = [(ecx.GfMap.from_matrix(np.array([[1, 1, 1]], np.uint8), in_slot=[0, 1, 3], out_slot=[0]), 1, ", 2>"),
+             (ecx.GfMap.from_matrix(enc[:, :15], in_slot=list(range(15)), out_slot=[0, 1, 2, 3]), 4, ", 8>")]
+    try:
+        for gm, n_out, tail in cases:
+            outs = []
+            for st in (2, 0):
+                ecx.tune("small_tiles", st)
+                o = torch.zeros((S, n_out, L), dtype=torch.uint8, device="cuda")
+                gm.apply_batch(inp, 16 * L, L, o, n_out * L, L, S, L)
+                torch.cuda.synchronize()
+                outs.append((o, ecx.last_kernel()))
+            assert outs[0][1].endswith(tail), outs[0][1]
+            assert outs[1][1].endswith(", 8>"), outs[1][1]
+            assert torch.equal(outs[0][0], outs[1][0])
+    finally:
+        ecx.tune("small_tiles", 2)
 
 
 @pytest.mark.parametrize("nbytes", [8192 * 3 + 4096, 4096 * 9 + 100, 65536])
