@@ -210,18 +210,24 @@ def cpu_baseline(seconds: float, erased: int, sample=None):
     }
 
 
-# Sources that define what the device executes for a given map: the kernels, their
-# launch selection and the plan format / compiler.  Their hash is stored with every PMC
-# profile (profiles/pmc_traffic.json); a profile taken on other kernel code is stale.
-KERNEL_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
-                  "apply_skew.hip", "apply_bits.hip", "bits.hpp", "engine.hpp", "engine.cpp", "clay_rtc.hpp",
-                  "clay_rtc.cpp", "codes.cpp", "codes.hpp"]
+# Sources that define what the device executes for a given map, per kernel family: the
+# shared planner / plan compiler / launch selection, plus either the composed-map kernels
+# or the generated (hiprtc) Clay repair kernels.  Their hash is stored with every PMC
+# profile (profiles/pmc_traffic.json, one per workload); a profile taken on other code
+# for its kernel family is stale.
+COMMON_SOURCES = ["engine.hpp", "engine.cpp", "codes.cpp", "codes.hpp"]
+COMPOSED_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
+                    "apply_skew.hip", "apply_bits.hip", "bits.hpp"]
+RTC_SOURCES = ["clay_rtc.hpp", "clay_rtc.cpp"]
 
 
-def kernel_source_hash() -> str:
+def kernel_source_hash(kernel: str = "") -> str:
+    """Hash of the sources behind `kernel` (a k_clay_repair* label selects the generated
+    family, anything else the composed-map family)."""
     import hashlib
+    names = COMMON_SOURCES + (RTC_SOURCES if kernel.startswith("k_clay_repair") else COMPOSED_SOURCES)
     h = hashlib.sha256()
-    for name in KERNEL_SOURCES:
+    for name in names:
         h.update(name.encode() + b"\0" + (ROOT / "repair-pipelining_amd" / "csrc" / name).read_bytes())
     return h.hexdigest()[:16]
 
@@ -239,7 +245,7 @@ def pmc_traffic(workload: str, pool: int, kernel: str):
         w = d.get("workloads", {}).get(workload)
         if w is None:
             return None, "no PMC profile for this workload"
-        if d.get("kernel_source_hash") != kernel_source_hash():
+        if w.get("kernel_source_hash") != kernel_source_hash(kernel):
             return None, "stale: PMC profile taken on other kernel sources"
         if w.get("pool_stripes") != pool or w.get("kernel") != kernel:
             return None, "stale: PMC profile taken on another pool size or kernel instance"
@@ -540,7 +546,7 @@ def main():
         Path(args.meta).write_text(json.dumps({
             "workload": args.workload, "kernel": kernel, "pool_stripes": P, "unit_bytes": wl.unit_bytes,
             "write_bytes_per_unit": wl.write_bytes, "algorithmic_bytes_per_launch": per_launch_bytes,
-            "kernel_source_hash": kernel_source_hash(), "avg_launch_ms": launch_ms}) + "\n")
+            "kernel_source_hash": kernel_source_hash(kernel), "avg_launch_ms": launch_ms}) + "\n")
     if rank == 0:
         line = {
             "metric": WORKLOADS[args.workload][0],
@@ -570,7 +576,7 @@ def main():
                 "traffic": traffic,
                 "traffic_note": traffic_note,
                 "kernel": kernel,
-                "kernel_source_hash": kernel_source_hash(),
+                "kernel_source_hash": kernel_source_hash(kernel),
                 "avg_launch_ms": round(launch_ms, 4),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "measured_ceilings": probes,

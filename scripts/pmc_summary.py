@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 PMC passes of scripts/pmc.sh into
 profiles/pmc_traffic.json (read by bench.py as roofline.traffic, only while the
-kernel sources still hash to the recorded value) and a per-workload counter table.
+kernel family's sources still hash to the value recorded per workload) and a per-workload counter table.
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts
 exactly half the bytes of a wide (16 B/lane) coalesced streaming read, so
@@ -38,12 +38,14 @@ def counter(rows, name):
 
 def main(src=None, out_table="profiles/r02_pmc_workloads.json"):
     src = Path(src) if src else ROOT / "gpurun_out"
-    traffic, table, hashes = {}, {}, set()
+    old = ROOT / "profiles" / "pmc_traffic.json"
+    traffic = json.loads(old.read_text()).get("workloads", {}) if old.exists() else {}
+    old_t = ROOT / out_table
+    table = json.loads(old_t.read_text()).get("workloads", {}) if old_t.exists() else {}
     for meta_f in sorted(glob.glob(str(src / "pmc_*_0" / "meta.json"))):
         d0 = Path(meta_f).parent
         w = json.loads(Path(meta_f).read_text())
         name, kernel = w["workload"], w["kernel"]
-        hashes.add(w["kernel_source_hash"])
         base = str(d0)[:-2]
         fetch = counter(rows_for(Path(base + "_0"), kernel), "FETCH_SIZE")
         write = counter(rows_for(Path(base + "_1"), kernel), "WRITE_SIZE")
@@ -51,7 +53,7 @@ def main(src=None, out_table="profiles/r02_pmc_workloads.json"):
         algo = w["algorithmic_bytes_per_launch"]
         algo_wr = w["pool_stripes"] * w["write_bytes_per_unit"]
         traffic[name] = {
-            "kernel": kernel, "pool_stripes": w["pool_stripes"],
+            "kernel": kernel, "pool_stripes": w["pool_stripes"], "kernel_source_hash": w["kernel_source_hash"],
             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
             "algorithmic_bytes_per_launch": algo, "traffic_over_algorithmic": (rd + wr) / algo,
             "read_over_algorithmic_read": rd / (algo - algo_wr), "write_over_algorithmic_write": wr / algo_wr,
@@ -73,15 +75,12 @@ def main(src=None, out_table="profiles/r02_pmc_workloads.json"):
             t["effective_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9  # GRBM sums the 8 XCDs
         t["bench_avg_launch_ms"] = w["avg_launch_ms"]
         table[name] = t
-    if len(hashes) != 1:
-        raise SystemExit("PMC passes span %d kernel-source hashes: %s" % (len(hashes), sorted(hashes)))
-    h = hashes.pop()
-    out = {"kernel_source_hash": h,
-           "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane streaming reads); "
+    # workloads not re-profiled in this run keep their entries (and their own hashes)
+    out = {"correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane streaming reads); "
                          "write = WRITE_SIZE x 1024",
            "workloads": traffic}
     (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
-    (ROOT / out_table).write_text(json.dumps({"kernel_source_hash": h, "workloads": table}, indent=1) + "\n")
+    (ROOT / out_table).write_text(json.dumps({"workloads": table}, indent=1) + "\n")
     print(json.dumps(table, indent=1))
 
 
