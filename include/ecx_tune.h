@@ -70,6 +70,16 @@
  *                      same, and for the plane-group kernel all slices and plane groups of one
  *                      (stripe, chunk) on one XCD, plane-group-fastest (default); 3 = the same, slice-fastest; 4 = as 3
  *                      with a contiguous range of (stripe, chunk) units per XCD
+ *   "map_planes"       the bit-plane kernel generated for one composed map and compiled with hiprtc
+ *                      (k_map_planes: every row of a <= 16-row map in registers, coefficients as
+ *                      fixed XOR networks over the 8 bit planes of each input), for the full 4 KiB
+ *                      chunks of 16-B-aligned layouts whose slot offsets fit 31 bits: 1 = auto
+ *                      (default) for multi-tile maps with >= 4 coefficients per used input on
+ *                      batches of >= 64 MiB of input (the Clay(4,2) two-node repairs), 2 = wherever
+ *                      it fits, 0 = never
+ *   "planes_lookahead" that kernel's load schedule: inputs in flight ahead of the one being
+ *                      computed, 0..15 (default 4)
+ *   "planes_waves"     that kernel's __launch_bounds__ minimum waves per SIMD, 1..4 (default 2)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered
@@ -112,6 +122,13 @@ int ecx_clay_rtc_compile_check(struct ecx_clay *clay);
 /* The generated kernel source: copied NUL-terminated into buf when len exceeds its
  * length; returns the length. */
 int ecx_clay_rtc_source(struct ecx_clay *clay, char *buf, int len);
+/* The bit-plane kernel of a composed map (ecx_tune "map_planes"), overwriting or, with
+ * accumulate != 0, XOR-accumulating its outputs: compile it with hiprtc for gfx950 (no
+ * device needed) and return the code-object size, or copy its source NUL-terminated into
+ * buf when len exceeds its length and return the length.  ECX_E_ILLEGAL_ARGUMENT if the
+ * map does not fit the kernel (more than 16 rows), ECX_E_DEVICE if hiprtc fails. */
+int ecx_map_planes_compile_check(const struct ecx_map *map, int accumulate);
+int ecx_map_planes_source(const struct ecx_map *map, int accumulate, char *buf, int len);
 #ifdef __cplusplus
 }
 #endif

@@ -409,6 +409,22 @@ class GfMap:
         f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_uint64], ctypes.c_int
         check(f(self._h, seed))
 
+    def planes_compile_check(self, accumulate: bool = False) -> int:
+        """Generate this map's bit-plane kernel (k_map_planes) and compile it with hiprtc
+        for gfx950; returns the code-object size (ecx_map_planes_compile_check)."""
+        f = lib().ecx_map_planes_compile_check
+        f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_int], ctypes.c_int
+        return check(f(self._h, int(accumulate)))
+
+    def planes_source(self, accumulate: bool = False) -> str:
+        """The generated k_map_planes source (ecx_map_planes_source)."""
+        f = lib().ecx_map_planes_source
+        f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+        n = check(f(self._h, int(accumulate), None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        check(f(self._h, int(accumulate), buf, n + 1))
+        return buf.value.decode()
+
     def plan_stats(self) -> dict:
         """Shape of the compiled plan (ecx_map_plan_stats, include/ecx_tune.h)."""
         f = lib().ecx_map_plan_stats

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "codes.hpp"
 
@@ -72,5 +73,13 @@ private:
 // Compile `source` with hiprtc for gfx950 (diagnostics / tests: no device needed).
 // Returns the code object size, throws ECX_E_DEVICE with the compiler log on failure.
 size_t rtc_compile_check(const std::string &source);
+
+// Shared by the generated kernels (clay_rtc.cpp, map_rtc.cpp): hiprtc compilation to a
+// gfx950 code object (throws ECX_E_DEVICE with the log), the common device prelude
+// (bit-plane transpose tr/untr, the 3-input XOR x3, uniform64), and the bit-plane
+// multiply: plane i of c*x is the XOR of the planes j in plane_sets(c)[i].
+std::vector<char> rtc_compile(const std::string &source);
+const char *rtc_prelude();
+std::vector<std::vector<int>> plane_sets(uint8_t c);
 
 }  // namespace ecx

@@ -9,6 +9,7 @@
 #include <string>
 
 #include "clay_rtc.hpp"
+#include "map_rtc.hpp"
 #include "engine.hpp"
 
 using namespace ecx;
@@ -775,6 +776,26 @@ int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
     });
 }
 
+int ecx_map_planes_compile_check(const ecx_map *map, int accumulate) {
+    return guarded([&]() -> int {
+        PlanesShape sh;
+        sh.lookahead = tuning().planes_lookahead;
+        sh.waves = tuning().planes_waves;
+        return (int)rtc_compile_check(map_planes_source(map->cm.map(), sh, accumulate != 0));
+    });
+}
+
+int ecx_map_planes_source(const ecx_map *map, int accumulate, char *buf, int len) {
+    return guarded([&]() -> int {
+        PlanesShape sh;
+        sh.lookahead = tuning().planes_lookahead;
+        sh.waves = tuning().planes_waves;
+        const std::string src = map_planes_source(map->cm.map(), sh, accumulate != 0);
+        if (buf && len > (int)src.size()) std::memcpy(buf, src.c_str(), src.size() + 1);
+        return (int)src.size();
+    });
+}
+
 // ---------------------------------------------------------------- LRC
 namespace {
 struct LrcCache {
@@ -974,6 +995,18 @@ int ecx_tune(const char *key, int value) {
     else if (k == "rtc_waves") {
         if (value < 2 || value > 4) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_waves = value;
+    }
+    else if (k == "map_planes") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.map_planes = value;
+    }
+    else if (k == "planes_lookahead") {
+        if (value < 0 || value > 15) return ECX_E_ILLEGAL_ARGUMENT;
+        t.planes_lookahead = value;
+    }
+    else if (k == "planes_waves") {
+        if (value < 1 || value > 4) return ECX_E_ILLEGAL_ARGUMENT;
+        t.planes_waves = value;
     }
     else if (k == "bitslice") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;

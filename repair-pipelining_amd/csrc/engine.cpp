@@ -1,6 +1,7 @@
 // engine.cpp -- plan compilation, device contexts, host-pointer execution.
 #include "engine.hpp"
 #include "bits.hpp"
+#include "map_rtc.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -635,6 +636,15 @@ CompiledMap &CompiledMap::compact() {
         compact_ = std::make_unique<CompiledMap>(std::move(c));
     }
     return *compact_;
+}
+
+MapPlanes *CompiledMap::planes() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!planes_checked_) {
+        planes_checked_ = true;
+        if (map_planes_supported(map_)) planes_ = std::make_unique<MapPlanes>(map_);
+    }
+    return planes_.get();
 }
 
 const std::vector<int> &CompiledMap::used_in_slots() {

@@ -41,6 +41,8 @@ constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 
 void check_hip(hipError_t e, const char *what);
 
+class MapPlanes;  // map_rtc.hpp
+
 constexpr uint32_t kDummySlot = 0xFFFFFFFFu;  // entry padding: loads the device's zero page
 
 struct DevicePlan {
@@ -135,12 +137,17 @@ public:
     // `bentries`, for `len` a multiple of kChunkBytes (the kernel's chunk).
     void emulate_bits(const HostPlan &p, const uint8_t *in, uint8_t *out, int64_t len) const;
     CompiledMap &compact();
+    // The generated bit-plane kernel for this map (map_rtc.hpp), created on first use;
+    // nullptr when the map does not fit it (more than 16 rows, too many coefficients).
+    MapPlanes *planes();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
 
 private:
     LinearMap map_;
     std::unique_ptr<CompiledMap> compact_;
+    std::unique_ptr<MapPlanes> planes_;
+    bool planes_checked_ = false;
     std::vector<int> used_in_, used_out_;
     std::vector<uint32_t> entries_, tiles_;  // unpadded
     std::vector<uint32_t> groups_, unions_;  // unpadded unions
@@ -233,6 +240,13 @@ struct Tuning {
     int rtc_xcd = 2;        // its block order: 1 = the helper planes of a (stripe, chunk) on one XCD;
                             // 2 (plane-group kernel): whole (stripe, chunk) units per XCD, +4.5 %
                             // (+1.1 % on Clay(10,4), profiles/r02_rtc_sweep.jsonl)
+    // Generated bit-plane kernel for one composed map (k_map_planes, map_rtc.hpp): 1 = auto
+    // for multi-tile maps of <= 16 rows whose coefficients outnumber their inputs by 4x or
+    // more (vector-bound under the split tables: the Clay(4,2) two-node repairs), on
+    // batches of >= 64 MiB of input; 2 = wherever it fits; 0 = never.
+    int map_planes = 1;
+    int planes_lookahead = 4;  // its load lookahead (inputs in flight), 0..15
+    int planes_waves = 2;      // its __launch_bounds__ minimum waves per SIMD, 1..4
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the

@@ -17,6 +17,7 @@
 //     coefficient 1 is a bare XOR (LRC local parity);
 //   * no LDS, no MFMA: this is HBM-bound byte work.
 #include "apply.hpp"
+#include "map_rtc.hpp"
 
 namespace ecx {
 
@@ -305,11 +306,38 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // (the chunk accounting below is in 4 KiB chunks only for 256-thread shapes)
     const bool bits_ok = aligned && offsets32 && !waves && threads == kBlockThreads && ntmode != 0 &&
                          nbytes >= kChunkBytes;
-    const bool bits = bits_ok && !skew &&
+    bool bits = bits_ok && !skew &&
                       (tu.bitslice == 2 || (tu.bitslice == 1 && cm.n_tiles() > 1 && !wide));
     if (bits) {
         depth = tu.depth == 2 ? 2 : 4;
         wide = false;  // the byte-safe tail runs k_gf_apply over the same padded tiles
+    }
+    // Generated bit-plane kernel (k_map_planes, map_rtc.hpp) for the full 4 KiB chunks:
+    // forced (2) wherever it fits, or auto (1) for multi-tile maps of <= 16 rows whose
+    // coefficients outnumber their used inputs 4x or more -- where the split tables are
+    // bound by vector issue (the Clay(4,2) two-node repairs: 184 coefficients over 32
+    // inputs) -- on batches big enough (>= 64 MiB of input) to amortise the one-time
+    // hiprtc compile.  The byte-safe tail runs on the composed plan below.
+    bool planes = false;
+    if (tu.map_planes && aligned && offsets32 && !waves && nbytes >= kChunkBytes &&
+        cm.map().n_out <= kPlanesMaxRows) {
+        if (tu.map_planes == 2) {
+            planes = true;
+        } else if (cm.n_tiles() > 1) {
+            int used = 0;
+            for (int j = 0; j < cm.map().n_in; ++j)
+                for (int o = 0; o < cm.map().n_out; ++o)
+                    if (cm.map().at(o, j)) {
+                        ++used;
+                        break;
+                    }
+            planes = cm.map().nnz() >= 4 * used && nstripes * (nbytes / kChunkBytes) * used >= 16384;
+        }
+        planes = planes && cm.planes() != nullptr;
+    }
+    if (planes) {
+        skew = 0;
+        bits = false;
     }
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
@@ -406,6 +434,12 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         }
     };
     int64_t first = 0;  // first full chunk left to the one-chunk kernels
+    if (planes) {
+        const int64_t n4k = nbytes / kChunkBytes;
+        cm.planes()->launch(in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes, n4k,
+                            accumulate, stream);
+        first = n4k * kChunkBytes / chunk;
+    }
     if (skew) {
         const int64_t groups = full / skew;
         a.chunk_begin = 0;

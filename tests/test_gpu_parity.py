@@ -663,7 +663,10 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     for wg, lt, sc, cm, bt, wd in ((1, 1, 0, 0, 256, 0), (0, 0, 0, 0, 256, 0), (0, 1, 0, 0, 256, 0),
                                    (0, 2, 0, 0, 256, 0), (0, 1, 1, 0, 256, 0), (0, 1, 0, 1, 256, 0),
                                    (0, 1, 0, 0, 64, 0), (0, 2, 0, 1, 64, 0), (2, 1, 0, 0, 256, 0),
-                                   (0, 1, 0, 0, 256, 2)):
+                                   (0, 1, 0, 0, 256, 2), (0, 1, 0, 0, 256, -1)):
+        # wd < 0: the generated bit-plane kernel forced (ecx_tune "map_planes" 2; maps of <= 16 rows)
+        ecx.tune("map_planes", 2 if wd < 0 else 0)
+        wd = max(wd, 0)
         ecx.tune("wave_groups", wg)
         ecx.tune("lds_tables", lt)
         ecx.tune("store_scope", sc)
@@ -680,6 +683,7 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
     ecx.tune("chunk_major", 0)
     ecx.tune("block_threads", 0)
     ecx.tune("wide_tiles", 1)
+    ecx.tune("map_planes", 1)
     for o in outs[1:]:
         assert (o == outs[0]).all()
     if v == 0:
@@ -1266,3 +1270,87 @@ def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):
     assert (outs[0][0] == outs[1][0]).all() and (outs[0][0] == outs[2][0]).all()
     del buf
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_map_planes_random_maps(ecx, torch_dev, seed):
+    """The bit-plane kernel generated per map (k_map_planes, map_rtc.cpp; ecx_tune
+    "map_planes" 2) on random maps of 1-16 rows over up to 40 scattered input slots
+    (coefficient-1 entries, zero rows and unread inputs), ragged byte counts (the tail
+    runs on the composed plan), at load lookaheads 0-8 and 1-3 waves per SIMD, and in
+    accumulate mode (out ^= M * in): each equals the oracle's table-driven product."""
+    from conftest import gf_apply_numpy
+    torch = torch_dev
+    rng = np.random.default_rng(7000 + seed)
+    n_out, n_in = int(rng.integers(1, 17)), int(rng.integers(1, 41))
+    m = rng.integers(2, 256, (n_out, n_in)).astype(np.uint8)
+    m[rng.random((n_out, n_in)) < 0.2] = 1
+    m[rng.random((n_out, n_in)) >= rng.uniform(0.2, 1.0)] = 0
+    if n_out > 2 and seed % 2:
+        m[1] = 0
+    in_slot = sorted(rng.choice(2 * n_in, n_in, replace=False).tolist())
+    out_slot = rng.permutation(rng.choice(2 * n_out, n_out, replace=False)).tolist()
+    gm = ecx.GfMap.from_matrix(m, in_slot=in_slot, out_slot=out_slot)
+    S, L = 3, 4096 * int(rng.integers(1, 4)) + (0 if seed == 0 else int(rng.integers(1, 4096)))
+    ni, no = 2 * n_in, 2 * n_out
+    inp = torch.empty((S, ni, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(inp, inp.numel(), 70 + seed)
+    host = inp.cpu().numpy()
+    ref = [gf_apply_numpy(m, [host[s, j] for j in in_slot]) for s in range(S)]
+    try:
+        ecx.tune("map_planes", 2)
+        for la, waves, acc in ((4, 2, False), (0, 2, False), (1, 3, False), (8, 1, False), (4, 2, True)):
+            ecx.tune("planes_lookahead", la)
+            ecx.tune("planes_waves", waves)
+            out = torch.empty((S, no, L), dtype=torch.uint8, device="cuda")
+            ecx.fill_random(out, out.numel(), 90 + seed)
+            prev = out.cpu().numpy()
+            if acc:
+                gm.accumulate_batch(inp, ni * L, L, out, no * L, L, S, L)
+            else:
+                gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
+            torch.cuda.synchronize()
+            assert ecx.last_kernel() == "k_map_planes"
+            got = out.cpu().numpy()
+            for s in range(S):
+                for o, slot in enumerate(out_slot):
+                    want = ref[s][o] ^ prev[s, slot] if acc else ref[s][o]
+                    assert (got[s, slot] == want).all(), (la, waves, acc, s, o)
+            untouched = sorted(set(range(no)) - set(out_slot))
+            assert (got[:, untouched] == prev[:, untouched]).all()
+    finally:
+        ecx.tune("map_planes", 1)
+        ecx.tune("planes_lookahead", 4)
+        ecx.tune("planes_waves", 2)
+
+
+@pytest.mark.parametrize("erased", [[0, 3], [4, 5], [1, 2]])
+def test_map_planes_auto_clay42_batches(ecx, torch_dev, erased):
+    """Clay(4,2) two-node repairs and the encode on a batch big enough for the auto rule
+    (64 stripes x 32 KiB sub-chunks): the generated bit-plane kernel runs (ecx_last_kernel),
+    and its bytes equal the split-table kernels' (map_planes 0) and, on a sampled
+    stripe, the oracle's performCoding."""
+    torch = torch_dev
+    k, m, B, S = 4, 2, 32768, 64
+    n, a = k + m, 8
+    step = ecx.ClayCodeErasureDecodingStep(erased, k, m)
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 41)
+    outs = []
+    try:
+        for mode in (1, 0):
+            ecx.tune("map_planes", mode)
+            o = torch.full((S, len(erased) * a, B), 7, dtype=torch.uint8, device="cuda")
+            step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
+            torch.cuda.synchronize()
+            if mode == 1:
+                assert ecx.last_kernel() == "k_map_planes"
+            outs.append(o.cpu().numpy())
+    finally:
+        ecx.tune("map_planes", 1)
+    assert (outs[0] == outs[1]).all()
+    host = pool[S // 2].cpu().numpy()
+    inputs = [None if (i % n) in erased else host[i].copy() for i in range(n * a)]
+    ref = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
+    O.Clay(k, m, erased).perform_coding(inputs, ref, B)
+    assert all((outs[0][S // 2, j] == ref[j]).all() for j in range(len(ref)))

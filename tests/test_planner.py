@@ -307,3 +307,43 @@ def test_clay_rtc_refuses_multi_erasure(ecx):
     step = ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2)
     with pytest.raises(ecx.EcxError):
         step.rtcCompileCheck()
+
+
+@pytest.mark.parametrize("case", ["clay42_03", "clay42_encode", "random16", "one_row", "accumulate"])
+def test_map_planes_source_compiles(ecx, case):
+    """The bit-plane kernel generated for one composed map (k_map_planes, map_rtc.cpp)
+    compiles with hiprtc for gfx950 without a device, for the Clay(4,2) two-node repair
+    and encode maps, a dense random 16-row map with coefficient-1 entries and zero rows,
+    a one-row map, and in accumulate mode; every used input is loaded exactly once and
+    every row stored exactly once."""
+    rng = np.random.default_rng(5)
+    acc = case == "accumulate"
+    if case == "clay42_03":
+        gm = ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2).map()
+    elif case == "clay42_encode":
+        gm = ecx.ClayCodeErasureDecodingStep([4, 5], 4, 2).map()
+    else:
+        n_out = 1 if case == "one_row" else 16
+        m = rng.integers(2, 256, (n_out, 40)).astype(np.uint8)
+        m[rng.random(m.shape) < 0.2] = 1
+        m[rng.random(m.shape) < 0.3] = 0
+        if n_out > 1:
+            m[3] = 0  # a row no input reaches
+            m[:, 7] = 0  # an input no row reads
+        gm = ecx.GfMap.from_matrix(m, in_slot=list(range(0, 80, 2)), out_slot=list(range(n_out)))
+    mat, ins, outs = gm.matrix()
+    src = gm.planes_source(acc)
+    assert "k_map_planes(" in src
+    used = [j for j in range(mat.shape[1]) if mat[:, j].any()]
+    assert src.count("    ld(") == len(used)
+    assert all(("    ld(%du * sl" % ins[j]) in src for j in used)
+    stored = [r for r in range(mat.shape[0]) if mat[r].any() or not acc]
+    assert src.count("    st(") == len(stored)
+    assert gm.planes_compile_check(acc) > 0
+
+
+def test_map_planes_refuses_wide_maps(ecx):
+    """More than 16 rows do not fit the kernel's registers: refused, not truncated."""
+    gm = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2).map()
+    with pytest.raises(ecx.EcxError):
+        gm.planes_source()
