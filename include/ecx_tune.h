@@ -78,7 +78,7 @@
  *                      batches of >= 64 MiB of input (the Clay(4,2) two-node repairs), 2 = wherever
  *                      it fits, 0 = never
  *   "planes_lookahead" that kernel's load schedule: inputs in flight ahead of the one being
- *                      computed, 0..15 (default 4)
+ *                      computed, 0..15 (default 12)
  *   "planes_waves"     that kernel's __launch_bounds__ minimum waves per SIMD, 1..4 (default 2)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)

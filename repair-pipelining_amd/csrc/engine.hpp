@@ -245,7 +245,7 @@ struct Tuning {
     // more (vector-bound under the split tables: the Clay(4,2) two-node repairs), on
     // batches of >= 64 MiB of input; 2 = wherever it fits; 0 = never.
     int map_planes = 1;
-    int planes_lookahead = 4;  // its load lookahead (inputs in flight), 0..15
+    int planes_lookahead = 12;  // its load lookahead (inputs in flight), 0..15 (profiles/r02_planes_ab.jsonl)
     int planes_waves = 2;      // its __launch_bounds__ minimum waves per SIMD, 1..4
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight

@@ -27,7 +27,7 @@ constexpr int kPlanesMaxRows = 16;   // 16 rows x 8 planes = 128 accumulator VGP
 constexpr int kPlanesMaxNnz = 1024;  // code size bound (~12 instructions per coefficient)
 
 struct PlanesShape {
-    int lookahead = 4;  // inputs whose loads are in flight ahead of the one being computed
+    int lookahead = 12;  // inputs whose loads are in flight ahead of the one being computed
     int waves = 2;      // __launch_bounds__ minimum waves per SIMD (VGPR budget)
     bool nt_loads = true;
 };

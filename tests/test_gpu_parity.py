@@ -1320,7 +1320,7 @@ def test_map_planes_random_maps(ecx, torch_dev, seed):
             assert (got[:, untouched] == prev[:, untouched]).all()
     finally:
         ecx.tune("map_planes", 1)
-        ecx.tune("planes_lookahead", 4)
+        ecx.tune("planes_lookahead", 12)
         ecx.tune("planes_waves", 2)
 
 
