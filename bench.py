@@ -28,6 +28,8 @@ contract (same launch, timing and JSON line; the default is the headline):
            512 resident stripes per GPU (shard pitch 4 MiB + 4 KiB, --pitch-pad)
   lrc      config 3: LRC (12 data, 4 XOR local parities), 64 KiB blocks, repair of
            data block 2 from its local group, 2^15 resident stripes per GPU
+  clay42x2 SURVEY 8(f) f4: Clay(4,2), 32 KiB, two-node repair of nodes {0, 3}
+           (doDecodeMulti) over the headline's pool of 2^15 stripes
 The cpu_baseline leg runs for the headline workload only.
 """
 import argparse
@@ -58,6 +60,8 @@ WORKLOADS = {
     "clay104": ("GiB/s repair-decode (device-resident), Clay(10,4) 1 MiB blocks, 1/2/4/8 GPU", 2048, 1 << 15),
     "rs124": ("GiB/s 2-erasure decode (device-resident), RS(12,4) 4 MiB blocks, 1/2/4/8 GPU", 512, 4096),
     "lrc": ("GiB/s local-group repair (device-resident), LRC(12,4) 64 KiB blocks, 1/2/4/8 GPU", 1 << 15, 1 << 18),
+    "clay42x2": ("GiB/s two-node repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU", 1 << 15,
+                 1 << 18),
 }
 
 
@@ -321,6 +325,31 @@ class Clay42(Workload):
         return bool(self.torch.equal(self.out, self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.erased, :]))
 
 
+class Clay42x2(Clay42):
+    """Clay(4,2), B = 32 KiB, repair of nodes {0, 3} (doDecodeMulti,
+    ClayCodeErasureDecodingStep.java:311-421) over the same resident pool of valid stripes."""
+    ERASED = [0, 3]
+
+    def __init__(self, ecx, torch, dev, P, erased, seed):
+        super().__init__(ecx, torch, dev, P, erased, seed)
+        self.out = torch.empty((P, ALPHA * len(self.ERASED), B), dtype=torch.uint8, device=dev)
+        self.step = ecx.ClayCodeErasureDecodingStep(self.ERASED, K, M)
+        info = self.step.map().info()
+        self.unit_bytes = (info["n_in"] + info["n_out"]) * B  # 32 helper + 16 repaired sub-chunks
+        self.write_bytes = info["n_out"] * B
+        self.reads, self.writes = info["n_in"], info["n_out"]
+        self.description = "Clay(4,2) two-node repair (erased nodes 0 and 3, doDecodeMulti), CLAY_BLOCK_SIZE=32768"
+
+    def launch(self):
+        e = len(self.ERASED)
+        self.step.performCodingBatch(self.pool, STRIPE_BYTES, B, self.out, e * ALPHA * B, B, self.P, B)
+
+    def verify(self):
+        e = len(self.ERASED)
+        want = self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.ERASED, :]
+        return bool(self.torch.equal(self.out.view(self.P, ALPHA, e, B), want))
+
+
 class Clay104(Workload):
     """Config 4: shortened Clay(10,4) (Clay(12,4) with 2 virtual zero data nodes),
     1 MiB node blocks = 256 planes x 4 KiB sub-chunks, single-node repair."""
@@ -484,6 +513,8 @@ def main():
         wl = Clay42(ecx, torch, dev, P, args.erased, seed)
     elif args.workload == "clay104":
         wl = Clay104(ecx, torch, dev, P, args.erased, seed)
+    elif args.workload == "clay42x2":
+        wl = Clay42x2(ecx, torch, dev, P, args.erased, seed)
     elif args.workload == "rs124":
         wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed)
     else:
