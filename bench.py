@@ -223,13 +223,20 @@ COMMON_SOURCES = ["engine.hpp", "engine.cpp", "codes.cpp", "codes.hpp"]
 COMPOSED_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
                     "apply_skew.hip", "apply_bits.hip", "bits.hpp"]
 RTC_SOURCES = ["clay_rtc.hpp", "clay_rtc.cpp"]
+# k_map_planes: its generator, the shared prelude (clay_rtc.cpp) and launch_apply's choice (kernels.hip)
+PLANES_SOURCES = RTC_SOURCES + ["map_rtc.hpp", "map_rtc.cpp", "kernels.hip"]
 
 
 def kernel_source_hash(kernel: str = "") -> str:
-    """Hash of the sources behind `kernel` (a k_clay_repair* label selects the generated
-    family, anything else the composed-map family)."""
+    """Hash of the sources behind `kernel`: the generated Clay kernels (k_clay_repair*),
+    the generated map kernel (k_map_planes) or the composed-map family (anything else)."""
     import hashlib
-    names = COMMON_SOURCES + (RTC_SOURCES if kernel.startswith("k_clay_repair") else COMPOSED_SOURCES)
+    if kernel.startswith("k_clay_repair"):
+        names = COMMON_SOURCES + RTC_SOURCES
+    elif kernel.startswith("k_map_planes"):
+        names = COMMON_SOURCES + PLANES_SOURCES
+    else:
+        names = COMMON_SOURCES + COMPOSED_SOURCES
     h = hashlib.sha256()
     for name in names:
         h.update(name.encode() + b"\0" + (ROOT / "repair-pipelining_amd" / "csrc" / name).read_bytes())

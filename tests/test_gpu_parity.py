@@ -1354,3 +1354,38 @@ def test_map_planes_auto_clay42_batches(ecx, torch_dev, erased):
     ref = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
     O.Clay(k, m, erased).perform_coding(inputs, ref, B)
     assert all((outs[0][S // 2, j] == ref[j]).all() for j in range(len(ref)))
+
+
+def test_map_planes_every_clay42_erasure_pattern(ecx, torch_dev):
+    """Every Clay(4,2) single and two-node erasure pattern (6 + 15 maps, performCoding's
+    doDecodeSingle / doDecodeMulti compositions) on the generated bit-plane kernel
+    (map_planes forced), two 4 KiB chunks plus a ragged tail: bit-exact against the
+    oracle's stage-by-stage performCoding on the last stripe and equal to the
+    split-table kernels on every stripe."""
+    import itertools
+    torch = torch_dev
+    k, m, B, S = 4, 2, 2 * 4096 + 272, 3
+    n, a = k + m, 8
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 57)
+    host = pool[S - 1].cpu().numpy()
+    patterns = [[e] for e in range(n)] + [list(p) for p in itertools.combinations(range(n), 2)]
+    try:
+        for erased in patterns:
+            step = ecx.ClayCodeErasureDecodingStep(erased, k, m)
+            got = []
+            for mode in (2, 0):
+                ecx.tune("map_planes", mode)
+                o = torch.full((S, len(erased) * a, B), 0xA5, dtype=torch.uint8, device="cuda")
+                step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
+                torch.cuda.synchronize()
+                if mode == 2:
+                    assert ecx.last_kernel() == "k_map_planes", erased
+                got.append(o.cpu().numpy())
+            assert (got[0] == got[1]).all(), erased
+            inputs = [None if (i % n) in erased else host[i].copy() for i in range(n * a)]
+            ref = [np.zeros(B, np.uint8) for _ in range(len(erased) * a)]
+            O.Clay(k, m, erased).perform_coding(inputs, ref, B)
+            assert all((got[0][S - 1, j] == ref[j]).all() for j in range(len(ref))), erased
+    finally:
+        ecx.tune("map_planes", 1)
