@@ -57,7 +57,8 @@
  *                      for the plane-group kernel bit 0 = partner and mate loads after row ya, bit 1
  *                      = skip the dot's and virtual partners' transposes by uniform branches, bit 2
  *                      = a second body for plane groups whose memory-row partner is virtual, bit 3 =
- *                      every load issued at the start
+ *                      every load issued at the start, bit 4 = DIAGNOSTIC data-movement-only build
+ *                      (coefficients taken as 1, no transposes: the outputs are not the repair)
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes

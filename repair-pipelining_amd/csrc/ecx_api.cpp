@@ -980,7 +980,7 @@ int ecx_tune(const char *key, int value) {
         t.clay_rtc = value;
     }
     else if (k == "rtc_lookahead") {
-        if (value < 0 || value > 15) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value < 0 || value > 31) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_lookahead = value;
     }
     else if (k == "rtc_xcd") {

@@ -143,7 +143,7 @@ def test_tuning_keys(ecx):
     for key, val in defaults.items():
         assert tune(key.encode(), val) == 0, key
     assert tune(b"no_such_knob", 1) == -1
-    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("plan_cache", -1), ("bitslice", 3), ("clay_rtc", 3), ("rtc_lookahead", 16), ("rtc_waves", 1), ("rtc_persist", 9), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5)):
+    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("plan_cache", -1), ("bitslice", 3), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5)):
         assert tune(key.encode(), bad) == -1, key
     for key, val in defaults.items():  # restore
         tune(key.encode(), val)
