@@ -1,0 +1,138 @@
+// clay104_probe.hip -- the data movement of a Clay(10,4) single repair (BASELINE config 4,
+// shortened Clay(12,4): 256 planes x 14 real nodes x 4 KiB sub-chunks per stripe,
+// plane-major as performCoding lays it out; repair of node 3 = (x 3, y 0) reads the 13
+// other real nodes of its 64 helper planes 192..255 and writes 256 x 4 KiB), with no GF
+// arithmetic (XOR folds only), under two work shapes:
+//   plane  one 256-thread workgroup per (stripe, helper plane): each wave-wide load is
+//          1 KiB contiguous, a workgroup reads 13 whole 4 KiB sub-chunks and writes the
+//          plane's 4 output sub-chunks (k_clay_repair's shape, without partners);
+//   group  one 256-thread workgroup per (stripe, 512-B slice, 16-plane group): lane row g
+//          of wave w holds plane 4w + g, each load instruction is four 256-B runs
+//          (k_clay_repair_grp's shape, without exchanges or partners).
+// Each with the identity block order and with a stripe's workgroups on one XCD.  Prints
+// algorithmic GB/s ((832 + 256) x 4 KiB per stripe) as a fraction of 8 TB/s.
+//
+//   hipcc --offload-arch=gfx950 -O3 scripts/clay104_probe.hip -o scripts/clay104_probe && ./scripts/clay104_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
+__device__ __forceinline__ u32x4 ldnt(const uint8_t *p) { return __builtin_nontemporal_load((const gu32x4 *)p); }
+__device__ __forceinline__ void stnt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (gu32x4 *)p); }
+
+constexpr int64_t kSub = 4096, kNodes = 14, kPlanes = 256, kHelp = 64;
+constexpr int64_t kStripe = kPlanes * kNodes * kSub;  // 14 MiB
+constexpr int64_t kOut = kPlanes * kSub;              // 1 MiB
+
+// XCD-local order (xcd = 1): blocks b, b+8, b+16, ... run on one XCD; give them the
+// `per` consecutive units of one stripe.
+__device__ __forceinline__ uint32_t unit_of(uint32_t b, uint32_t per, int xcd, uint32_t n) {
+    if (!xcd) return b;
+    const uint32_t full = n / (8u * per) * (8u * per);
+    if (b >= full) return b;
+    const uint32_t j = b / 8u;
+    return ((j / per) * 8u + (b % 8u)) * per + j % per;
+}
+
+// MODE 0: as the repair; 1: no stores (a never-taken store keeps the loads live);
+// 2: the 4 outputs of a plane written contiguously (16 KiB) instead of 256 KiB apart;
+// 3: all 14 nodes of the plane read (one contiguous 56 KiB run per workgroup).
+template <int XCD, int MODE = 0>
+__global__ void __launch_bounds__(256) k_plane(const uint8_t *pool, uint8_t *out, uint32_t n) {
+    const uint32_t u = unit_of(blockIdx.x, kHelp, XCD, n);
+    const int64_t s = u / kHelp, p = u % kHelp, z = 192 + p;
+    const uint8_t *in = pool + s * kStripe + z * kNodes * kSub + threadIdx.x * 16;
+    constexpr int NJ = MODE == 3 ? 14 : 13;
+    u32x4 v[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) v[j] = ldnt(in + (int64_t)(MODE == 3 || j < 3 ? j : j + 1) * kSub);
+    u32x4 acc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = v[r] ^ v[r + 4] ^ v[r + 8] ^ (r == 0 ? v[12] : (u32x4){0u, 0u, 0u, 0u});
+    if (MODE == 3) acc[1] ^= v[13];
+    uint8_t *o = out + s * kOut + threadIdx.x * 16;
+    if (MODE == 1) {
+        const u32x4 a = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+        if (a.x == 0x12345678u && a.y == 0x9abcdef0u) stnt(o, a);
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) stnt(o + (MODE == 2 ? (int64_t)(4 * p + r) : (int64_t)(p + 64 * r)) * kSub, acc[r]);
+}
+
+template <int XCD>
+__global__ void __launch_bounds__(256) k_group(const uint8_t *pool, uint8_t *out, uint32_t n) {
+    const uint32_t u = unit_of(blockIdx.x, 32, XCD, n);  // 8 slices x 4 plane groups per stripe
+    const int64_t s = u / 32, sl = (u % 32) / 4, grp = u % 4;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, g = lane >> 4;
+    const int64_t p = grp * 16 + w * 4 + g, z = 192 + p;
+    const uint8_t *in = pool + s * kStripe + z * kNodes * kSub + sl * 512 + (lane & 15u) * 16;
+    u32x4 v[13][2];
+#pragma unroll
+    for (int j = 0; j < 13; ++j) {
+        const int64_t node = j < 3 ? j : j + 1;
+        v[j][0] = ldnt(in + node * kSub);
+        v[j][1] = ldnt(in + node * kSub + 256);
+    }
+    uint8_t *o = out + s * kOut + sl * 512 + (lane & 15u) * 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            u32x4 a = v[r][h] ^ v[r + 4][h] ^ v[r + 8][h];
+            if (r == 0) a ^= v[12][h];
+            stnt(o + (int64_t)(p + 64 * r) * kSub + h * 256, a);
+        }
+}
+
+template <typename F>
+float best_ms(F launch) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best = 1e9f;
+    for (int rep = 0; rep < 8; ++rep) {
+        float ms = 0;
+        hipEventRecord(e0);
+        launch();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best = ms < best ? ms : best;
+    }
+    return best;
+}
+
+int main() {
+    const int64_t S = 2048;
+    uint8_t *pool = nullptr, *out = nullptr;
+    if (hipMalloc(&pool, S * kStripe) != hipSuccess || hipMalloc(&out, S * kOut) != hipSuccess) return 1;
+    hipMemset(pool, 0x5A, S * kStripe);
+    const double bytes = (double)S * (832 + 256) * kSub;
+    for (int round = 0; round < 2; ++round) {
+        const uint32_t np = (uint32_t)(S * kHelp), ng = (uint32_t)(S * 32);
+        const char *names[] = {"plane", "plane_xcd", "group", "group_xcd", "plane_readonly", "plane_out_contig",
+                               "plane_read14"};
+        float ms[7];
+        ms[0] = best_ms([&] { hipLaunchKernelGGL((k_plane<0>), dim3(np), dim3(256), 0, 0, pool, out, np); });
+        ms[1] = best_ms([&] { hipLaunchKernelGGL((k_plane<1>), dim3(np), dim3(256), 0, 0, pool, out, np); });
+        ms[2] = best_ms([&] { hipLaunchKernelGGL((k_group<0>), dim3(ng), dim3(256), 0, 0, pool, out, ng); });
+        ms[3] = best_ms([&] { hipLaunchKernelGGL((k_group<1>), dim3(ng), dim3(256), 0, 0, pool, out, ng); });
+        ms[4] = best_ms([&] { hipLaunchKernelGGL((k_plane<0, 1>), dim3(np), dim3(256), 0, 0, pool, out, np); });
+        ms[5] = best_ms([&] { hipLaunchKernelGGL((k_plane<0, 2>), dim3(np), dim3(256), 0, 0, pool, out, np); });
+        ms[6] = best_ms([&] { hipLaunchKernelGGL((k_plane<0, 3>), dim3(np), dim3(256), 0, 0, pool, out, np); });
+        for (int i = 0; i < 7; ++i) {
+            // read-only: the 832 read sub-chunks only; read14: 896 read + 256 written
+            const double b = i == 4 ? (double)S * 832 * kSub : (i == 6 ? (double)S * (896 + 256) * kSub : bytes);
+            printf("{\"round\": %d, \"shape\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", round,
+                   names[i], ms[i], b / (ms[i] * 1e-3) / 1e9, b / (ms[i] * 1e-3) / 1e9 / 8000.0);
+        }
+    }
+    hipFree(pool);
+    hipFree(out);
+    return 0;
+}
