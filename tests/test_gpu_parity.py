@@ -1118,7 +1118,9 @@ def test_multitile_slot_offset_near_2gib(ecx, torch_dev, stride):
     scalar offset, valid only while max_in_slot * in_slot_stride + 4 KiB < 2^31.  A
     16 x 2 map (two 8-row tiles sharing both inputs) with slot 1 just under and just
     over 2 GiB from slot 0 -- the descriptor path, and the 64-bit fallback -- equals
-    the oracle's table product, with wide tiles on and off."""
+    the oracle's table product, with wide tiles on and off, and with the generated
+    bit-plane kernel forced (map_planes 2: it runs under the limit and yields to the
+    64-bit composed kernels over it)."""
     from conftest import gf_apply_numpy
     torch = torch_dev
     rng = np.random.default_rng(stride & 0xFFFF)
@@ -1131,14 +1133,18 @@ def test_multitile_slot_offset_near_2gib(ecx, torch_dev, stride):
     x0, x1 = buf[:L].cpu().numpy(), buf[stride:].cpu().numpy()
     ref = gf_apply_numpy(m, [x0, x1])
     try:
-        for wide in (0, 2):
+        for wide, planes in ((0, 0), (2, 0), (1, 2)):
             ecx.tune("wide_tiles", wide)
+            ecx.tune("map_planes", planes)
             out = torch.full((16, L), 0x5A, dtype=torch.uint8, device="cuda")
             gm.apply_batch(buf, stride + L, stride, out, 16 * L, L, 1, L)
             torch.cuda.synchronize()
             assert (out.cpu().numpy() == ref).all(), (stride, wide, ecx.last_kernel())
+            if planes:
+                assert (ecx.last_kernel() == "k_map_planes") == (stride < (1 << 31)), ecx.last_kernel()
     finally:
         ecx.tune("wide_tiles", 1)
+        ecx.tune("map_planes", 1)
     del buf
     torch.cuda.empty_cache()
 
