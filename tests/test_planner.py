@@ -347,3 +347,20 @@ def test_map_planes_refuses_wide_maps(ecx):
     gm = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2).map()
     with pytest.raises(ecx.EcxError):
         gm.planes_source()
+
+
+def test_clay_grp_movement_only_build_is_isolated(ecx):
+    """rtc_lookahead bit 4 (16) generates the plane-group kernel's data-movement-only
+    diagnostic build (coefficients as 1, no transposes), marked as such; the next
+    default generation is byte-identical to one made before it."""
+    step = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2)
+    try:
+        before = step.rtcSource()
+        ecx.tune("rtc_lookahead", 17)
+        diag = step.rtcSource()
+        assert diag.startswith("// DIAGNOSTIC BUILD") and "    tr(" not in diag and "untr(" not in diag.split("DEV void untr")[1].split("\n", 1)[1]
+        assert step.rtcCompileCheck() > 0
+        ecx.tune("rtc_lookahead", 1)
+        assert step.rtcSource() == before and "DIAGNOSTIC" not in before
+    finally:
+        ecx.tune("rtc_lookahead", 1)
