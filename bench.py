@@ -221,7 +221,7 @@ def cpu_baseline(seconds: float, erased: int, sample=None):
 # for its kernel family is stale.
 COMMON_SOURCES = ["engine.hpp", "engine.cpp", "codes.cpp", "codes.hpp"]
 COMPOSED_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
-                    "apply_skew.hip", "apply_bits.hip", "bits.hpp"]
+                    "apply_skew.hip", "apply_bits.hip", "apply_lut.hip", "bits.hpp"]
 RTC_SOURCES = ["clay_rtc.hpp", "clay_rtc.cpp"]
 # k_map_planes: its generator, the shared prelude (clay_rtc.cpp) and launch_apply's choice (kernels.hip)
 PLANES_SOURCES = RTC_SOURCES + ["map_rtc.hpp", "map_rtc.cpp", "kernels.hip"]

@@ -47,6 +47,10 @@
  *                      aligned layouts whose slot offsets fit 31 bits: 1 = for multi-tile maps
  *                      that do not run as wide tiles, 2 = for every such map, 0 = never (default;
  *                      measured slower, bound by its scalar branches)
+ *   "lds_lut"          per-byte lookup tables in LDS (k_gf_lut) for the full 4 KiB chunks of
+ *                      aligned layouts: 1 = log/antilog tables (LOG u16, EXP 1 KiB), 2 = one 256-B
+ *                      product row per coefficient (single-tile maps of <= 256 general
+ *                      coefficients); 0 = never (default: measured slower)
  *   "clay_rtc"         Clay single-node repair batches (ecx_clay_perform_coding_batch): the
  *                      per-helper-plane kernel generated for the repair and compiled with hiprtc, for
  *                      the whole 4 KiB chunks of 16-B-aligned layouts: 1 = when the composed map spans

@@ -317,4 +317,10 @@ void launch_skew(int k, int rows, int depth, bool ntl, dim3 grid, hipStream_t st
 // chunks, ring depth 2 or 4; grid = stripes x chunks x tiles, as k_gf_apply.
 void launch_bits(bool ntl, int depth, dim3 grid, hipStream_t stream, const ApplyArgs &a);
 
+// k_gf_lut (apply_lut.hip): per-byte LDS table lookups -- mode 0 log/antilog, mode 1
+// product rows (single-tile maps, `pairs` general coefficients) -- over n_units
+// (stripe, 4 KiB chunk, tile) units of the depth-4 padded plan, persistent workgroups.
+void launch_lut(int mode, bool ntl, int pairs, int64_t n_units, hipStream_t stream, const ApplyArgs &a);
+constexpr int kLutMaxPairs = 256;  // mode 1: 64 KiB of product rows per workgroup at most
+
 }  // namespace ecx

@@ -1012,6 +1012,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.bitslice = value;
     }
+    else if (k == "lds_lut") {
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.lds_lut = value;
+    }
     else if (k == "host_buffers") {
         if (value < 1 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_buffers = value;

@@ -228,6 +228,11 @@ struct Tuning {
     // tiles, 0 = never (default: it measured 4-10 % slower on every BASELINE map, bound
     // by its scalar branches -- profiles/r02_bits_ab.jsonl, r02_bits_sq_ab.json).
     int bitslice = 0;
+    // LDS lookup-table kernel (k_gf_lut, apply_lut.hip) for the full 4 KiB chunks of
+    // aligned layouts, forced-only: 1 = log/antilog tables, 2 = one 256-B product row per
+    // coefficient (single-tile maps of <= kLutMaxPairs general coefficients); 0 = never
+    // (default: measured against the split tables in DESIGN.md 4.4).
+    int lds_lut = 0;
     // Clay single-node repair batches: the per-helper-plane kernel generated for the
     // repair and compiled with hiprtc (clay_rtc.hpp) for whole 4 KiB chunks -- 1 = when
     // the composed map spans several tiles (auto), 2 = always, 0 = never.

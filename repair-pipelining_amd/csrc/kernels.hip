@@ -253,7 +253,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool skew_pitch = in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4;
     const bool one_wave = tu.block_threads == 64 ||
                           (tu.block_threads == 0 && cm.n_tiles() == 1 && cm.max_tile_rows() <= 2 &&
-                           cm.map().n_in >= 8 && !skew_pitch && tu.bitslice != 2);
+                           cm.map().n_in >= 8 && !skew_pitch && tu.bitslice != 2 && !tu.lds_lut);
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     // Small-row kernel variants: forced (1), or auto (2) for maps of <= 2 rows over <= 4
@@ -338,6 +338,20 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     if (planes) {
         skew = 0;
         bits = false;
+    }
+    // LDS lookup-table kernel (k_gf_lut, apply_lut.hip), forced only: 1 = log/antilog, 2 =
+    // product rows for single-tile maps of <= kLutMaxPairs general coefficients.  Full
+    // 4 KiB chunks of aligned layouts on the depth-4 padded plan; the byte-safe tail
+    // runs k_gf_apply on the same plan.
+    int lut_pairs = 0;
+    for (int o = 0; o < cm.map().n_out; ++o)
+        for (int j = 0; j < cm.map().n_in; ++j) lut_pairs += cm.map().at(o, j) > 1;
+    const bool lut = tu.lds_lut && aligned && !waves && nbytes >= kChunkBytes && threads == kBlockThreads &&
+                     (tu.lds_lut == 1 || (cm.n_tiles() == 1 && lut_pairs <= kLutMaxPairs));
+    if (lut) {
+        planes = bits = wide = false;
+        skew = 0;
+        depth = 4;
     }
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
@@ -434,6 +448,13 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         }
     };
     int64_t first = 0;  // first full chunk left to the one-chunk kernels
+    if (lut) {
+        a.chunk_begin = 0;
+        a.n_chunks = full;
+        a.stripe_begin = 0;
+        launch_lut(tu.lds_lut - 1, ntmode == 2, lut_pairs, nstripes * full * a.n_tiles, stream, a);
+        first = full;
+    }
     if (planes) {
         const int64_t n4k = nbytes / kChunkBytes;
         cm.planes()->launch(in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes, n4k,

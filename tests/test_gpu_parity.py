@@ -1195,6 +1195,67 @@ def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
             assert bad.size == 0, (case, s, o, bad[:8], got[s, slot][bad[:8]], ref[o][bad[:8]])
 
 
+@pytest.mark.parametrize("case", ["clay104", "clay42", "rs124", "dense40x24", "ones", "dense8x30"])
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("acc", [False, True])
+def test_lds_lut_kernel_vs_table_product(ecx, torch_dev, case, mode, acc):
+    """k_gf_lut (apply_lut.hip, forced by ecx_tune "lds_lut"): mode 1 (log/antilog tables
+    in LDS) on every map, mode 2 (one product row per coefficient, single-tile maps of
+    <= 256 general coefficients) where it applies, overwriting or accumulating, equals
+    the oracle's table-driven product on every stripe, over whole 4 KiB chunks plus a
+    byte-safe tail; more stripes than one persistent grid covers at once."""
+    from conftest import gf_apply_numpy
+    torch = torch_dev
+    rng = np.random.default_rng(78)
+    if case == "clay104":
+        m, ins, outs = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2).map().matrix()
+    elif case == "clay42":
+        m, ins, outs = ecx.ClayCodeErasureDecodingStep([1], 4, 2).map().matrix()
+    elif case == "rs124":
+        m, ins, outs = ecx.ReedSolomon.create(12, 4).decode_map([False, False] + [True] * 14).matrix()
+    elif case.startswith("dense"):
+        r, c = (int(v) for v in case[5:].split("x"))
+        m = rng.integers(0, 256, (r, c)).astype(np.uint8)
+        ins, outs = np.arange(c), np.arange(r)
+    else:
+        m = np.ones((16, 20), np.uint8)
+        ins, outs = np.arange(20), np.arange(16)
+    m = np.asarray(m)
+    single_tile = len(m) <= 8
+    runs_lut = mode == 1 or (single_tile and int((m > 1).sum()) <= 256)
+    gm = ecx.GfMap.from_matrix(m, in_slot=[int(i) for i in ins], out_slot=[int(o) for o in outs])
+    ni, no = int(max(ins)) + 1, int(max(outs)) + 1
+    S = 3 if case == "clay104" else 700  # Clay(4,2): 700 stripes x 2 chunks > 256 CUs x occupancy
+    L = 4096 * 2 + 112
+    inp = torch.empty((S, ni, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(inp, inp.numel(), 6)
+    host = inp.cpu().numpy()
+    out = torch.empty((S, no, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(out, out.numel(), 7)
+    before = out.cpu().numpy()
+    try:
+        ecx.tune("lds_lut", mode)
+        if acc:
+            gm.accumulate_batch(inp, ni * L, L, out, no * L, L, S, L)
+        else:
+            gm.apply_batch(inp, ni * L, L, out, no * L, L, S, L)
+        torch.cuda.synchronize()
+        kern = ecx.last_kernel()
+    finally:
+        ecx.tune("lds_lut", 0)
+    if runs_lut:
+        assert kern == "k_gf_lut<%d, %s>" % (mode - 1, "true" if single_tile else "false"), kern
+    else:
+        assert not kern.startswith("k_gf_lut"), kern
+    got = out.cpu().numpy()
+    for s in sorted({0, 1, S // 2, S - 1}):
+        ref = gf_apply_numpy(m, [host[s, j] for j in ins])
+        for o, slot in enumerate(outs):
+            want = ref[o] ^ before[s, slot] if acc else ref[o]
+            bad = np.nonzero(got[s, slot] != want)[0]
+            assert bad.size == 0, (case, mode, s, o, bad[:8])
+
+
 @pytest.mark.parametrize("k,m,v,e,B,S", [(4, 2, 0, 1, 4096 * 2 + 112, 3), (4, 2, 0, 4, 4096, 9), (4, 2, 0, 0, 8192, 3),
                                          (10, 4, 2, 3, 4096, 3), (10, 4, 2, 13, 4096 + 16, 3), (10, 4, 2, 9, 4096, 17),
                                          (12, 4, 0, 5, 4096, 3), (12, 4, 0, 15, 8192 + 512, 5), (8, 4, 0, 0, 4096, 3),
