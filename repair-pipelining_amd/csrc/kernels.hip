@@ -343,9 +343,10 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // product rows for single-tile maps of <= kLutMaxPairs general coefficients.  Full
     // 4 KiB chunks of aligned layouts on the depth-4 padded plan; the byte-safe tail
     // runs k_gf_apply on the same plan.
-    int lut_pairs = 0;
-    for (int o = 0; o < cm.map().n_out; ++o)
-        for (int j = 0; j < cm.map().n_in; ++j) lut_pairs += cm.map().at(o, j) > 1;
+    int lut_pairs = 0;  // general coefficients (counted only when the kernel is asked for)
+    if (tu.lds_lut == 2)
+        for (int o = 0; o < cm.map().n_out; ++o)
+            for (int j = 0; j < cm.map().n_in; ++j) lut_pairs += cm.map().at(o, j) > 1;
     const bool lut = tu.lds_lut && aligned && !waves && nbytes >= kChunkBytes && threads == kBlockThreads &&
                      (tu.lds_lut == 1 || (cm.n_tiles() == 1 && lut_pairs <= kLutMaxPairs));
     if (lut) {
