@@ -400,6 +400,42 @@ def test_clay_batch_noncodeword_vs_oracle(ecx, torch_dev):
         assert all((got[s, z] == ref[z]).all() for z in range(8))
 
 
+@pytest.mark.parametrize("k,m", [(2, 2), (4, 2), (3, 3), (6, 2), (6, 3)])
+def test_clay_batch_erasure_patterns_vs_oracle(ecx, torch_dev, k, m):
+    """Non-codeword stripes through the device batch path for many erasure patterns of
+    every size 1..m (all of them for Clay(2,2) and Clay(4,2), 12 random ones per size
+    otherwise): single repairs (doDecodeSingle) and doDecodeMulti's IS-ordered type
+    0/1/2 solves, each equal to the oracle's stage-by-stage run on every stripe."""
+    import itertools
+    torch = torch_dev
+    n = k + m
+    rng = np.random.default_rng(k * 10 + m)
+    pats = []
+    for size in range(1, m + 1):
+        allp = [list(p) for p in itertools.combinations(range(n), size)]
+        if n <= 6:
+            pats += allp
+        else:
+            pats += [allp[i] for i in rng.choice(len(allp), min(12, len(allp)), replace=False)]
+    a = ecx.ClayCodeErasureDecodingStep([0], k, m).subPacketSize
+    B, S = 4096 + 48, 2
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 31 + k + m)
+    host = pool.cpu().numpy()
+    for erased in pats:
+        E = len(erased)
+        out = torch.full((S, E * a, B), 0x5A, dtype=torch.uint8, device="cuda")
+        ecx.ClayCodeErasureDecodingStep(erased, k, m).performCodingBatch(pool, n * a * B, B, out, E * a * B, B, S, B)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for s in range(S):
+            inputs = [None if (i % n) in erased else host[s, i].copy() for i in range(n * a)]
+            ref = [np.zeros(B, np.uint8) for _ in range(E * a)]
+            O.Clay(k, m, erased).perform_coding(inputs, ref, B)
+            for o in range(E * a):
+                assert (got[s, o] == ref[o]).all(), (erased, s, o)
+
+
 def test_clay_batch_unaligned_layout(ecx, torch_dev):
     """Unaligned base/strides take the byte-safe kernel path; results unchanged."""
     torch = torch_dev
