@@ -9,6 +9,8 @@
 //   group  one 256-thread workgroup per (stripe, 512-B slice, 16-plane group): lane row g
 //          of wave w holds plane 4w + g, each load instruction is four 256-B runs
 //          (k_clay_repair_grp's shape, without exchanges or partners).
+//   planesK[_wave]  K consecutive helper planes per workgroup, all 13K loads of a lane in
+//          flight at once, 256-thread workgroups over 4 KiB or one wave over 1 KiB.
 // Each with the identity block order and with a stripe's workgroups on one XCD.  Prints
 // algorithmic GB/s ((832 + 256) x 4 KiB per stripe) as a fraction of 8 TB/s.
 //
@@ -89,6 +91,37 @@ __global__ void __launch_bounds__(256) k_group(const uint8_t *pool, uint8_t *out
         }
 }
 
+// PLANES consecutive helper planes per workgroup (THREADS lanes x 16 B per 4 KiB
+// sub-chunk slice; THREADS = 64: one-wave workgroups over 1 KiB slices), every load of
+// the workgroup issued before the first XOR: more loads in flight per lane than the
+// one-plane shape, as the headline kernel's 20-deep ring has.
+template <int PLANES, int THREADS>
+__global__ void __launch_bounds__(THREADS) k_planes(const uint8_t *pool, uint8_t *out, uint32_t n) {
+    constexpr uint32_t slices = kSub / (THREADS * 16);
+    const uint32_t u = blockIdx.x;
+    const uint32_t per_stripe = (kHelp / PLANES) * slices;
+    const int64_t s = u / per_stripe, q = (u % per_stripe) / slices, sl = u % slices;
+    u32x4 v[PLANES][13];
+#pragma unroll
+    for (int k = 0; k < PLANES; ++k) {
+        const int64_t z = 192 + q * PLANES + k;
+        const uint8_t *in = pool + s * kStripe + z * kNodes * kSub + sl * THREADS * 16 + threadIdx.x * 16;
+#pragma unroll
+        for (int j = 0; j < 13; ++j) v[k][j] = ldnt(in + (int64_t)(j < 3 ? j : j + 1) * kSub);
+    }
+    uint8_t *o = out + s * kOut + sl * THREADS * 16 + threadIdx.x * 16;
+#pragma unroll
+    for (int k = 0; k < PLANES; ++k) {
+        const int64_t p = q * PLANES + k;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            u32x4 a = v[k][r] ^ v[k][r + 4] ^ v[k][r + 8];
+            if (r == 0) a ^= v[k][12];
+            stnt(o + (p + 64 * r) * kSub, a);
+        }
+    }
+}
+
 template <typename F>
 float best_ms(F launch) {
     hipEvent_t e0, e1;
@@ -116,8 +149,8 @@ int main() {
     for (int round = 0; round < 2; ++round) {
         const uint32_t np = (uint32_t)(S * kHelp), ng = (uint32_t)(S * 32);
         const char *names[] = {"plane", "plane_xcd", "group", "group_xcd", "plane_readonly", "plane_out_contig",
-                               "plane_read14"};
-        float ms[7];
+                               "plane_read14", "planes2", "planes4", "plane_wave", "planes2_wave"};
+        float ms[11];
         ms[0] = best_ms([&] { hipLaunchKernelGGL((k_plane<0>), dim3(np), dim3(256), 0, 0, pool, out, np); });
         ms[1] = best_ms([&] { hipLaunchKernelGGL((k_plane<1>), dim3(np), dim3(256), 0, 0, pool, out, np); });
         ms[2] = best_ms([&] { hipLaunchKernelGGL((k_group<0>), dim3(ng), dim3(256), 0, 0, pool, out, ng); });
@@ -125,7 +158,11 @@ int main() {
         ms[4] = best_ms([&] { hipLaunchKernelGGL((k_plane<0, 1>), dim3(np), dim3(256), 0, 0, pool, out, np); });
         ms[5] = best_ms([&] { hipLaunchKernelGGL((k_plane<0, 2>), dim3(np), dim3(256), 0, 0, pool, out, np); });
         ms[6] = best_ms([&] { hipLaunchKernelGGL((k_plane<0, 3>), dim3(np), dim3(256), 0, 0, pool, out, np); });
-        for (int i = 0; i < 7; ++i) {
+        ms[7] = best_ms([&] { hipLaunchKernelGGL((k_planes<2, 256>), dim3(np / 2), dim3(256), 0, 0, pool, out, np / 2); });
+        ms[8] = best_ms([&] { hipLaunchKernelGGL((k_planes<4, 256>), dim3(np / 4), dim3(256), 0, 0, pool, out, np / 4); });
+        ms[9] = best_ms([&] { hipLaunchKernelGGL((k_planes<1, 64>), dim3(np * 4), dim3(64), 0, 0, pool, out, np * 4); });
+        ms[10] = best_ms([&] { hipLaunchKernelGGL((k_planes<2, 64>), dim3(np * 2), dim3(64), 0, 0, pool, out, np * 2); });
+        for (int i = 0; i < 11; ++i) {
             // read-only: the 832 read sub-chunks only; read14: 896 read + 256 written
             const double b = i == 4 ? (double)S * 832 * kSub : (i == 6 ? (double)S * (896 + 256) * kSub : bytes);
             printf("{\"round\": %d, \"shape\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", round,
