@@ -85,6 +85,9 @@
  *   "planes_lookahead" that kernel's load schedule: inputs in flight ahead of the one being
  *                      computed, 0..15 (default 12)
  *   "planes_waves"     that kernel's __launch_bounds__ minimum waves per SIMD, 1..4 (default 2)
+ *   "roctx"            1 = a roctx range named after the entry point around every C-ABI call that
+ *                      can fail (shown by `rocprofv3 --marker-trace`; also ECX_ROCTX=1 in the
+ *                      environment at load), 0 = none (default)
  *   "host_chunk_kib"   host-memory batches: input KiB per pipelined H2D chunk (default 65536)
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered

@@ -1,6 +1,9 @@
 // ecx_api.cpp -- the C ABI (include/ecx.h).  Translates planner/HIP errors into
 // ecx_status codes; every arithmetic entry point executes on the HIP device.
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
+#include <dlfcn.h>
 #include <list>
 #include <map>
 #include <memory>
@@ -42,8 +45,48 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// roctx ranges around the entry points (ecx_tune "roctx", or ECX_ROCTX=1 in the
+// environment): `rocprofv3 --marker-trace` then shows which call issued which kernels.
+// The marker library is opened on first use; without it the ranges are no-ops.
+struct Roctx {
+    int (*push)(const char *) = nullptr;
+    int (*pop)() = nullptr;
+};
+const Roctx &roctx_lib() {
+    static const Roctx r = [] {
+        Roctx x;
+        void *h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            x.push = reinterpret_cast<int (*)(const char *)>(dlsym(h, "roctxRangePushA"));
+            x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+            if (!x.push || !x.pop) x = Roctx{};
+        }
+        return x;
+    }();
+    return r;
+}
+std::atomic<int> g_roctx{[] {
+    const char *e = std::getenv("ECX_ROCTX");
+    return e && e[0] == '1' ? 1 : 0;
+}()};
+
+struct Range {
+    const Roctx *lib = nullptr;
+    explicit Range(const char *name) {
+        if (g_roctx.load(std::memory_order_relaxed) && roctx_lib().push) {
+            lib = &roctx_lib();
+            lib->push(name);
+        }
+    }
+    ~Range() {
+        if (lib) lib->pop();
+    }
+};
+
 template <class F>
-int guarded(F &&f) {
+int guarded(const char *name, F &&f) {
+    Range range(name);
     try {
         return f();
     } catch (const Error &e) {
@@ -181,7 +224,7 @@ int ecx_version(void) { return 100; }
 
 // ---------------------------------------------------------------- device
 int ecx_device_count(int *count) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         int n = 0;
         check_hip(hipGetDeviceCount(&n), "hipGetDeviceCount");
         *count = n;
@@ -190,14 +233,14 @@ int ecx_device_count(int *count) {
 }
 
 int ecx_set_device(int device) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         check_hip(hipSetDevice(device), "hipSetDevice");
         return ECX_OK;
     });
 }
 
 int ecx_synchronize(void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         check_hip(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
         return ECX_OK;
     });
@@ -207,11 +250,11 @@ int ecx_synchronize(void *stream) {
 int ecx_gf_multiply(int a, int b) { return Field::get().mul((uint8_t)a, (uint8_t)b); }
 
 int ecx_gf_divide(int a, int b) {
-    return guarded([&]() -> int { return (int)Field::get().div((uint8_t)a, (uint8_t)b); });
+    return guarded(__func__, [&]() -> int { return (int)Field::get().div((uint8_t)a, (uint8_t)b); });
 }
 
 int ecx_gf_exp(int a, int n) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (n < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative exponent");
         return (int)Field::get().pow((uint8_t)a, n);
     });
@@ -229,7 +272,7 @@ int ecx_gf_tables(int16_t *log_table, uint8_t *exp_table, uint8_t *mul_table) {
 }
 
 int ecx_matrix_times(const uint8_t *a, int ar, int ac, const uint8_t *b, int br, int bc, uint8_t *out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         Matrix A(ar, ac), B(br, bc);
         std::memcpy(A.row(0), a, (size_t)ar * ac);
         std::memcpy(B.row(0), b, (size_t)br * bc);
@@ -240,7 +283,7 @@ int ecx_matrix_times(const uint8_t *a, int ar, int ac, const uint8_t *b, int br,
 }
 
 int ecx_matrix_invert(const uint8_t *m, int n, uint8_t *out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         Matrix A(n, n);
         std::memcpy(A.row(0), m, (size_t)n * n);
         Matrix I = A.inverse();
@@ -252,7 +295,7 @@ int ecx_matrix_invert(const uint8_t *m, int n, uint8_t *out) {
 // ---------------------------------------------------------------- CodingLoop
 int ecx_code_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inputs, int input_count,
                          uint8_t *const *outputs, int output_count, int offset, int byte_count) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (input_count <= 0 || output_count < 0 || offset < 0 || byte_count < 0)
             throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
         const std::shared_ptr<CompiledMap> cm = cached_plan(dense_map(matrix_rows, output_count, input_count).pruned());
@@ -266,7 +309,7 @@ int ecx_check_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inpu
                           const uint8_t *const *to_check, int check_count, int offset, int byte_count,
                           uint8_t *temp_buffer) {
     (void)temp_buffer;
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (input_count <= 0 || check_count < 0 || offset < 0 || byte_count < 0)
             throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
         // row o: sum_i M[o][i]*in[i] + 1*to_check[o] == 0  <=>  to_check[o] is correct
@@ -290,7 +333,7 @@ int ecx_check_some_shards(const uint8_t *matrix_rows, const uint8_t *const *inpu
 
 int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *input, int index, uint8_t *output,
                     int output_index, int offset, int byte_count, int is_first_time) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (index < 0 || index >= row_length || output_index < 0) throw Error(ECX_E_INDEX, "matrix index");
         if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
         const uint8_t c = matrix_rows[(size_t)output_index * row_length + index];
@@ -305,7 +348,7 @@ int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *i
 
 // ---------------------------------------------------------------- ReedSolomon
 int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         *out = nullptr;
         *out = new ecx_rs(data_shards, parity_shards);
         return ECX_OK;
@@ -321,7 +364,7 @@ int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out) {
 }
 
 int ecx_rs_encode_map(ecx_rs *rs, const ecx_map **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         std::lock_guard<std::mutex> lk(rs->mu);
         if (!rs->enc) rs->enc = std::make_unique<ecx_map>(rs->code.encode_map());
         *out = rs->enc.get();
@@ -330,7 +373,7 @@ int ecx_rs_encode_map(ecx_rs *rs, const ecx_map **out) {
 }
 
 int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         std::vector<bool> present = present_vec(shard_present, rs->code.n());
         int np = 0;
         for (bool b : present) np += b;
@@ -342,7 +385,7 @@ int ecx_rs_decode_map(ecx_rs *rs, const uint8_t *shard_present, const ecx_map **
 
 int ecx_rs_encode_parity_batch(ecx_rs *rs, uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
                                int64_t nstripes, int64_t offset, int64_t byte_count, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (nstripes < 0 || offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!base) throw Error(ECX_E_NULL, "null device pointer");
         const ecx_map *m = nullptr;
@@ -357,7 +400,7 @@ int ecx_rs_encode_parity_batch(ecx_rs *rs, uint8_t *base, int64_t stripe_stride,
 int ecx_rs_decode_missing_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base, int64_t stripe_stride,
                                 int64_t shard_stride, int64_t nstripes, int64_t offset, int64_t byte_count,
                                 void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (nstripes < 0 || offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!base) throw Error(ECX_E_NULL, "null device pointer");
         const ecx_map *m = nullptr;
@@ -372,7 +415,7 @@ int ecx_rs_decode_missing_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_
 
 int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int offset,
                          int byte_count) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         check_buffers(rs->code, shards, shard_count, shard_length, offset, byte_count);
         const ecx_map *m = nullptr;
         int st = ecx_rs_encode_map(rs, &m);
@@ -384,7 +427,7 @@ int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, in
 
 int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *output, int input_index,
                                 int output_index, int offset, int byte_count) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         const RsCode &c = rs->code;
         if (output_index < 0 || output_index >= c.m() || input_index < 0 || input_index >= c.k())
             throw Error(ECX_E_INDEX, "parity row / column index");
@@ -400,7 +443,7 @@ int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *outpu
 
 int ecx_rs_is_parity_correct(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int first_byte,
                              int byte_count, uint8_t *temp_buffer, int temp_length) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         check_buffers(rs->code, shards, shard_count, shard_length, first_byte, byte_count);
         if (temp_buffer && (long long)temp_length < (long long)first_byte + byte_count)
             throw Error(ECX_E_ILLEGAL_ARGUMENT, "tempBuffer is not big enough");
@@ -429,7 +472,7 @@ int ecx_rs_is_parity_correct(ecx_rs *rs, uint8_t *const *shards, int shard_count
 
 int ecx_rs_decode_missing(ecx_rs *rs, uint8_t *const *shards, const uint8_t *shard_present, int shard_count,
                           int shard_length, int offset, int byte_count) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         check_buffers(rs->code, shards, shard_count, shard_length, offset, byte_count);
         std::vector<bool> present = present_vec(shard_present, rs->code.n());
         int np = 0;
@@ -446,7 +489,7 @@ int ecx_rs_decode_missing_single(ecx_rs *rs, const uint8_t *shard, int shard_ind
                                  const uint8_t *shard_present, uint8_t *const *outputs, int output_count, int offset,
                                  int byte_count, int is_first) {
     (void)shard_index;
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         const RsCode &c = rs->code;
         std::vector<bool> present = present_vec(shard_present, c.n());
         int np = 0;
@@ -485,7 +528,7 @@ int ecx_rs_decode_missing_single(ecx_rs *rs, const uint8_t *shard, int shard_ind
 // ---------------------------------------------------------------- maps
 int ecx_map_create(const uint8_t *matrix, int n_out, int n_in, const int *in_slot, const int *out_slot,
                    ecx_map **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         *out = nullptr;
         if (n_out < 0 || n_in <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "map shape");
         LinearMap lm = dense_map(matrix, n_out, n_in);
@@ -521,7 +564,7 @@ int ecx_map_matrix(const ecx_map *map, uint8_t *matrix, int *in_slot, int *out_s
 int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                         uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                         int64_t byte_count, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
         launch_apply(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
@@ -533,7 +576,7 @@ int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe
 int ecx_map_accumulate_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                              uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                              int64_t byte_count, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
         launch_apply(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
@@ -563,7 +606,7 @@ int ecx_rs_decode_partial_batch(ecx_rs *rs, const uint8_t *shard_present, int sh
                                 int64_t in_stripe_stride, uint8_t *acc, int64_t acc_stripe_stride,
                                 int64_t acc_row_stride, int64_t nstripes, int64_t byte_count, int is_first,
                                 void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         const RsCode &c = rs->code;
         if (shard_index < 0 || shard_index >= c.n()) throw Error(ECX_E_INDEX, "shard index");
         std::vector<bool> present = present_vec(shard_present, c.n());
@@ -592,7 +635,7 @@ int ecx_rs_decode_partial_batch(ecx_rs *rs, const uint8_t *shard_present, int sh
 int ecx_rs_encode_partial_batch(ecx_rs *rs, int input_index, const uint8_t *in, int64_t in_stripe_stride,
                                 uint8_t *acc, int64_t acc_stripe_stride, int64_t acc_row_stride, int64_t nstripes,
                                 int64_t byte_count, int is_first, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         const RsCode &c = rs->code;
         if (input_index < 0 || input_index >= c.k()) throw Error(ECX_E_INDEX, "data shard index");
         ecx_map *part;
@@ -620,7 +663,7 @@ int ecx_rs_encode_partial_batch(ecx_rs *rs, int input_index, const uint8_t *in, 
 
 // ---------------------------------------------------------------- Clay
 int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_erased, ecx_clay **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         *out = nullptr;
         if (n_erased < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased");
         *out = new ecx_clay(data_units, parity_units, std::vector<int>(erased, erased + n_erased));
@@ -630,7 +673,7 @@ int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_e
 
 int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
                               ecx_clay **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         *out = nullptr;
         if (n_erased < 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased / virtual_units");
         *out = new ecx_clay(data_units, parity_units, std::vector<int>(erased, erased + n_erased), virtual_units);
@@ -648,7 +691,7 @@ int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha) {
 }
 
 int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         std::vector<int> h = clay->pl.helper_planes(erased_index);
         std::copy(h.begin(), h.end(), out);
         return (int)h.size();
@@ -656,7 +699,7 @@ int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out) {
 }
 
 int ecx_clay_perform_coding(ecx_clay *clay, const uint8_t *const *inputs, uint8_t *const *outputs, int buf_size) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (clay->pl.erased().empty()) return ECX_OK;
         if (buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "buf_size");
         const int w = clay->pl.n_real() * clay->pl.alpha();
@@ -676,7 +719,7 @@ int ecx_clay_perform_coding(ecx_clay *clay, const uint8_t *const *inputs, uint8_
 
 int ecx_clay_decode_single_helper(ecx_clay *clay, const uint8_t *const *helper_coupled, int helper_i,
                                   uint8_t *const *outputs, int erased_index, int buf_size) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "buf_size");
         const int nh = (int)clay->pl.helper_planes(erased_index).size();
         const int w = nh * clay->pl.n_real();
@@ -695,7 +738,7 @@ int ecx_clay_decode_single_helper(ecx_clay *clay, const uint8_t *const *helper_c
 }
 
 int ecx_clay_map(ecx_clay *clay, const ecx_map **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         *out = clay_standard_map(clay);
         return ECX_OK;
     });
@@ -724,7 +767,7 @@ ClayRtc *clay_rtc(ecx_clay *clay) {
 int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride, int64_t in_sub_stride,
                                   uint8_t *out, int64_t out_stripe_stride, int64_t out_sub_stride, int64_t nstripes,
                                   int64_t buf_size, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (clay->pl.erased().empty()) return ECX_OK;
         if (nstripes < 0 || buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!in || !out) throw Error(ECX_E_NULL, "null device pointer");
@@ -759,7 +802,7 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
 }
 
 int ecx_clay_rtc_compile_check(ecx_clay *clay) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         ClayRtc *r = clay_rtc(clay);
         if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
         return (int)rtc_compile_check(clay_rtc_selected_source(r->program()));
@@ -767,7 +810,7 @@ int ecx_clay_rtc_compile_check(ecx_clay *clay) {
 }
 
 int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         ClayRtc *r = clay_rtc(clay);
         if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
         const std::string src = clay_rtc_selected_source(r->program());
@@ -777,7 +820,7 @@ int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
 }
 
 int ecx_map_planes_compile_check(const ecx_map *map, int accumulate) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         PlanesShape sh;
         sh.lookahead = tuning().planes_lookahead;
         sh.waves = tuning().planes_waves;
@@ -786,7 +829,7 @@ int ecx_map_planes_compile_check(const ecx_map *map, int accumulate) {
 }
 
 int ecx_map_planes_source(const ecx_map *map, int accumulate, char *buf, int len) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         PlanesShape sh;
         sh.lookahead = tuning().planes_lookahead;
         sh.waves = tuning().planes_waves;
@@ -811,7 +854,7 @@ LrcCache *lrc_cache() {
 }  // namespace
 
 int ecx_lrc_map(const uint8_t *block_present, const ecx_map **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (!out) throw Error(ECX_E_NULL, "null out pointer");
         LrcCache &c = *lrc_cache();
         std::lock_guard<std::mutex> lk(c.mu);
@@ -857,7 +900,7 @@ int ecx_lrc_decode_batch(uint8_t *stripes, int64_t stripe_stride, int64_t block_
 int ecx_map_apply_batch_host(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                              uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                              int64_t byte_count) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!in || !out) throw Error(ECX_E_NULL, "null host pointer");
         run_host_batch(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
@@ -869,7 +912,7 @@ int ecx_map_apply_batch_host(const ecx_map *map, const uint8_t *in, int64_t in_s
 int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
                                        int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
                                        int64_t out_sub_stride, int64_t nstripes, int64_t buf_size) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (clay->pl.erased().empty()) return ECX_OK;
         if (nstripes < 0 || buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         if (!in || !out) throw Error(ECX_E_NULL, "null host pointer");
@@ -881,7 +924,7 @@ int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_
 }
 
 int ecx_host_alloc(int64_t nbytes, void **out) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (!out) throw Error(ECX_E_NULL, "null out pointer");
         if (nbytes < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative size");
         *out = nullptr;
@@ -891,14 +934,14 @@ int ecx_host_alloc(int64_t nbytes, void **out) {
 }
 
 int ecx_host_free(void *ptr) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (ptr) check_hip(hipHostFree(ptr), "hipHostFree");
         return ECX_OK;
     });
 }
 
 int ecx_host_register(void *ptr, int64_t nbytes) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (!ptr) throw Error(ECX_E_NULL, "null pointer");
         if (nbytes <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "non-positive size");
         check_hip(hipHostRegister(ptr, (size_t)nbytes, hipHostRegisterDefault), "hipHostRegister");
@@ -907,7 +950,7 @@ int ecx_host_register(void *ptr, int64_t nbytes) {
 }
 
 int ecx_host_unregister(void *ptr) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         if (!ptr) throw Error(ECX_E_NULL, "null pointer");
         check_hip(hipHostUnregister(ptr), "hipHostUnregister");
         return ECX_OK;
@@ -1012,6 +1055,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.bitslice = value;
     }
+    else if (k == "roctx") {
+        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        g_roctx.store(value);
+    }
     else if (k == "lds_lut") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.lds_lut = value;
@@ -1025,14 +1072,14 @@ int ecx_tune(const char *key, int value) {
 }
 
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         launch_probe(kind, src, dst, nbytes, nontemporal != 0, (hipStream_t)stream);
         return ECX_OK;
     });
 }
 
 int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         const CompiledMap &cm = map->cm;
         if (n_tiles) *n_tiles = cm.n_tiles();
         if (n_entries) *n_entries = cm.n_tiles() ? cm.n_entries() : 0;
@@ -1050,7 +1097,7 @@ int ecx_last_kernel(char *buf, int len) {
 }
 
 int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         const CompiledMap &cm = map->cm;
         const LinearMap &m = cm.map();
         const int64_t len = 97;  // ragged on purpose
@@ -1128,7 +1175,7 @@ int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
 
 // ---------------------------------------------------------------- synthetic data / verification
 int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         launch_fill_random(dst, nbytes, seed, (hipStream_t)stream);
         return ECX_OK;
     });
@@ -1136,7 +1183,7 @@ int ecx_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, void *stream) {
 
 int ecx_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
                        int64_t row_bytes, uint64_t *d_count, void *stream) {
-    return guarded([&]() -> int {
+    return guarded(__func__, [&]() -> int {
         launch_count_mismatch(a, a_stride, b, b_stride, nrows, row_bytes, d_count, (hipStream_t)stream);
         return ECX_OK;
     });
