@@ -10,6 +10,8 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <string>
 #include <functional>
 #include <random>
 #include <vector>
@@ -32,6 +34,14 @@ static double median_us(const std::function<int()> &call, int reps = 300) {
 }
 
 int main() {
+    // PERCALL_SCHED=spin|yield|blocking: the HIP device scheduling flag, set before any
+    // HIP call (how the host thread waits in hipStreamSynchronize); unset = the default.
+    if (const char *m = std::getenv("PERCALL_SCHED")) {
+        const std::string s = m;
+        const unsigned f = s == "spin" ? hipDeviceScheduleSpin : s == "yield" ? hipDeviceScheduleYield
+                         : s == "blocking" ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+        if (hipSetDeviceFlags(f) != hipSuccess) return 2;
+    }
     std::mt19937 rng(7);
     auto fill = [&](std::vector<uint8_t> &v) {
         for (auto &b : v) b = (uint8_t)rng();
