@@ -478,6 +478,42 @@ def test_rs124_two_erasure_batch_roundtrip(ecx, torch_dev):
     assert all((b[i] == host[i]).all() for i in range(12, 16))
 
 
+def test_rs124_random_erasure_pairs(ecx, torch_dev):
+    """BASELINE config 5's "plus random pairs" (SURVEY.md 8(d)): RS(12,4) decodeMissing of
+    random erasure pairs -- data+data, data+parity, parity+parity -- in place on valid
+    stripes restores every shard; on non-codeword stripes it equals the oracle's
+    decodeMissing (first-k-present rule) on a window that includes the ragged tail."""
+    torch = torch_dev
+    k, m, S = 12, 4, 2
+    L, P = (1 << 20) + 208, (1 << 20) + 4096
+    rs = ecx.ReedSolomon.create(k, m)
+    rng = np.random.default_rng(124)
+    pairs = [(0, 5), (3, 14), (12, 15), (7, 11), (1, 13)]
+    pairs += [tuple(sorted(rng.choice(16, 2, replace=False).tolist())) for _ in range(5)]
+    pool = torch.empty((S, 16, P), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 41)
+    rs.encode_map().apply_batch(pool, 16 * P, P, pool, 16 * P, P, S, L)
+    noise = torch.empty_like(pool)
+    ecx.fill_random(noise, noise.numel(), 42)
+    torch.cuda.synchronize()
+    for pair in pairs:
+        present = [i not in pair for i in range(16)]
+        work = pool.clone()
+        for i in pair:
+            work[:, i, :L] = 0
+        rs.decode_map(present).apply_batch(work, 16 * P, P, work, 16 * P, P, S, L)
+        torch.cuda.synchronize()
+        assert torch.equal(work[:, :, :L], pool[:, :, :L]), pair
+        nc = noise.clone()
+        rs.decode_map(present).apply_batch(nc, 16 * P, P, nc, 16 * P, P, S, L)
+        torch.cuda.synchronize()
+        w0 = L - 3000
+        b = [x.copy() for x in noise[1, :, w0:L].cpu().numpy()]
+        O.ReedSolomon(k, m).decode_missing(b, present, 0, L - w0)
+        got = nc[1, :, w0:L].cpu().numpy()
+        assert all((b[i] == got[i]).all() for i in range(16)), pair
+
+
 @pytest.mark.parametrize("L", [(1 << 20) + 1008, 4 << 20])
 def test_rs124_padded_pitch_one_wave_auto(ecx, torch_dev, L):
     """RS(12,4) decode on a padded shard pitch (4 MiB + 4 KiB style) runs on one-wave
