@@ -1,0 +1,85 @@
+"""Host logic of bench.py (no GPU): the kernel-source hash families behind
+roofline.traffic, the staleness rules of pmc_traffic(), the --gpus / WORLD_SIZE guard,
+and the self-launch of N ranks propagating a failing rank's status."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+
+def test_source_hash_families_are_separate_and_stable():
+    """Each kernel family hashes its own sources: a change to the generated Clay kernels
+    does not stale the composed-map profile, and the other way round."""
+    composed = bench.kernel_source_hash("k_gf_apply<false, true, 1, 20, false, 256, 8>")
+    assert composed == bench.kernel_source_hash("k_gf_apply_wide<false, true, 1, 8>")
+    assert composed == bench.kernel_source_hash("k_gf_lut<0, true>")  # launch_apply can pick it
+    clay = bench.kernel_source_hash("k_clay_repair_grp")
+    planes = bench.kernel_source_hash("k_map_planes")
+    assert len({composed, clay, planes}) == 3
+    assert all(len(h) == 16 for h in (composed, clay, planes))
+    assert clay == bench.kernel_source_hash("k_clay_repair_grp")
+    # every source a family names exists (a renamed file must not silently drop out)
+    for name in bench.COMMON_SOURCES + bench.COMPOSED_SOURCES + bench.RTC_SOURCES + bench.PLANES_SOURCES:
+        assert (ROOT / "repair-pipelining_amd" / "csrc" / name).is_file(), name
+
+
+def test_committed_pmc_profile_matches_current_sources():
+    """profiles/pmc_traffic.json was taken on the sources in this tree for every bench
+    workload, so the bench line carries measured traffic (not a stale constant)."""
+    d = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())["workloads"]
+    assert set(d) >= {"clay42", "clay104", "rs124", "lrc", "clay42x2"}
+    stale = [w for w, e in d.items() if bench.pmc_traffic(w, e["pool_stripes"], e["kernel"])[1] is not None]
+    if stale:  # kernel sources edited since the last PMC pass: the bench reports traffic null until re-profiled
+        pytest.skip("PMC profile stale for %s: re-run scripts/pmc.sh + scripts/pmc_summary.py on a GPU" % stale)
+    for w, e in d.items():
+        traffic, note = bench.pmc_traffic(w, e["pool_stripes"], e["kernel"])
+        assert note is None and traffic == e["hbm_bytes_per_launch"], (w, note)
+        # within 2 % of the algorithmic bytes: no wasted re-reads on any workload
+        assert 1.0 <= traffic / e["algorithmic_bytes_per_launch"] < 1.02, w
+
+
+def test_pmc_traffic_staleness_rules(monkeypatch):
+    d = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())["workloads"]["clay42"]
+    pool, kernel = d["pool_stripes"], d["kernel"]
+    assert bench.pmc_traffic("clay42", pool, kernel)[0] == d["hbm_bytes_per_launch"]
+    assert bench.pmc_traffic("clay42", pool * 2, kernel) == (
+        None, "stale: PMC profile taken on another pool size or kernel instance")
+    assert bench.pmc_traffic("no_such_workload", pool, kernel) == (None, "no PMC profile for this workload")
+    monkeypatch.setattr(bench, "kernel_source_hash", lambda kernel="": "0" * 16)
+    assert bench.pmc_traffic("clay42", pool, kernel) == (None, "stale: PMC profile taken on other kernel sources")
+
+
+def _run_bench(args, env_extra, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, env=env, capture_output=True, text=True,
+                          timeout=timeout, cwd=str(ROOT))
+
+
+def test_gpus_must_match_world_size():
+    """Under an external launcher, a --gpus that differs from WORLD_SIZE is refused
+    before anything touches a device (a scaling record must never measure fewer GPUs
+    than it claims)."""
+    r = _run_bench(["--gpus", "2"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert r.returncode != 0
+    assert "--gpus 2 but WORLD_SIZE=3" in r.stderr
+
+
+def test_self_launch_propagates_a_failing_rank():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks through torch.distributed.run
+    as a child process; with no usable GPU here every rank fails, and the failure must
+    reach the exit status (not a silent one-GPU line)."""
+    import torch
+    if torch.cuda.device_count() > 0:  # counting devices does not initialise HIP on this image
+        pytest.skip("a GPU is visible: the ranks would run the real bench")
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--cpu-seconds", "0", "--no-probes"],
+                   {"ECX_BENCH_BACKEND": "gloo", "MASTER_ADDR": "127.0.0.1"})
+    assert r.returncode != 0
+    assert '"n_gpus"' not in r.stdout
