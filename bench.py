@@ -499,7 +499,11 @@ def main():
     local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # Under a launcher (WORLD_SIZE set) the process group is created even for one rank, so
+    # `torch.distributed.run --nproc-per-node 1` rehearses the RCCL init, barriers and
+    # max-reduction of the N-GPU path on a one-GPU box; a plain `python bench.py` has none.
+    grouped = "WORLD_SIZE" in os.environ
+    if grouped:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
@@ -544,7 +548,7 @@ def main():
     stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps * passes)]
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -556,10 +560,10 @@ def main():
             evs[i][1].record(stream)
             i += 1
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if grouped:
         t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -625,7 +629,7 @@ def main():
             "verified": verified,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 
