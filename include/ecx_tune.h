@@ -85,6 +85,9 @@
  *   "planes_lookahead" that kernel's load schedule: inputs in flight ahead of the one being
  *                      computed, 0..15 (default 12)
  *   "planes_waves"     that kernel's __launch_bounds__ minimum waves per SIMD, 1..4 (default 2)
+ *   "host_contexts"    per-call host entry points: 1 = each call leases a free context (stream and
+ *                      staging areas) of the device, so calls from several threads overlap (default);
+ *                      0 = one context per device, calls serialised
  *   "roctx"            1 = a roctx range named after the entry point around every C-ABI call that
  *                      can fail (shown by `rocprofv3 --marker-trace`; also ECX_ROCTX=1 in the
  *                      environment at load), 0 = none (default)

@@ -1055,6 +1055,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.bitslice = value;
     }
+    else if (k == "host_contexts") {
+        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        t.host_contexts = value;
+    }
     else if (k == "roctx") {
         if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
         g_roctx.store(value);

@@ -658,20 +658,44 @@ const std::vector<int> &CompiledMap::used_out_slots() {
 }
 
 // ---------------------------------------------------------------- contexts
-DeviceContext &DeviceContext::current() {
+DeviceContext::Lease DeviceContext::acquire() {
     static std::mutex reg_mu;
-    static std::map<int, std::unique_ptr<DeviceContext>> reg;
+    static std::map<int, std::vector<std::unique_ptr<DeviceContext>>> reg;  // never shrinks: reused
+    thread_local DeviceContext *last = nullptr;  // this thread's previous lease: usually still free
     int dev = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
-    std::lock_guard<std::mutex> lk(reg_mu);
-    auto &slot = reg[dev];
-    if (!slot) {
-        auto ctx = std::make_unique<DeviceContext>();
-        ctx->device = dev;
-        check_hip(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
-        slot = std::move(ctx);
+    const bool pool = tuning().host_contexts != 0;
+    if (pool && last && last->device == dev) {
+        std::unique_lock<std::mutex> l(last->mu, std::try_to_lock);
+        if (l.owns_lock()) return Lease{last, std::move(l)};
     }
-    return *slot;
+    DeviceContext *shared = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(reg_mu);
+        auto &v = reg[dev];
+        if (pool) {
+            for (auto &c : v) {  // a free context of this device (try_lock never blocks under reg_mu)
+                std::unique_lock<std::mutex> l(c->mu, std::try_to_lock);
+                if (l.owns_lock()) {
+                    last = c.get();
+                    return Lease{c.get(), std::move(l)};
+                }
+            }
+        } else if (!v.empty()) {
+            shared = v.front().get();
+        }
+        if (!shared) {  // every context busy (or none yet): a new one, leased before it is published
+            auto ctx = std::make_unique<DeviceContext>();
+            ctx->device = dev;
+            check_hip(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
+            DeviceContext *c = ctx.get();
+            std::unique_lock<std::mutex> l(c->mu);
+            v.push_back(std::move(ctx));
+            last = c;
+            return Lease{c, std::move(l)};
+        }
+    }
+    return Lease{shared, std::unique_lock<std::mutex>(shared->mu)};  // one shared context: wait for it
 }
 
 uint8_t *DeviceContext::ensure(size_t bytes) {
@@ -756,8 +780,8 @@ const uint8_t *run_gathered(DeviceContext &ctx, CompiledMap &cm, const uint8_t *
 void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
               int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return;
-    DeviceContext &ctx = DeviceContext::current();
-    std::lock_guard<std::mutex> lk(ctx.mu);
+    DeviceContext::Lease lease = DeviceContext::acquire();
+    DeviceContext &ctx = *lease.ctx;
     const int64_t zc_pitch = (byte_count + 255) / 256 * 256;
     void *zc_dev = nullptr;
     bool zero_copy = byte_count <= tuning().host_gather_max && tuning().host_zero_copy;
@@ -822,8 +846,8 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
 
 bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return true;
-    DeviceContext &ctx = DeviceContext::current();
-    std::lock_guard<std::mutex> lk(ctx.mu);
+    DeviceContext::Lease lease = DeviceContext::acquire();
+    DeviceContext &ctx = *lease.ctx;
     uint64_t *cnt = ctx.counter();
     check_hip(hipMemsetAsync(cnt, 0, sizeof(uint64_t), ctx.stream), "hipMemsetAsync");
     if (byte_count <= tuning().host_gather_max) {

@@ -256,6 +256,7 @@ struct Tuning {
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
     int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the
                                           // used slots into pinned staging (one H2D / one D2H)
+    int host_contexts = 1;  // per-call host APIs: 1 = a pool of contexts (streams) leased per call, 0 = one per device
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 Tuning &tuning();
@@ -285,11 +286,20 @@ void launch_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, hipStream_t
 void launch_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
                            int64_t row_bytes, uint64_t *d_count, hipStream_t stream);
 
-// Per-device context for the host (byte[][]) entry points: one stream and a
-// growable staging area, serialised by a mutex.
+// Per-device contexts for the host (byte[][]) entry points: a stream and growable
+// device / pinned staging areas each.  A call leases a free context of the current
+// device for its duration (acquire), so calls from different threads run on different
+// streams and overlap; a new context is created only when every existing one is busy,
+// so their number follows the peak concurrency, not the thread count (a JVM thread pool
+// that replaces its threads creates none).  Tuning::host_contexts 0 = one shared,
+// serialised context per device.
 class DeviceContext {
 public:
-    static DeviceContext &current();
+    struct Lease {
+        DeviceContext *ctx;
+        std::unique_lock<std::mutex> lk;
+    };
+    static Lease acquire();
     std::mutex mu;
     hipStream_t stream = nullptr;
     int device = 0;

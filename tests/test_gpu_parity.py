@@ -822,14 +822,17 @@ def test_per_call_paths_agree(ecx, L):
         ecx.tune("host_zero_copy", 1)
 
 
-def test_per_call_concurrent_threads(ecx):
+@pytest.mark.parametrize("contexts", [1, 0])
+def test_per_call_concurrent_threads(ecx, contexts):
     """The reference's callers are per-process pub/sub threads (SURVEY.md section 8b,
     "Threading"); the C ABI is documented thread-safe.  Eight host threads call the
     per-call entry points at once -- two sharing one RS(4,2) codec, the others with
     their own RS or Clay(4,2) objects -- over sizes that take the zero-copy gather
     path (4 KiB, 32 KiB) and the per-slot copy path (300,000 B); every result must be
-    the oracle's."""
+    the oracle's, with contexts leased per call (host_contexts 1: calls overlap on
+    separate streams) and with one shared context (0)."""
     import threading
+    ecx.tune("host_contexts", contexts)
 
     sizes = (4096, 32768, 300000)
     rng = np.random.default_rng(99)
@@ -889,6 +892,7 @@ def test_per_call_concurrent_threads(ecx):
         t.start()
     for t in threads:
         t.join(timeout=90)
+    ecx.tune("host_contexts", 1)
     assert not any(t.is_alive() for t in threads), "a worker thread hung"
     assert not errors, errors[:5]
 
