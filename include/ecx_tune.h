@@ -95,7 +95,7 @@
  *   "host_buffers"     host-memory batches: device buffer sets in flight, 1..8 (default 3)
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered
  *                      through pinned staging (one H2D / one D2H); 0 = always per-slot copies
- *                      (default 256)
+ *                      (default 512)
  *   "host_zero_copy"   per-call host entry points on the gather path: 1 = the kernel reads and
  *                      writes the pinned staging area over PCIe (no DMA copies; default);
  *                      0 = one H2D and one D2H copy

@@ -254,8 +254,10 @@ struct Tuning {
     int planes_waves = 2;      // its __launch_bounds__ minimum waves per SIMD, 1..4
     int64_t host_chunk = 64 << 20;  // host-batch pipeline: input bytes per H2D chunk
     int host_buffers = 3;           // host-batch pipeline: device buffer sets in flight
-    int64_t host_gather_max = 256 << 10;  // per-call host APIs: byte counts up to this gather the
-                                          // used slots into pinned staging (one H2D / one D2H)
+    // per-call host APIs: byte counts up to this gather the used slots into pinned staging (one
+    // H2D / one D2H); above it the runtime copies each slot (512 KiB: the crossover of the two,
+    // profiles/r02_percall_sizes.jsonl)
+    int64_t host_gather_max = 512 << 10;
     int host_contexts = 1;  // per-call host APIs: 1 = a pool of contexts (streams) leased per call, 0 = one per device
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);

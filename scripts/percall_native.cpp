@@ -140,6 +140,29 @@ int main() {
         (void)hipFree(d_acc);
         ecx_rs_destroy(rs31);
     }
+    // Large per-call buffers (the byte[][] API on BASELINE config 5's shape): RS(12,4)
+    // encodeParity and a 2-erasure decodeMissing over 16 x L host shards; algorithmic
+    // GB/s = (12 read + 4 or 2 written) x L per call.
+    {
+        ecx_rs *rs124 = nullptr;
+        if (ecx_rs_create(12, 4, &rs124)) return 1;
+        for (int L : {1 << 20, 4 << 20}) {
+            std::vector<std::vector<uint8_t>> sh(16, std::vector<uint8_t>(L));
+            for (auto &s : sh) fill(s);
+            std::vector<uint8_t *> p(16);
+            for (int i = 0; i < 16; ++i) p[i] = sh[i].data();
+            uint8_t present[16];
+            for (int i = 0; i < 16; ++i) present[i] = i >= 2;
+            const double enc = median_us([&] { return ecx_rs_encode_parity(rs124, p.data(), 16, L, 0, L); }, 20);
+            const double dec = median_us([&] { return ecx_rs_decode_missing(rs124, p.data(), present, 16, L, 0, L); }, 20);
+            printf("{\"case\": \"RS(12,4) encodeParity, %d B shards (host)\", \"us_per_call\": %.1f, \"GBps\": %.2f}\n", L,
+                   enc, 16.0 * L / enc / 1e3);
+            printf("{\"case\": \"RS(12,4) decodeMissing {0,1}, %d B shards (host)\", \"us_per_call\": %.1f, \"GBps\": %.2f}\n", L,
+                   dec, 14.0 * L / dec / 1e3);
+            fflush(stdout);
+        }
+        ecx_rs_destroy(rs124);
+    }
     ecx_clay_destroy(clay);
     ecx_rs_destroy(rs);
     return 0;

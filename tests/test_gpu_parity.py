@@ -818,7 +818,7 @@ def test_per_call_paths_agree(ecx, L):
             rs.decodeMissing(sh, present, 0, L)
             assert all((sh[i] == ref[i]).all() for i in range(6))
     finally:
-        ecx.tune("host_gather_kib", 256)
+        ecx.tune("host_gather_kib", 512)
         ecx.tune("host_zero_copy", 1)
 
 
