@@ -48,6 +48,8 @@ def test_committed_pmc_profile_matches_current_sources():
 def test_pmc_traffic_staleness_rules(monkeypatch):
     d = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())["workloads"]["clay42"]
     pool, kernel = d["pool_stripes"], d["kernel"]
+    # as if the tree's sources were the profiled ones (freshness itself is the test above)
+    monkeypatch.setattr(bench, "kernel_source_hash", lambda kernel="": d["kernel_source_hash"])
     assert bench.pmc_traffic("clay42", pool, kernel)[0] == d["hbm_bytes_per_launch"]
     assert bench.pmc_traffic("clay42", pool * 2, kernel) == (
         None, "stale: PMC profile taken on another pool size or kernel instance")
