@@ -91,6 +91,9 @@ typedef struct ecx_rs ecx_rs;
 int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out); /* ReedSolomon.create :34-61 */
 void ecx_rs_destroy(ecx_rs *rs);
 int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out /* total x data */); /* buildMatrix :373-385 */
+/* getDataShardCount / getParityShardCount (ReedSolomon.java:63-75); bindings size their
+ * argument checks with it (the JNI shim's checkBuffersAndSizes, :338-363). */
+int ecx_rs_shape(const ecx_rs *rs, int *data_shards, int *parity_shards);
 int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int offset,
                          int byte_count);                            /* encodeParity :94-108 */
 int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *output, int input_index,
@@ -177,6 +180,10 @@ int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_unit
 void ecx_clay_destroy(ecx_clay *clay);
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha); /* ClayCodeUtil :690-695 */
 int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out /* alpha */); /* :924-941 */
+/* The step's real node count n (= data + parity; virtual nodes excluded), its number of
+ * erased nodes and alpha: performCoding takes n*alpha inputs and n_erased*alpha outputs
+ * (the "Invalid inputs/outputs length" checks, ClayCodeErasureDecodingStep.java:76-82). */
+int ecx_clay_shape(const ecx_clay *clay, int *nodes, int *n_erased, int *alpha);
 /* performCoding(ECChunk[],ECChunk[]) -- ClayCodeErasureDecodingStep.java:53-107.
  * inputs: n*alpha host pointers, NULL = absent; outputs: n_erased*alpha host pointers. */
 int ecx_clay_perform_coding(ecx_clay *clay, const uint8_t *const *inputs, uint8_t *const *outputs, int buf_size);

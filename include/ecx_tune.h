@@ -55,14 +55,17 @@
  *                      per-helper-plane kernel generated for the repair and compiled with hiprtc, for
  *                      the whole 4 KiB chunks of 16-B-aligned layouts: 1 = when the composed map spans
  *                      several 8-row tiles (alpha > 8: Clay(10,4), Clay(12,4); default), 2 = always,
- *                      0 = never (the composed-map kernel only)
+ *                      0 = never (the composed-map kernel only).  If the kernel cannot be compiled
+ *                      or loaded (no libhiprtc, another GPU target), auto falls back to the composed
+ *                      map (the failure is remembered, not retried); 2 returns ECX_E_DEVICE
  *   "rtc_lookahead"    that kernel's generated load schedule: items (non-column nodes, mates) whose
  *                      loads are issued ahead of the one being computed, 0..3 (bits 0-1; default 1);
  *                      for the plane-group kernel bit 0 = partner and mate loads after row ya, bit 1
  *                      = skip the dot's and virtual partners' transposes by uniform branches, bit 2
  *                      = a second body for plane groups whose memory-row partner is virtual, bit 3 =
  *                      every load issued at the start, bit 4 = DIAGNOSTIC data-movement-only build
- *                      (coefficients taken as 1, no transposes: the outputs are not the repair)
+ *                      (coefficients taken as 1, no transposes: the outputs are not the repair;
+ *                      refused with ECX_E_ILLEGAL_ARGUMENT unless the environment has ECX_DIAGNOSTIC=1)
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes
@@ -81,7 +84,7 @@
  *                      chunks of 16-B-aligned layouts whose slot offsets fit 31 bits: 1 = auto
  *                      (default) for multi-tile maps with >= 4 coefficients per used input on
  *                      batches of >= 64 MiB of input (the Clay(4,2) two-node repairs), 2 = wherever
- *                      it fits, 0 = never
+ *                      it fits, 0 = never; the same compile/load fallback as "clay_rtc"
  *   "planes_lookahead" that kernel's load schedule: inputs in flight ahead of the one being
  *                      computed, 0..15 (default 12)
  *   "planes_waves"     that kernel's __launch_bounds__ minimum waves per SIMD, 1..4 (default 2)

@@ -23,8 +23,25 @@ count_mismatch) byte pointers are addresses (long): device pointers, or pinned /
 direct-buffer host addresses; only the *_present flag arrays there are byte[].
 
 JNI rules kept by every forwarder: all non-critical JNI calls (array elements,
-positions) happen before the first GetPrimitiveArrayCritical and after the last
+positions, lengths) happen before the first GetPrimitiveArrayCritical and after the last
 release, so no JNI call runs inside a critical region.
+
+Argument checks (RULES below): the C ABI takes plain pointers and cannot know a Java
+array's length, so before anything is pinned every forwarder checks what the export
+will touch, and returns the status of the exception the reference would throw instead
+of reading or writing past a Java array:
+  * a handle of 0, or a null array the export dereferences     -> ECX_E_NULL
+    (NullPointerException)
+  * a negative count / size / offset                           -> ECX_E_ILLEGAL_ARGUMENT
+  * a byte[][] shorter than the count the export reads (Clay: not exactly n*alpha /
+    |E|*alpha, ClayCodeErasureDecodingStep.java:76-82; RS shard lists: "wrong number of
+    shards", ReedSolomon.java:341-343)                         -> ECX_E_ILLEGAL_ARGUMENT
+    or ECX_E_INDEX (ArrayIndexOutOfBoundsException, CodingLoop lists)
+  * an element (or array) with fewer than position + offset + byteCount bytes, or a
+    negative position                                          -> ECX_E_INDEX, or
+    ECX_E_ILLEGAL_ARGUMENT where the reference's checkBuffersAndSizes throws
+    ("buffers to small", ReedSolomon.java:360-362)
+Every pointer parameter of every export must have a rule: the generator stops otherwise.
 
 Run:  python jni/gen_jni.py   (tests/test_jni.py fails if the committed files are stale)
 """
@@ -40,7 +57,99 @@ JCLASS = "com_backblaze_erasure_ecx_EcxNative"
 HANDLES = ("ecx_rs", "ecx_clay", "ecx_map")
 # byte pointers of these functions may be NULL (C side: "NULL = ..." or unused)
 NULLABLE = {("ecx_check_some_shards", "temp_buffer"), ("ecx_rs_is_parity_correct", "temp_buffer"),
-            ("ecx_lrc_map", "block_present")}
+            ("ecx_lrc_map", "block_present"), ("ecx_map_create", "in_slot"), ("ecx_map_create", "out_slot"),
+            ("ecx_map_info", "n_out"), ("ecx_map_info", "n_in"), ("ecx_map_info", "nnz"),
+            ("ecx_map_matrix", "matrix"), ("ecx_map_matrix", "in_slot"), ("ecx_map_matrix", "out_slot"),
+            ("ecx_clay_geometry", "q"), ("ecx_clay_geometry", "t"), ("ecx_clay_geometry", "alpha"),
+            ("ecx_clay_shape", "nodes"), ("ecx_clay_shape", "n_erased"), ("ecx_clay_shape", "alpha"),
+            ("ecx_rs_shape", "data_shards"), ("ecx_rs_shape", "parity_shards"),
+            ("ecx_gf_tables", "log_table"), ("ecx_gf_tables", "exp_table"), ("ecx_gf_tables", "mul_table")}
+
+ILL, IDX = "ECX_E_ILLEGAL_ARGUMENT", "ECX_E_INDEX"
+OFF_BC = "(int64_t)offset + byte_count"
+RS_N = "(int64_t)rs_k + rs_m"
+# Queries a forwarder runs (after its handle checks) to size its argument checks.
+QUERIES = {
+    "rs": "    int rs_k = 0, rs_m = 0;\n    if (st == ECX_OK) st = ecx_rs_shape((const ecx_rs *)(intptr_t)rs, &rs_k, &rs_m);",
+    "clay": "    int cl_n = 0, cl_ne = 0, cl_a = 0, cl_q = 1;\n"
+            "    if (st == ECX_OK) st = ecx_clay_shape((const ecx_clay *)(intptr_t)clay, &cl_n, &cl_ne, &cl_a);\n"
+            "    if (st == ECX_OK) st = ecx_clay_geometry((const ecx_clay *)(intptr_t)clay, &cl_q, NULL, NULL);",
+    "map": "    int mp_out = 0, mp_in = 0;\n    if (st == ECX_OK) st = ecx_map_info((const ecx_map *)(intptr_t)map, &mp_out, &mp_in, NULL);",
+}
+
+
+def A(param, need, err=IDX):
+    """A primitive array (byte[] / int[] / short[] / boolean flags) of >= need elements."""
+    return ("array", param, need, err)
+
+
+def L(param, count, need, count_err=IDX, len_err=IDX, exact=False, nulls=False, when=None):
+    """A byte[][]: >= count entries (== with exact); entry i < count non-null (unless
+    nulls) with pos[i] >= 0 and pos[i] + need bytes; only checked when `when` holds."""
+    return ("list", param, count, need, count_err, len_err, exact, nulls, when)
+
+
+def NN(*params, err=ILL):
+    return ("nonneg", params, err)
+
+
+# export -> (queries, rules); exports without pointer parameters need no entry.
+RULES = {
+    "ecx_device_count": ((), [A("count", "1")]),
+    "ecx_gf_tables": ((), [A("log_table", "256"), A("exp_table", "510"), A("mul_table", "65536")]),
+    "ecx_matrix_times": ((), [NN("a_rows", "a_cols", "b_rows", "b_cols"), A("a", "(int64_t)a_rows * a_cols"),
+                              A("b", "(int64_t)b_rows * b_cols"), A("out", "(int64_t)a_rows * b_cols")]),
+    "ecx_matrix_invert": ((), [NN("n"), A("m", "(int64_t)n * n"), A("out", "(int64_t)n * n")]),
+    "ecx_code_some_shards": ((), [NN("input_count", "output_count", "offset", "byte_count"),
+                                  A("matrix_rows", "(int64_t)output_count * input_count"),
+                                  L("inputs", "input_count", OFF_BC), L("outputs", "output_count", OFF_BC)]),
+    "ecx_check_some_shards": ((), [NN("input_count", "check_count", "offset", "byte_count"),
+                                   A("matrix_rows", "(int64_t)check_count * input_count"),
+                                   L("inputs", "input_count", OFF_BC), L("to_check", "check_count", OFF_BC),
+                                   A("temp_buffer", "0")]),
+    "ecx_code_single": ((), [NN("row_length", "offset", "byte_count"), NN("index", "output_index", err=IDX),
+                             A("matrix_rows", "((int64_t)output_index + 1) * row_length"),
+                             A("input", OFF_BC), A("output", OFF_BC)]),
+    "ecx_rs_create": ((), []),
+    "ecx_rs_matrix": (("rs",), [A("out", "(%s) * rs_k" % RS_N)]),
+    "ecx_rs_shape": ((), [A("data_shards", "1"), A("parity_shards", "1")]),
+    "ecx_rs_encode_parity": ((), [NN("shard_count", "shard_length", "offset", "byte_count"),
+                                  L("shards", "shard_count", "shard_length", count_err=ILL, len_err=ILL)]),
+    "ecx_rs_encode_parity_single": ((), [NN("offset", "byte_count"), A("shard", OFF_BC), A("output", OFF_BC)]),
+    "ecx_rs_is_parity_correct": ((), [NN("shard_count", "shard_length", "first_byte", "byte_count", "temp_length"),
+                                      L("shards", "shard_count", "shard_length", count_err=ILL, len_err=ILL),
+                                      A("temp_buffer", "temp_length", err=ILL)]),
+    "ecx_rs_decode_missing": (("rs",), [NN("shard_count", "shard_length", "offset", "byte_count"),
+                                        L("shards", "shard_count", "shard_length", count_err=ILL, len_err=ILL),
+                                        A("shard_present", RS_N)]),
+    "ecx_rs_decode_missing_single": (("rs",), [NN("output_count", "offset", "byte_count"), A("shard", OFF_BC),
+                                               A("shard_present", RS_N), L("outputs", "output_count", OFF_BC)]),
+    "ecx_map_create": ((), [NN("n_out", "n_in"), A("matrix", "(int64_t)n_out * n_in"), A("in_slot", "n_in"),
+                            A("out_slot", "n_out")]),
+    "ecx_map_info": ((), [A("n_out", "1"), A("n_in", "1"), A("nnz", "1")]),
+    "ecx_map_matrix": (("map",), [A("matrix", "(int64_t)mp_out * mp_in"), A("in_slot", "mp_in"),
+                                  A("out_slot", "mp_out")]),
+    "ecx_rs_decode_map": (("rs",), [A("shard_present", RS_N)]),
+    "ecx_rs_decode_missing_batch": (("rs",), [A("shard_present", RS_N)]),
+    "ecx_rs_decode_partial_batch": (("rs",), [A("shard_present", RS_N)]),
+    "ecx_clay_create": ((), [NN("n_erased"), A("erased", "n_erased")]),
+    "ecx_clay_create_shortened": ((), [NN("n_erased"), A("erased", "n_erased")]),
+    "ecx_clay_geometry": ((), [A("q", "1"), A("t", "1"), A("alpha", "1")]),
+    "ecx_clay_shape": ((), [A("nodes", "1"), A("n_erased", "1"), A("alpha", "1")]),
+    "ecx_clay_helper_planes": (("clay",), [A("out", "cl_a / (cl_q > 0 ? cl_q : 1)")]),
+    # performCoding returns before its length checks when nothing is erased (:54-56)
+    "ecx_clay_perform_coding": (("clay",), [NN("buf_size"),
+                                            L("inputs", "(int64_t)cl_n * cl_a", "buf_size", count_err=ILL,
+                                              exact=True, nulls=True, when="cl_ne > 0"),
+                                            L("outputs", "(int64_t)cl_ne * cl_a", "buf_size", count_err=ILL,
+                                              exact=True, when="cl_ne > 0")]),
+    "ecx_clay_decode_single_helper": (("clay",), [NN("buf_size"),
+                                                  L("helper_coupled", "(int64_t)(cl_a / (cl_q > 0 ? cl_q : 1)) * cl_n",
+                                                    "buf_size", nulls=True),
+                                                  L("outputs", "cl_a", "buf_size", nulls=True)]),
+    "ecx_lrc_map": ((), [A("block_present", "16")]),
+    "ecx_lrc_decode_batch": ((), [A("block_present", "16")]),
+}
 
 
 def exports():
@@ -121,6 +230,7 @@ typedef struct {
     jsize n;
     jbyteArray *refs;
     jint *pos;
+    jsize *lens;
     uint8_t **ptrs;
 } ecx_jni_buflist;
 
@@ -128,14 +238,45 @@ static int buflist_refs(JNIEnv *env, jobjectArray arr, jintArray positions, ecx_
     b->n = arr ? (*env)->GetArrayLength(env, arr) : 0;
     b->refs = (jbyteArray *)calloc((size_t)b->n + 1, sizeof(jbyteArray));
     b->pos = (jint *)calloc((size_t)b->n + 1, sizeof(jint));
+    b->lens = (jsize *)calloc((size_t)b->n + 1, sizeof(jsize));
     b->ptrs = (uint8_t **)calloc((size_t)b->n + 1, sizeof(uint8_t *));
-    if (!b->refs || !b->pos || !b->ptrs) return ECX_E_NOMEM;
-    for (jsize i = 0; i < b->n; ++i) b->refs[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, arr, i);
+    if (!b->refs || !b->pos || !b->lens || !b->ptrs) return ECX_E_NOMEM;
+    for (jsize i = 0; i < b->n; ++i) {
+        b->refs[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, arr, i);
+        b->lens[i] = b->refs[i] ? (*env)->GetArrayLength(env, b->refs[i]) : 0;
+    }
     if (positions) {
         if ((*env)->GetArrayLength(env, positions) < b->n) return ECX_E_ILLEGAL_ARGUMENT;
         (*env)->GetIntArrayRegion(env, positions, 0, b->n, b->pos);
     }
     return ECX_OK;
+}
+
+/* A byte[][] the export reads `count` entries of: at least `count` entries (exactly,
+ * with `exact`), entry i < count non-null unless `nulls`, pos[i] >= 0 and
+ * pos[i] + need <= its length.  Runs before anything is pinned. */
+static int buflist_check(const ecx_jni_buflist *b, jobjectArray arr, int64_t count, int64_t need, int exact,
+                         int nulls, int count_err, int len_err) {
+    if (count < 0) return ECX_E_ILLEGAL_ARGUMENT;
+    if (!arr) return count > 0 ? ECX_E_NULL : ECX_OK;
+    if (exact ? (int64_t)b->n != count : (int64_t)b->n < count) return count_err;
+    if (need < 0) need = 0;
+    for (int64_t i = 0; i < count; ++i) {
+        if (!b->refs[i]) {
+            if (nulls) continue;
+            return ECX_E_NULL;
+        }
+        if (b->pos[i] < 0 || (int64_t)b->pos[i] + need > (int64_t)b->lens[i]) return len_err;
+    }
+    return ECX_OK;
+}
+
+/* A primitive array the export touches `need` elements of (null: NullPointerException
+ * unless the export accepts NULL). */
+static int array_check(JNIEnv *env, jarray arr, int64_t need, int nullable, int err) {
+    if (!arr) return nullable ? ECX_OK : ECX_E_NULL;
+    if (need < 0) return ECX_E_ILLEGAL_ARGUMENT;
+    return (int64_t)(*env)->GetArrayLength(env, arr) < need ? err : ECX_OK;
 }
 
 static int buflist_pin(JNIEnv *env, ecx_jni_buflist *b) {
@@ -158,6 +299,7 @@ static void buflist_free(JNIEnv *env, ecx_jni_buflist *b) {
         if (b->refs && b->refs[i]) (*env)->DeleteLocalRef(env, b->refs[i]);
     free(b->refs);
     free(b->pos);
+    free(b->lens);
     free(b->ptrs);
 }
 
@@ -215,6 +357,39 @@ public final class EcxNative {
         java.append("\n    public static native %s %s(%s);\n" % (jret, jname, ", ".join(jparams)))
         body = []
         pre, pin, unpin, post, args = [], [], [], [], []
+        pnames = {p: kind for (kind, _, _), t, p in kinds}
+        needs_rule = [p for p, k in pnames.items() if k in ("bytes", "ints", "shorts", "buflist")]
+        if needs_rule and name not in RULES:
+            raise SystemExit("no argument rule for %s (pointer parameters %s)" % (name, needs_rule))
+        queries, rules = RULES.get(name, ((), []))
+        covered = {r[1] for r in rules if r[0] in ("array", "list")}
+        if set(needs_rule) - covered:
+            raise SystemExit("%s: no rule for %s" % (name, sorted(set(needs_rule) - covered)))
+        checks = []
+        if not name.endswith("_destroy"):
+            for p, k in pnames.items():
+                if k == "handle":
+                    checks.append("    if (st == ECX_OK && !%s) st = ECX_E_NULL;" % p)
+        for r in rules:
+            if r[0] == "nonneg":
+                for p in r[1]:
+                    checks.append("    if (st == ECX_OK && %s < 0) st = %s;" % (p, r[2]))
+        for q in queries:
+            checks.append(QUERIES[q])
+        late = []  # after the buffer lists' references are taken, before pinning
+        for r in rules:
+            if r[0] == "array":
+                _, p, need, err = r
+                late.append("    if (st == ECX_OK) st = array_check(env, %s, %s, %d, %s);"
+                            % (p, need, 1 if (name, p) in NULLABLE else 0, err))
+            elif r[0] == "list":
+                _, p, count, need, cerr, lerr, exact, nulls, when = r
+                cond = "st == ECX_OK" + (" && (%s)" % when if when else "")
+                late.append("    if (%s) st = buflist_check(&%s_b, %s, %s, %s, %d, %d, %s, %s);"
+                            % (cond, p, p, count, need, int(exact), int(nulls), cerr, lerr))
+        for (kind, _, _), t, p in kinds:
+            if kind == "outhandle":
+                late.append("    if (st == ECX_OK) st = array_check(env, %s, 1, 0, ECX_E_INDEX);" % p)
         for (kind, jt, jnt), t, p in kinds:
             ct = t.replace("const ", "const ").strip()
             if kind == "int":
@@ -235,12 +410,12 @@ public final class EcxNative {
                 cty = {"bytes": "uint8_t", "ints": "int", "shorts": "int16_t"}[kind]
                 mode = "JNI_ABORT" if t.startswith("const") else "0"
                 pre.append("    %s *%s_p = NULL;" % (cty, p))
-                pin.append("    %s_p = (%s *)PIN(%s);" % (p, cty, p))
+                pin.append("    if (st == ECX_OK) %s_p = (%s *)PIN(%s);" % (p, cty, p))
                 unpin.insert(0, "    UNPIN(%s, %s_p, %s);" % (p, p, mode))
                 args.append("%s_p" % p)
             elif kind == "buflist":
                 mode = "JNI_ABORT" if t.startswith("const") else "0"
-                pre.append("    ecx_jni_buflist %s_b = {0, NULL, NULL, NULL};" % p)
+                pre.append("    ecx_jni_buflist %s_b = {0, NULL, NULL, NULL, NULL};" % p)
                 pre.append("    if (st == ECX_OK) st = buflist_refs(env, %s, %s_positions, &%s_b);" % (p, p, p))
                 pin.append("    if (st == ECX_OK) st = buflist_pin(env, &%s_b);" % p)
                 unpin.insert(0, "    buflist_unpin(env, &%s_b, %s);" % (p, mode))
@@ -259,7 +434,9 @@ public final class EcxNative {
         else:
             body.append("    (void)cls;")
             body.append("    jint st = ECX_OK;")
+            body.extend(checks)
             body.extend(pre)
+            body.extend(late)
             body.extend(pin)
             pinned = [ln for ln in pin]
             if pinned:

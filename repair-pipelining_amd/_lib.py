@@ -39,10 +39,26 @@ class EcxError(Exception):
         super().__init__(f"{STATUS.get(code, 'status')} ({code}){': ' + detail if detail else ''}")
 
 
-def build(verbose: bool = False) -> Path:
-    """Compile libecx.so for gfx950 with hipcc (repair-pipelining_amd/Makefile)."""
-    jobs = str(min(8, os.cpu_count() or 1))
-    subprocess.run(["make", "-C", str(PKG_DIR), "-j", jobs] + ([] if verbose else ["-s"]), check=True)
+BUILD_LOCK = PKG_DIR / ".build.lock"
+
+
+def build(verbose: bool = False, only_if_missing: bool = False) -> Path:
+    """Compile libecx.so for gfx950 with hipcc (repair-pipelining_amd/Makefile).
+
+    Serialised across processes by an exclusive flock on PKG_DIR/.build.lock, so the N
+    ranks of `bench.py --gpus N` (or parallel test workers) on a checkout without a
+    build never run `make` in the same directory at once; with ``only_if_missing`` the
+    existence check runs under the lock too, so only the first rank builds."""
+    import fcntl
+    with open(BUILD_LOCK, "a") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if only_if_missing and LIB_PATH.exists():
+                return LIB_PATH
+            jobs = str(min(8, os.cpu_count() or 1))
+            subprocess.run(["make", "-C", str(PKG_DIR), "-j", jobs] + ([] if verbose else ["-s"]), check=True)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return LIB_PATH
 
 
@@ -73,6 +89,7 @@ SIGNATURES = {
     "ecx_rs_create": (I, [I, I, ctypes.POINTER(P)]),
     "ecx_rs_destroy": (None, [P]),
     "ecx_rs_matrix": (I, [P, P]),
+    "ecx_rs_shape": (I, [P, PI, PI]),
     "ecx_rs_encode_parity": (I, [P, PP, I, I, I, I]),
     "ecx_rs_encode_parity_single": (I, [P, P, P, I, I, I, I]),
     "ecx_rs_is_parity_correct": (I, [P, PP, I, I, I, I, P, I]),
@@ -95,6 +112,7 @@ SIGNATURES = {
     "ecx_clay_destroy": (None, [P]),
     "ecx_clay_geometry": (I, [P, PI, PI, PI]),
     "ecx_clay_helper_planes": (I, [P, I, P]),
+    "ecx_clay_shape": (I, [P, PI, PI, PI]),
     "ecx_clay_perform_coding": (I, [P, PP, PP, I]),
     "ecx_clay_decode_single_helper": (I, [P, PP, I, PP, I, I]),
     "ecx_clay_map": (I, [P, ctypes.POINTER(P)]),
@@ -133,7 +151,7 @@ def lib():
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
-            build()
+            build(only_if_missing=True)
         _share_torch_hip_runtime()
         l = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():

@@ -44,41 +44,48 @@ std::string clay_rtc_source(const ClayRepairProgram &pg, const RtcShape &shape =
 // shortened Clay(10,4), Clay(8,4), ...); `why` gets the reason otherwise.
 bool clay_grp_supported(const ClayRepairProgram &pg, std::string *why = nullptr);
 std::string clay_grp_source(const ClayRepairProgram &pg, const RtcShape &shape = RtcShape());
-// The source of the kernel the current tuning (ecx_tune "rtc_group", ...) selects.
-std::string clay_rtc_selected_source(const ClayRepairProgram &pg);
+// The shape the current tuning (ecx_tune "rtc_lookahead", "rtc_group", ...) selects, read
+// in one snapshot, and the source of the kernel it selects for `pg`.
+RtcShape rtc_current_shape();
+std::string clay_rtc_selected_source(const ClayRepairProgram &pg, const RtcShape &shape);
 
 class ClayRtc {
 public:
     explicit ClayRtc(ClayRepairProgram pg);
     ~ClayRtc();
     const ClayRepairProgram &program() const { return pg_; }
-    // Compile (hiprtc, once per process) and load (once per device).  Throws
-    // ECX_E_DEVICE when hiprtc or the module load fails.
-    void prepare();
+    // The kernel `shape` selects for this program: "k_clay_repair_grp" or "k_clay_repair".
+    const char *kernel_name(const RtcShape &shape) const;
+    // Compile (hiprtc, once per process and target) and load (once per device) the kernel
+    // `shape` selects, uploading its program table on `stream`.  False (with the reason)
+    // when hiprtc, the compile or the module load fails; a failure is remembered per
+    // (source, device) and not retried, so an auto path falls back at no further cost.
+    bool available(const RtcShape &shape, hipStream_t stream, std::string *why = nullptr);
     // Enqueue the repair of `nchunks` whole 4 KiB chunks (bytes [0, nchunks * 4 KiB) of
-    // every sub-chunk) over nstripes stripes, in the performCoding batch layout.
-    // The kernel the current tuning selects for this program: "k_clay_repair_grp" or
-    // "k_clay_repair".
-    const char *kernel_name() const;
-    void launch(const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
-                int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nchunks,
+    // every sub-chunk) over nstripes stripes, in the performCoding batch layout, with the
+    // kernel `shape` selects.  Throws ECX_E_DEVICE when that kernel is not available.
+    void launch(const RtcShape &shape, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nchunks,
                 hipStream_t stream);
 
 private:
+    bool prepare(const RtcShape &shape, const std::string &src, hipStream_t stream, std::string *why);
     struct Impl;
     ClayRepairProgram pg_;
     std::unique_ptr<Impl> impl_;
 };
 
-// Compile `source` with hiprtc for gfx950 (diagnostics / tests: no device needed).
+// Compile `source` with hiprtc (diagnostics / tests: no device needed).
 // Returns the code object size, throws ECX_E_DEVICE with the compiler log on failure.
 size_t rtc_compile_check(const std::string &source);
 
 // Shared by the generated kernels (clay_rtc.cpp, map_rtc.cpp): hiprtc compilation to a
-// gfx950 code object (throws ECX_E_DEVICE with the log), the common device prelude
+// code object for `arch` (empty = the current device's target ID, or the library's build
+// ARCH without a device; throws ECX_E_DEVICE with the log), the common device prelude
 // (bit-plane transpose tr/untr, the 3-input XOR x3, uniform64), and the bit-plane
 // multiply: plane i of c*x is the XOR of the planes j in plane_sets(c)[i].
-std::vector<char> rtc_compile(const std::string &source);
+std::string rtc_offload_arch();
+std::vector<char> rtc_compile(const std::string &source, const std::string &arch = std::string());
 const char *rtc_prelude();
 std::vector<std::vector<int>> plane_sets(uint8_t c);
 

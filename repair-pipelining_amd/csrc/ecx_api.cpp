@@ -363,6 +363,13 @@ int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out) {
     return ECX_OK;
 }
 
+int ecx_rs_shape(const ecx_rs *rs, int *data_shards, int *parity_shards) {
+    if (!rs) return ECX_E_NULL;
+    if (data_shards) *data_shards = rs->code.k();
+    if (parity_shards) *parity_shards = rs->code.m();
+    return ECX_OK;
+}
+
 int ecx_rs_encode_map(ecx_rs *rs, const ecx_map **out) {
     return guarded(__func__, [&]() -> int {
         std::lock_guard<std::mutex> lk(rs->mu);
@@ -690,6 +697,14 @@ int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha) {
     return ECX_OK;
 }
 
+int ecx_clay_shape(const ecx_clay *clay, int *nodes, int *n_erased, int *alpha) {
+    if (!clay) return ECX_E_NULL;
+    if (nodes) *nodes = clay->pl.n_real();
+    if (n_erased) *n_erased = (int)clay->pl.erased().size();
+    if (alpha) *alpha = clay->pl.alpha();
+    return ECX_OK;
+}
+
 int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out) {
     return guarded(__func__, [&]() -> int {
         std::vector<int> h = clay->pl.helper_planes(erased_index);
@@ -776,6 +791,7 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
         // 4 KiB chunks of 16-B-aligned layouts whose slot offsets fit 31 bits; the
         // composed-map kernel takes any tail and every other layout.
         int64_t done = 0;
+        const char *rtc_kernel = nullptr;
         // auto (1): repairs whose composed map spans several 8-row tiles (alpha > 8), where
         // the composed kernel is bound by vector issue (Clay(10,4): 0.61 -> 0.70 of HBM);
         // Clay(4,2)'s single-tile map is memory-bound and stays on the composed kernel
@@ -786,17 +802,22 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
             in_stripe_stride % 16 == 0 && in_sub_stride % 16 == 0 && out_stripe_stride % 16 == 0 &&
             out_sub_stride % 16 == 0 && in_sub_stride >= 0 && out_sub_stride >= 0) {
             if (ClayRtc *r = clay_rtc(clay)) {
-                if ((int64_t)r->program().max_in_slot * in_sub_stride + kChunkBytes <= 0x7FFFFFFF) {
+                // auto: a generated kernel that cannot be compiled or loaded here (no
+                // hiprtc, another target) falls back to the composed map; forced (2) throws
+                const RtcShape sh = rtc_current_shape();
+                if ((int64_t)r->program().max_in_slot * in_sub_stride + kChunkBytes <= 0x7FFFFFFF &&
+                    (rtc_mode == 2 || r->available(sh, (hipStream_t)stream))) {
                     done = buf_size / kChunkBytes * kChunkBytes;
-                    r->launch(in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
-                              done / kChunkBytes, (hipStream_t)stream);
+                    r->launch(sh, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
+                              nstripes, done / kChunkBytes, (hipStream_t)stream);
+                    rtc_kernel = r->kernel_name(sh);
                 }
             }
         }
         if (done < buf_size)
             launch_apply(m->cm, in + done, in_stripe_stride, in_sub_stride, out + done, out_stripe_stride,
                          out_sub_stride, nstripes, buf_size - done, (hipStream_t)stream);
-        if (done > 0) set_last_kernel(clay_rtc(clay)->kernel_name());
+        if (rtc_kernel) set_last_kernel(rtc_kernel);
         return ECX_OK;
     });
 }
@@ -805,7 +826,7 @@ int ecx_clay_rtc_compile_check(ecx_clay *clay) {
     return guarded(__func__, [&]() -> int {
         ClayRtc *r = clay_rtc(clay);
         if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
-        return (int)rtc_compile_check(clay_rtc_selected_source(r->program()));
+        return (int)rtc_compile_check(clay_rtc_selected_source(r->program(), rtc_current_shape()));
     });
 }
 
@@ -813,7 +834,7 @@ int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
     return guarded(__func__, [&]() -> int {
         ClayRtc *r = clay_rtc(clay);
         if (!r) throw Error(ECX_E_ILLEGAL_ARGUMENT, "no per-helper-plane program: " + clay->rtc_why);
-        const std::string src = clay_rtc_selected_source(r->program());
+        const std::string src = clay_rtc_selected_source(r->program(), rtc_current_shape());
         if (buf && len > (int)src.size()) std::memcpy(buf, src.c_str(), src.size() + 1);
         return (int)src.size();
     });
@@ -958,6 +979,13 @@ int ecx_host_unregister(void *ptr) {
 }
 
 // ---------------------------------------------------------------- tuning hook (include/ecx_tune.h)
+namespace {
+bool diagnostic_builds_allowed() {
+    const char *v = std::getenv("ECX_DIAGNOSTIC");
+    return v && std::strcmp(v, "1") == 0;
+}
+}  // namespace
+
 int ecx_tune(const char *key, int value) {
     const std::string k = key ? key : "";
     Tuning &t = tuning();
@@ -1024,6 +1052,9 @@ int ecx_tune(const char *key, int value) {
     }
     else if (k == "rtc_lookahead") {
         if (value < 0 || value > 31) return ECX_E_ILLEGAL_ARGUMENT;
+        // bit 4 is the DIAGNOSTIC movement-only build, whose outputs are not the repair:
+        // refused unless the process opted in with ECX_DIAGNOSTIC=1
+        if ((value & 16) && !diagnostic_builds_allowed()) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_lookahead = value;
     }
     else if (k == "rtc_xcd") {

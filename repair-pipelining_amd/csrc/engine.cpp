@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <exception>
 
 namespace ecx {
 
@@ -777,11 +778,35 @@ const uint8_t *run_gathered(DeviceContext &ctx, CompiledMap &cm, const uint8_t *
 }
 }  // namespace
 
+namespace {
+// Every buffer the map reads or writes must exist before anything is enqueued: a null
+// found halfway would leave copies to or from the caller's (e.g. JNI-pinned) arrays in flight.
+void check_host_buffers(const LinearMap &m, const uint8_t *const *inputs, uint8_t *const *outputs) {
+    for (int j = 0; j < m.n_in; ++j)
+        if (!inputs[m.in_slot[j]]) throw Error(ECX_E_NULL, "input buffer is null");
+    if (outputs)
+        for (int o = 0; o < m.n_out; ++o)
+            if (!outputs[m.out_slot[o]]) throw Error(ECX_E_NULL, "output buffer is null");
+}
+
+// Drains the leased stream when an error unwinds a host call, before the lease (and the
+// caller's buffers) are released: no DMA to or from caller memory outlives the call.
+struct DrainOnUnwind {
+    hipStream_t stream;
+    int depth = std::uncaught_exceptions();
+    ~DrainOnUnwind() {
+        if (std::uncaught_exceptions() > depth) (void)hipStreamSynchronize(stream);
+    }
+};
+}  // namespace
+
 void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
               int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return;
+    check_host_buffers(cm.map(), inputs, outputs);
     DeviceContext::Lease lease = DeviceContext::acquire();
     DeviceContext &ctx = *lease.ctx;
+    DrainOnUnwind drain{ctx.stream};
     const int64_t zc_pitch = (byte_count + 255) / 256 * 256;
     void *zc_dev = nullptr;
     bool zero_copy = byte_count <= tuning().host_gather_max && tuning().host_zero_copy;
@@ -846,8 +871,10 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
 
 bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return true;
+    check_host_buffers(cm.map(), inputs, nullptr);
     DeviceContext::Lease lease = DeviceContext::acquire();
     DeviceContext &ctx = *lease.ctx;
+    DrainOnUnwind drain{ctx.stream};
     uint64_t *cnt = ctx.counter();
     check_hip(hipMemsetAsync(cnt, 0, sizeof(uint64_t), ctx.stream), "hipMemsetAsync");
     if (byte_count <= tuning().host_gather_max) {

@@ -333,7 +333,8 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                     }
             planes = cm.map().nnz() >= 4 * used && nstripes * (nbytes / kChunkBytes) * used >= 16384;
         }
-        planes = planes && cm.planes() != nullptr;
+        // auto falls back to the composed kernels when the generated one cannot be built here
+        planes = planes && cm.planes() != nullptr && (tu.map_planes == 2 || cm.planes()->available(accumulate));
     }
     if (planes) {
         skew = 0;

@@ -193,9 +193,10 @@ struct MapPlanes::Impl {
         hipModule_t mod = nullptr;
         hipFunction_t fn = nullptr;
     };
-    std::map<std::string, std::string> source;        // shape key -> source
-    std::map<std::string, std::vector<char>> code;    // source -> code object (compiled once)
-    std::map<std::pair<std::string, int>, Loaded> dev;  // (source, device) -> module
+    std::map<std::string, std::string> source;                  // shape key -> source
+    std::map<std::string, std::vector<char>> code;              // arch + source -> code object (compiled once)
+    std::map<std::pair<std::string, int>, Loaded> dev;          // (source, device) -> module
+    std::map<std::pair<std::string, int>, std::string> failed;  // (source, device) -> why (not retried)
 };
 
 MapPlanes::MapPlanes(LinearMap m) : map_(std::move(m)), impl_(new Impl) {
@@ -213,34 +214,63 @@ MapPlanes::~MapPlanes() {
     (void)hipSetDevice(cur);
 }
 
+namespace {
+PlanesShape planes_current_shape() {
+    const Tuning t = tuning();  // one snapshot
+    PlanesShape sh;
+    sh.lookahead = t.planes_lookahead;
+    sh.waves = t.planes_waves;
+    return sh;
+}
+}  // namespace
+
+bool MapPlanes::load(const PlanesShape &sh, bool accumulate, hipFunction_t *fn, std::string *why) {
+    int d = 0;
+    check_hip(hipGetDevice(&d), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(impl_->mu);
+    const std::string key = std::to_string(sh.lookahead) + "/" + std::to_string(sh.waves) + "/" +
+                            std::to_string((int)sh.nt_loads) + "/" + std::to_string((int)accumulate);
+    auto si = impl_->source.find(key);
+    if (si == impl_->source.end()) si = impl_->source.emplace(key, map_planes_source(map_, sh, accumulate)).first;
+    const std::string &src = si->second;
+    const std::pair<std::string, int> dk{src, d};
+    auto di = impl_->dev.find(dk);
+    if (di == impl_->dev.end()) {
+        auto f = impl_->failed.find(dk);
+        if (f != impl_->failed.end()) {
+            if (why) *why = f->second;
+            return false;
+        }
+        Impl::Loaded n;
+        try {
+            const std::string arch = rtc_offload_arch();
+            auto ci = impl_->code.find(arch + "\n" + src);
+            if (ci == impl_->code.end()) ci = impl_->code.emplace(arch + "\n" + src, rtc_compile(src, arch)).first;
+            check_hip(hipModuleLoadData(&n.mod, ci->second.data()), "hipModuleLoadData(k_map_planes)");
+            check_hip(hipModuleGetFunction(&n.fn, n.mod, kernel_name()), "hipModuleGetFunction(k_map_planes)");
+        } catch (const Error &e) {
+            if (n.mod) (void)hipModuleUnload(n.mod);
+            impl_->failed[dk] = e.what();
+            if (why) *why = e.what();
+            return false;
+        }
+        di = impl_->dev.emplace(dk, n).first;
+    }
+    if (fn) *fn = di->second.fn;
+    return true;
+}
+
+bool MapPlanes::available(bool accumulate, std::string *why) {
+    return load(planes_current_shape(), accumulate, nullptr, why);
+}
+
 void MapPlanes::launch(const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                        int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nchunks,
                        bool accumulate, hipStream_t stream) {
     if (nstripes <= 0 || nchunks <= 0) return;
-    PlanesShape sh;
-    sh.lookahead = tuning().planes_lookahead;
-    sh.waves = tuning().planes_waves;
-    int d = 0;
-    check_hip(hipGetDevice(&d), "hipGetDevice");
-    Impl::Loaded L;
-    {
-        std::lock_guard<std::mutex> lk(impl_->mu);
-        const std::string key = std::to_string(sh.lookahead) + "/" + std::to_string(sh.waves) + "/" +
-                                std::to_string((int)sh.nt_loads) + "/" + std::to_string((int)accumulate);
-        auto si = impl_->source.find(key);
-        if (si == impl_->source.end()) si = impl_->source.emplace(key, map_planes_source(map_, sh, accumulate)).first;
-        const std::string &src = si->second;
-        auto di = impl_->dev.find({src, d});
-        if (di == impl_->dev.end()) {
-            auto ci = impl_->code.find(src);
-            if (ci == impl_->code.end()) ci = impl_->code.emplace(src, rtc_compile(src)).first;
-            Impl::Loaded n;
-            check_hip(hipModuleLoadData(&n.mod, ci->second.data()), "hipModuleLoadData(k_map_planes)");
-            check_hip(hipModuleGetFunction(&n.fn, n.mod, kernel_name()), "hipModuleGetFunction(k_map_planes)");
-            di = impl_->dev.emplace(std::make_pair(src, d), n).first;
-        }
-        L = di->second;
-    }
+    hipFunction_t fn = nullptr;
+    std::string why;
+    if (!load(planes_current_shape(), accumulate, &fn, &why)) throw Error(ECX_E_DEVICE, why);
     const int64_t max_blocks = (int64_t)1 << 30;
     const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / nchunks);
     set_last_kernel(kernel_name());
@@ -251,7 +281,7 @@ void MapPlanes::launch(const uint8_t *in, int64_t in_stripe_stride, int64_t in_s
         long long iss = in_stripe_stride, isl = in_slot_stride, oss = out_stripe_stride, osl = out_slot_stride;
         long long nc = nchunks;
         void *args[] = {&pin, &iss, &isl, &pout, &oss, &osl, &nc};
-        check_hip(hipModuleLaunchKernel(L.fn, (unsigned)(ns * nchunks), 1, 1, kPlanesThreads, 1, 1, 0, stream, args,
+        check_hip(hipModuleLaunchKernel(fn, (unsigned)(ns * nchunks), 1, 1, kPlanesThreads, 1, 1, 0, stream, args,
                                         nullptr),
                   "k_map_planes launch");
     }

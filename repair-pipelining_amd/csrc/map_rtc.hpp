@@ -48,12 +48,18 @@ public:
     // stripes (the launch_apply batch layout).  Inputs are read through a buffer
     // descriptor with 32-bit slot offsets: the caller guarantees max_in_slot * slot
     // stride + 4 KiB < 2^31 and 16-byte alignment.  Compiles (once per process) and
-    // loads (once per device) on first use; throws ECX_E_DEVICE if hiprtc fails.
+    // loads (once per device) on first use; throws ECX_E_DEVICE if hiprtc or the load fails.
     void launch(const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                 int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nchunks, bool accumulate,
                 hipStream_t stream);
 
+    // Compiles and loads the kernel the current tuning selects; false (with the reason)
+    // when hiprtc, the compile or the module load fails.  A failure is remembered per
+    // (source, device), so the auto path falls back to the composed map at no further cost.
+    bool available(bool accumulate, std::string *why = nullptr);
+
 private:
+    bool load(const PlanesShape &shape, bool accumulate, hipFunction_t *fn, std::string *why);
     struct Impl;
     LinearMap map_;
     std::unique_ptr<Impl> impl_;

@@ -3,7 +3,10 @@
  * tests/test_jni.py checks the generated JNI forwarders (jni/ecx_jni.c) with
  * `gcc -fsyntax-only` against this file: the JNI types and the function-table entries
  * ecx_jni.c uses, declared with the shapes of the JNI specification (jni.h of any JDK).
- * Nothing is built or linked with it; the real build (jni/Makefile) uses $JAVA_HOME.
+ * The table here holds only those entries (not the JDK's slot layout), which is all the
+ * forwarders reference by name; tests/native/jni_fake_env.c fills it with fakes so that
+ * tests/test_jni_runtime.py can execute the forwarders.  The real build (jni/Makefile)
+ * uses $JAVA_HOME's jni.h.
  */
 #ifndef JNI_SYNTAX_STUB_H
 #define JNI_SYNTAX_STUB_H

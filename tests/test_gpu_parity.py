@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from conftest import shortened_clay_oracle
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -1375,13 +1376,114 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
         want = "k_clay_repair_grp" if mode[2] else "k_clay_repair"
         assert outs[mode][1] == want, (mode, outs[mode][1])
         assert (outs[mode][0] == ref0).all(), mode
+    host = pool[S - 1].cpu().numpy()
+    inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
     if v == 0:
-        host = pool[S - 1].cpu().numpy()
-        inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
         ref = [np.zeros(B, np.uint8) for _ in range(a)]
         O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
-        assert all((ref0[S - 1, z] == ref[z]).all() for z in range(a))
-        assert all((outs[modes[-1]][0][S - 1, z] == ref[z]).all() for z in range(a))
+    else:  # shortened: the reference Clay(k+v, m) with the virtual nodes zero-filled
+        ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
+    for mode in modes:
+        bad = [z for z in range(a) if not (outs[mode][0][S - 1, z] == ref[z]).all()]
+        assert not bad, (mode, bad[:8])
+
+
+@pytest.mark.parametrize("e", [0, 3, 9, 10, 13])
+def test_clay104_shipped_repair_kernel_vs_shortened_oracle(ecx, torch_dev, e):
+    """BASELINE config 4 as shipped: the default launch of a shortened Clay(10,4)
+    single-node repair (4 KiB sub-chunks of 1 MiB node blocks) runs the plane-group
+    kernel k_clay_repair_grp, and its output on random NON-codeword stripes equals the
+    oracle Clay(12,4) (ClayCodeErasureDecodingStep.java:171-203 stage sequence) with the
+    two virtual data nodes zero-filled, on every sub-chunk of first, middle and last
+    stripe.  e covers a data node of each node row (0, 3, 9), the first parity node (10)
+    and the last (13)."""
+    torch = torch_dev
+    k, m, v, B, S = 10, 4, 2, 4096, 5
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    n, a = k + m, step.subPacketSize
+    assert a == 256
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 1000 + e)
+    o = torch.full((S, a, B), 0x5A, dtype=torch.uint8, device="cuda")
+    step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
+    torch.cuda.synchronize()
+    assert ecx.last_kernel() == "k_clay_repair_grp", ecx.last_kernel()
+    got = o.cpu().numpy()
+    for s in (0, S // 2, S - 1):
+        host = pool[s].cpu().numpy()
+        inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
+        ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
+        bad = [z for z in range(a) if not (got[s, z] == ref[z]).all()]
+        assert not bad, (e, s, bad[:8])
+
+
+_NO_HIPRTC_SCRIPT = r"""
+import sys
+import numpy as np
+import torch
+import rpamd
+sys.path.insert(0, sys.argv[1])
+import oracle as O
+from conftest import shortened_clay_oracle
+ecx = rpamd.load()
+# Clay(10,4) single repair: auto (clay_rtc 1) would run k_clay_repair_grp
+k, m, v, e, B, S = 10, 4, 2, 3, 4096, 2
+step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+n, a = k + m, step.subPacketSize
+pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+ecx.fill_random(pool, pool.numel(), 5)
+o = torch.zeros((S, a, B), dtype=torch.uint8, device="cuda")
+step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
+torch.cuda.synchronize()
+kern = ecx.last_kernel()
+assert not kern.startswith("k_clay_repair"), kern
+host = pool[S - 1].cpu().numpy()
+inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
+ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
+got = o[S - 1].cpu().numpy()
+assert all((got[z] == ref[z]).all() for z in range(a))
+ecx.tune("clay_rtc", 2)
+try:
+    step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
+    raise SystemExit("forced clay_rtc without hiprtc did not fail")
+except ecx.EcxError as err:
+    assert err.code == -10, err
+ecx.tune("clay_rtc", 1)
+# Clay(4,2) repair of {0, 3}: auto (map_planes 1) would run k_map_planes on >= 64 MiB
+B2, S2 = 32768, 64
+step2 = ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2)
+pool2 = torch.empty((S2, 48, B2), dtype=torch.uint8, device="cuda")
+ecx.fill_random(pool2, pool2.numel(), 6)
+o2 = torch.zeros((S2, 16, B2), dtype=torch.uint8, device="cuda")
+step2.performCodingBatch(pool2, 48 * B2, B2, o2, 16 * B2, B2, S2, B2)
+torch.cuda.synchronize()
+kern2 = ecx.last_kernel()
+assert kern2 != "k_map_planes", kern2
+h2 = pool2[S2 - 1].cpu().numpy()
+ins2 = [None if (i % 6) in (0, 3) else h2[i].copy() for i in range(48)]
+ref2 = [np.zeros(B2, np.uint8) for _ in range(16)]
+O.Clay(4, 2, [0, 3]).perform_coding(ins2, ref2, B2)
+g2 = o2[S2 - 1].cpu().numpy()
+assert all((g2[z] == ref2[z]).all() for z in range(16))
+print("fallback ok", kern, kern2)
+"""
+
+
+def test_generated_kernels_fall_back_without_hiprtc(tmp_path):
+    """No usable libhiprtc: the auto Clay(10,4) repair and the auto Clay(4,2) two-node
+    repair run the composed-map kernels instead of the generated ones, with oracle-exact
+    results; forcing the generated kernel (clay_rtc 2) fails loudly with ECX_E_DEVICE.
+    A child process, because hiprtc is bound once per process."""
+    import os
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, ECX_HIPRTC_LIB=str(tmp_path / "no-libhiprtc.so"),
+               PYTHONPATH=os.pathsep.join([str(root), str(root / "oracle")]))
+    r = subprocess.run([sys.executable, "-c", _NO_HIPRTC_SCRIPT, str(root / "tests")], capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "fallback ok" in r.stdout
 
 
 def test_clay_rtc_kernel_far_stripes(ecx, torch_dev):

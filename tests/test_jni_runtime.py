@@ -1,0 +1,305 @@
+"""The JNI binding EXECUTED: the generated forwarders of jni/ecx_jni.c, compiled with a
+fake JNIEnv over C memory (tests/native/jni_fake_env.c; no JDK in this image) and linked
+to libecx.so, are called the way EcxNative's natives would be.
+
+CPU: every argument check the forwarders run before pinning returns the status of the
+exception the reference throws (ReedSolomon.checkBuffersAndSizes, ReedSolomon.java:338-363;
+"Invalid inputs/outputs length", ClayCodeErasureDecodingStep.java:76-82;
+ArrayIndexOutOfBoundsException of the CodingLoop byte loop, InputOutputByteTableCodingLoop
+.java:34-41) without reaching the export, null Clay sub-chunks pass, the planner entry
+points return the reference's values through the binding, and every pin is released
+with no JNI call made inside a critical region.
+GPU: codeSomeShards (RS(4,2) parity rows), the RS codec calls, decodeMissingSingle and
+clayPerformCoding (Clay(4,2), e = 1) through the binding equal the oracle, with array
+positions (ByteBuffer.arrayOffset + position) applied."""
+import numpy as np
+import pytest
+
+import oracle as O
+from jni_harness import Jni
+
+OK, ILL, NSH, IDX, NUL, DEV = 0, -1, -2, -5, -6, -10
+
+
+@pytest.fixture(scope="module")
+def jni():
+    j = Jni()
+    yield j
+    j.free_all()
+
+
+@pytest.fixture
+def J(jni):
+    jni.reset()
+    yield jni
+    c = jni.counters()
+    assert c["pins_now"] == 0 and c["pins"] == c["unpins"], c
+    assert c["violations"] == 0 and c["calls_while_pinned"] == 0, c
+
+
+def has_device(J):
+    n = np.zeros(1, np.int32)
+    return J.call("deviceCount", J.array(n)) == OK and n[0] > 0
+
+
+def handle(J, fn, *args):
+    h = np.zeros(1, np.int64)
+    assert J.call(fn, *args, J.array(h)) == OK
+    assert h[0] != 0
+    return int(h[0])
+
+
+def rnd(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+# ---------------------------------------------------------------- CPU: argument checks
+def test_code_some_shards_argument_checks(J):
+    rows = np.ones(2 * 4, np.uint8)
+    ins = [rnd(64, i) for i in range(4)]
+    outs = [np.zeros(64, np.uint8) for _ in range(2)]
+    call = lambda rows_, ins_, outs_, nin=4, nout=2, off=0, bc=64, ipos=None, opos=None: J.call(  # noqa: E731
+        "codeSomeShards", J.array(rows_), J.array2d(ins_), J.ints(ipos) if ipos is not None else None, nin,
+        J.array2d(outs_), J.ints(opos) if opos is not None else None, nout, off, bc)
+    assert call(rows[:7], ins, outs) == IDX                       # matrixRows too short
+    assert call(rows, ins[:3], outs) == IDX                       # fewer inputs than inputCount
+    assert call(rows, ins[:3] + [rnd(63, 9)], outs) == IDX        # an input shorter than offset + byteCount
+    assert call(rows, ins, outs[:1] + [np.zeros(10, np.uint8)]) == IDX  # a short output
+    assert call(rows, ins, outs, off=8, bc=57) == IDX             # offset + byteCount past the shards
+    assert call(rows, ins, outs, ipos=[0, 0, 1, 0]) == IDX       # position + byteCount past a shard
+    assert call(rows, ins, outs, ipos=[0, -1, 0, 0]) == IDX      # negative position
+    assert call(rows, ins, outs, ipos=[0, 0]) == ILL             # positions shorter than the list
+    assert call(rows, ins[:2] + [None] + ins[3:], outs) == NUL    # null input shard
+    assert call(rows, ins, outs, off=-1) == ILL
+    assert call(rows, ins, outs, bc=-1) == ILL
+    assert call(None, ins, outs) == NUL
+    assert J.counters()["pins"] == 0  # nothing above was pinned: rejected before the export
+    assert all((o == 0).all() for o in outs)
+
+
+def test_rs_codec_argument_checks(J):
+    rs = handle(J, "rsCreate", 4, 2)
+    try:
+        shards = [rnd(100, i) for i in range(6)]
+        enc = lambda sh, count=6, length=100, off=0, bc=100, pos=None: J.call(  # noqa: E731
+            "rsEncodeParity", rs, J.array2d(sh), J.ints(pos) if pos is not None else None, count, length, off, bc)
+        assert enc(shards[:5]) == ILL                             # wrong number of shards (:341-343)
+        assert enc(shards[:5] + [rnd(99, 7)]) == ILL              # shards of different sizes (:346-351)
+        assert enc(shards, pos=[0, 0, 0, 0, 0, 1]) == ILL         # position leaves fewer than shardLength bytes
+        assert enc(shards[:5] + [None]) == NUL
+        assert enc(shards, off=-1) == ILL and enc(shards, bc=-1) == ILL
+        present = np.ones(6, np.uint8)
+        assert J.call("rsDecodeMissing", rs, J.array2d(shards), None, J.array(present[:5]), 6, 100, 0, 100) == IDX
+        assert J.call("rsIsParityCorrect", rs, J.array2d(shards), None, 6, 100, 0, 100, J.array(rnd(50, 1)), 100) == ILL
+        # encodeParitySingle (EcxPartialSums): outputs the caller supplies are checked too
+        assert J.call("rsEncodeParitySingle", rs, J.array(rnd(100, 1)), J.array(np.zeros(99, np.uint8)), 0, 0, 0,
+                      100) == IDX
+        assert J.call("rsEncodeParitySingle", rs, J.array(rnd(10, 1)), J.array(np.zeros(100, np.uint8)), 0, 0, 0,
+                      100) == IDX
+        pres = np.array([0, 1, 1, 1, 1, 1], np.uint8)
+        outs = [np.zeros(100, np.uint8)]
+        assert J.call("rsDecodeMissingSingle", rs, J.array(rnd(100, 2)), 1, 0, J.array(pres[:4]), J.array2d(outs),
+                      None, 1, 0, 100, 1) == IDX
+        assert J.call("rsDecodeMissingSingle", rs, J.array(rnd(100, 2)), 1, 0, J.array(pres),
+                      J.array2d([np.zeros(50, np.uint8)]), None, 1, 0, 100, 1) == IDX
+        assert J.call("rsMatrix", rs, J.array(np.zeros(6 * 4 - 1, np.uint8))) == IDX
+        assert J.call("rsEncodeParity", 0, J.array2d(shards), None, 6, 100, 0, 100) == NUL  # handle 0
+        assert J.counters()["pins"] == 0
+    finally:
+        J.call("rsDestroy", rs)
+
+
+def test_clay_perform_coding_argument_checks(J):
+    clay = handle(J, "clayCreate", 4, 2, J.ints([1]), 1)
+    J.reset()
+    try:
+        n, a, B = 6, 8, 64
+        ins = [None if i % n == 1 else rnd(B, i) for i in range(n * a)]
+        outs = [np.zeros(B, np.uint8) for _ in range(a)]
+        pc = lambda i, o, bs=B, ipos=None: J.call("clayPerformCoding", clay, J.array2d(i),  # noqa: E731
+                                                 J.ints(ipos) if ipos is not None else None, J.array2d(o), None, bs)
+        assert pc(ins[:-1], outs) == ILL                  # Invalid inputs length (:76-78)
+        assert pc(ins + [rnd(B, 0)], outs) == ILL         # ... not fewer, not more
+        assert pc(ins, outs[:-1]) == ILL                  # Invalid outputs length (:80-82)
+        assert pc(ins, outs[:-1] + [np.zeros(B - 1, np.uint8)]) == IDX
+        assert pc(ins, outs[:-1] + [None]) == NUL
+        short = list(ins)
+        short[2] = rnd(B - 1, 3)
+        assert pc(short, outs) == IDX                     # a helper sub-chunk shorter than bufSize
+        assert pc(ins, outs, ipos=[0] * (n * a - 1) + [1]) == IDX
+        assert pc(ins, outs, bs=-1) == ILL
+        assert J.counters()["pins"] == 0
+        # null inputs (absent sub-chunks) pass the checks and reach the device
+        st = pc(ins, outs)
+        assert st == (OK if has_device(J) else DEV), st
+        hp = np.zeros(1, np.int32)
+        assert J.call("clayHelperPlanes", clay, 1, J.array(hp)) == IDX  # needs alpha/q = 4 entries
+    finally:
+        J.call("clayDestroy", clay)
+
+
+def test_clay_nothing_erased_returns_before_length_checks(J):
+    """performCoding with no erased index returns at once (:54-56), even for arrays of
+    the wrong length."""
+    clay = handle(J, "clayCreate", 4, 2, J.ints([]), 0)
+    try:
+        assert J.call("clayPerformCoding", clay, J.array2d([rnd(8, 1)]), None, J.array2d([]), None, 8) == OK
+    finally:
+        J.call("clayDestroy", clay)
+
+
+def test_handles_and_out_arrays(J):
+    assert J.call("rsCreate", 4, 2, J.array(np.zeros(0, np.int64))) == IDX  # long[0] for the handle
+    assert J.call("rsCreate", 4, 2, None) == NUL
+    assert J.call("mapInfo", 0, None, None, None) == NUL
+    assert J.call("clayGeometry", 0, None, None, None) == NUL
+    assert J.call("matrixTimes", J.array(np.ones(6, np.uint8)), -2, -3, J.array(np.ones(6, np.uint8)), 3, 2,
+                  J.array(np.zeros(4, np.uint8))) == ILL
+    assert J.call("matrixInvert", J.array(np.ones(8, np.uint8)), 3, J.array(np.zeros(9, np.uint8))) == IDX
+
+
+# ---------------------------------------------------------------- CPU: planner through the binding
+def test_planner_calls_through_binding(J, kats):
+    assert J.call("gfMultiply", 3, 7) == O.gf_multiply(3, 7)
+    t = kats["matrix"]["times"]
+    a, b = np.array(t["a"], np.uint8), np.array(t["b"], np.uint8)
+    out = np.zeros((a.shape[0], b.shape[1]), np.uint8)
+    assert J.call("matrixTimes", J.array(a), a.shape[0], a.shape[1], J.array(b), b.shape[0], b.shape[1],
+                  J.array(out)) == OK
+    assert out.tolist() == t["out"]
+    case = kats["matrix"]["invert"][0]
+    m = np.array(case["m"], np.uint8)
+    inv = np.zeros_like(m)
+    assert J.call("matrixInvert", J.array(m), m.shape[0], J.array(inv)) == OK
+    assert inv.tolist() == case["inv"]
+    log, exp, mul = np.zeros(256, np.int16), np.zeros(510, np.uint8), np.zeros(65536, np.uint8)
+    assert J.call("gfTables", J.array(log), J.array(exp), J.array(mul)) == OK
+    assert log.tolist() == kats["galois"]["log_table"] and (mul.reshape(256, 256) == O.mul_table()).all()
+    assert J.string(J.call("statusString", -5)).startswith("ArrayIndexOutOfBounds") or J.string(
+        J.call("statusString", -5))
+
+    rs = handle(J, "rsCreate", 17, 3)
+    try:
+        k, m_ = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        assert J.call("rsShape", rs, J.array(k), J.array(m_)) == OK and (k[0], m_[0]) == (17, 3)
+        mat = np.zeros((20, 17), np.uint8)
+        assert J.call("rsMatrix", rs, J.array(mat)) == OK
+        assert (mat == O.ReedSolomon(17, 3).matrix).all()
+    finally:
+        J.call("rsDestroy", rs)
+
+    clay = handle(J, "clayCreateShortened", 10, 4, 2, J.ints([3]), 1)
+    try:
+        q, t_, al = (np.zeros(1, np.int32) for _ in range(3))
+        assert J.call("clayGeometry", clay, J.array(q), J.array(t_), J.array(al)) == OK
+        assert (q[0], t_[0], al[0]) == (4, 4, 256)
+        nodes, ne = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        assert J.call("clayShape", clay, J.array(nodes), J.array(ne), J.array(al)) == OK
+        assert (nodes[0], ne[0], al[0]) == (14, 1, 256)
+        hp = np.zeros(64, np.int32)
+        assert J.call("clayHelperPlanes", clay, 3, J.array(hp)) == 64
+    finally:
+        J.call("clayDestroy", clay)
+
+    mat = np.arange(1, 13, dtype=np.uint8).reshape(3, 4)
+    mp = handle(J, "mapCreate", J.array(mat), 3, 4, J.ints([0, 2, 4, 6]), J.ints([1, 3, 5]))
+    try:
+        no, ni, nnz = (np.zeros(1, np.int32) for _ in range(3))
+        assert J.call("mapInfo", mp, J.array(no), J.array(ni), J.array(nnz)) == OK
+        assert (no[0], ni[0], nnz[0]) == (3, 4, 12)
+        got, ins, outs = np.zeros((3, 4), np.uint8), np.zeros(4, np.int32), np.zeros(3, np.int32)
+        assert J.call("mapMatrix", mp, J.array(got[:2]), J.array(ins), J.array(outs)) == IDX
+        assert J.call("mapMatrix", mp, J.array(got), J.array(ins), J.array(outs)) == OK
+        assert (got == mat).all() and ins.tolist() == [0, 2, 4, 6] and outs.tolist() == [1, 3, 5]
+    finally:
+        J.call("mapDestroy", mp)
+
+
+def test_valid_per_call_reaches_the_export(J):
+    """Well-formed arguments pass every check and reach the device (ECX_E_DEVICE without
+    one: there is no CPU fallback), with every pin released and the outputs released
+    with mode 0 (copy back) and the read-only inputs with JNI_ABORT."""
+    rows = O.ReedSolomon(4, 2).parity_rows.astype(np.uint8).copy()
+    ins = [rnd(64, i) for i in range(4)]
+    outs = [np.zeros(64, np.uint8) for _ in range(2)]
+    st = J.call("codeSomeShards", J.array(rows), J.array2d(ins), None, 4, J.array2d(outs), None, 2, 0, 64)
+    c = J.counters()
+    assert st == (OK if has_device(J) else DEV), st
+    assert c["pins"] == 1 + 4 + 2 and c["last_mode"] == 2  # matrixRows released last, JNI_ABORT
+
+
+# ---------------------------------------------------------------- GPU: results through the binding
+@pytest.mark.gpu
+def test_code_some_shards_via_jni_vs_oracle(J):
+    rows = O.ReedSolomon(4, 2).parity_rows.astype(np.uint8).copy()
+    L, off, pos = 5000, 7, 3
+    ins = [rnd(pos + off + L, 10 + i) for i in range(4)]
+    outs = [rnd(pos + off + L + 5, 20 + i) for i in range(2)]
+    before = [o.copy() for o in outs]
+    st = J.call("codeSomeShards", J.array(rows), J.array2d(ins), J.ints([pos] * 4), 4, J.array2d(outs),
+                J.ints([pos] * 2), 2, off, L)
+    assert st == OK, st
+    ref = [np.zeros(L, np.uint8) for _ in range(2)]
+    O.code_some_shards(rows, [i[pos + off:pos + off + L] for i in ins], ref, 0, L)
+    for o, b, r in zip(outs, before, ref):
+        assert (o[pos + off:pos + off + L] == r).all()
+        assert (o[:pos + off] == b[:pos + off]).all() and (o[pos + off + L:] == b[pos + off + L:]).all()
+    chk = np.zeros(1, np.int32)
+    assert J.call("checkSomeShards", J.array(rows), J.array2d(ins), J.ints([pos] * 4), 4, J.array2d(outs),
+                  J.ints([pos] * 2), 2, off, L, None) == 1
+    outs[1][pos + off + 100] ^= 1
+    assert J.call("checkSomeShards", J.array(rows), J.array2d(ins), J.ints([pos] * 4), 4, J.array2d(outs),
+                  J.ints([pos] * 2), 2, off, L, None) == 0
+    del chk
+
+
+@pytest.mark.gpu
+def test_rs_codec_via_jni_vs_oracle(J):
+    rs = handle(J, "rsCreate", 4, 2)
+    try:
+        L = 4097
+        shards = [rnd(L, 30 + i) for i in range(4)] + [np.zeros(L, np.uint8) for _ in range(2)]
+        assert J.call("rsEncodeParity", rs, J.array2d(shards), None, 6, L, 0, L) == OK
+        ref = [s.copy() for s in shards]
+        ref[4][:] = 0
+        ref[5][:] = 0
+        O.ReedSolomon(4, 2).encode_parity(ref, 0, L)
+        assert all((a == b).all() for a, b in zip(shards, ref))
+        assert J.call("rsIsParityCorrect", rs, J.array2d(shards), None, 6, L, 0, L, None, 0) == 1
+        lost = [s.copy() for s in shards]
+        lost[1][:] = 0
+        lost[4][:] = 0
+        present = np.array([1, 0, 1, 1, 0, 1], np.uint8)
+        assert J.call("rsDecodeMissing", rs, J.array2d(lost), None, J.array(present), 6, L, 0, L) == OK
+        assert all((a == b).all() for a, b in zip(lost, ref))
+        three = np.array([1, 0, 0, 1, 0, 1], np.uint8)
+        assert J.call("rsDecodeMissing", rs, J.array2d(lost), None, J.array(three), 6, L, 0, L) == NSH
+        # decodeMissingSingle: helper 2's share of the missing data shard 1 (ClayCodeNode chain hop)
+        pres = np.array([1, 0, 1, 1, 1, 1], np.uint8)
+        got = [rnd(L, 5)]
+        want = [np.zeros(L, np.uint8)]
+        assert J.call("rsDecodeMissingSingle", rs, J.array(shards[2]), 2, 1, J.array(pres), J.array2d(got), None, 1,
+                      0, L, 1) == OK
+        O.ReedSolomon(4, 2).decode_missing_single(shards[2], 2, 1, [bool(p) for p in pres], want, 0, L, True)
+        assert (got[0] == want[0]).all()
+    finally:
+        J.call("rsDestroy", rs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,pos", [(4096, 0), (1000, 3)])
+def test_clay_perform_coding_via_jni_vs_oracle(J, B, pos):
+    clay = handle(J, "clayCreate", 4, 2, J.ints([1]), 1)
+    try:
+        n, a = 6, 8
+        ins = [None if i % n == 1 else rnd(pos + B, 40 + i) for i in range(n * a)]
+        outs = [np.full(pos + B, 0x77, np.uint8) for _ in range(a)]
+        st = J.call("clayPerformCoding", clay, J.array2d(ins), J.ints([pos] * (n * a)), J.array2d(outs),
+                    J.ints([pos] * a), B)
+        assert st == OK, st
+        ref = [np.zeros(B, np.uint8) for _ in range(a)]
+        O.Clay(4, 2, [1]).perform_coding([None if x is None else x[pos:].copy() for x in ins], ref, B)
+        for o, r in zip(outs, ref):
+            assert (o[pos:] == r).all() and (o[:pos] == 0x77).all()
+    finally:
+        J.call("clayDestroy", clay)

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from conftest import gf_apply_numpy
+from conftest import gf_apply_numpy, shortened_clay_oracle as _shortened_oracle
 
 
 def test_field_tables_match_reference(ecx, kats):
@@ -156,24 +156,6 @@ def test_helper_overload_maps(ecx):
             oc.decode_single_helper(helper, i, ref, e, B)
         step = ecx.ClayCodeErasureDecodingStep([e], k, m)
         assert step.getHelperPlanesIndexes(e) == hidx
-
-
-def _shortened_oracle(k, m, v, erased_real, inputs_real, B):
-    """Oracle for a shortened code: the reference Clay(k+v, m) with the v virtual
-    data nodes zero-filled."""
-    n_r, n_u = k + m, k + v + m
-    und = lambda r: r if r < k else r + v
-    c = O.Clay(k + v, m, [und(e) for e in erased_real])
-    a = c.alpha
-    inputs = [None] * (n_u * a)
-    for z in range(a):
-        for r in range(n_r):
-            inputs[z * n_u + und(r)] = inputs_real[z * n_r + r]
-        for u in range(k, k + v):
-            inputs[z * n_u + u] = np.zeros(B, np.uint8)
-    outs = [np.zeros(B, np.uint8) for _ in range(len(erased_real) * a)]
-    c.perform_coding(inputs, outs, B)
-    return outs
 
 
 @pytest.mark.parametrize("k,m,v,erased", [(10, 4, 2, [3]), (10, 4, 2, [13]), (10, 4, 2, [10, 11, 12, 13]),
@@ -349,11 +331,17 @@ def test_map_planes_refuses_wide_maps(ecx):
         gm.planes_source()
 
 
-def test_clay_grp_movement_only_build_is_isolated(ecx):
+def test_clay_grp_movement_only_build_is_isolated(ecx, monkeypatch):
     """rtc_lookahead bit 4 (16) generates the plane-group kernel's data-movement-only
     diagnostic build (coefficients as 1, no transposes), marked as such; the next
-    default generation is byte-identical to one made before it."""
+    default generation is byte-identical to one made before it.  Its outputs are not
+    the repair, so ecx_tune refuses the bit unless the process set ECX_DIAGNOSTIC=1."""
     step = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2)
+    monkeypatch.delenv("ECX_DIAGNOSTIC", raising=False)
+    with pytest.raises(ecx.EcxError) as e:
+        ecx.tune("rtc_lookahead", 17)
+    assert e.value.code == -1
+    monkeypatch.setenv("ECX_DIAGNOSTIC", "1")
     try:
         before = step.rtcSource()
         ecx.tune("rtc_lookahead", 17)
@@ -364,3 +352,25 @@ def test_clay_grp_movement_only_build_is_isolated(ecx):
         assert step.rtcSource() == before and "DIAGNOSTIC" not in before
     finally:
         ecx.tune("rtc_lookahead", 1)
+
+
+def test_generated_kernels_without_hiprtc(tmp_path):
+    """With no usable libhiprtc (ECX_HIPRTC_LIB names a missing file) the generated-kernel
+    compile reports ECX_E_DEVICE with the reason, instead of crashing; run in a child
+    process because the library is bound once per process."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import rpamd\n"
+        "ecx = rpamd.load()\n"
+        "step = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2)\n"
+        "try:\n"
+        "    step.rtcCompileCheck()\n"
+        "except ecx.EcxError as e:\n"
+        "    print('code', e.code, 'hiprtc' in str(e))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ECX_HIPRTC_LIB=str(tmp_path / "no-libhiprtc.so"), PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "code -10 True" in r.stdout, r.stdout
