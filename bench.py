@@ -30,7 +30,8 @@ contract (same launch, timing and JSON line; the default is the headline):
            data block 2 from its local group, 2^15 resident stripes per GPU
   clay42x2 SURVEY 8(f) f4: Clay(4,2), 32 KiB, two-node repair of nodes {0, 3}
            (doDecodeMulti) over the headline's pool of 2^15 stripes
-The cpu_baseline leg runs for the headline workload only.
+Every workload carries a cpu_baseline (rank 0, after the timed region, at any N): the
+oracle's restatement of the reference path for that workload on this host's cores.
 """
 import argparse
 import json
@@ -144,60 +145,56 @@ def host_cpu_info() -> dict:
             "l3_bytes_machine": l3_all or None, "l3_bytes_affinity": l3_aff or None}
 
 
-def cpu_baseline(seconds: float, erased: int, sample=None):
-    """Oracle (C restatement of the reference JVM path: InputOutputByteTableCodingLoop
-    + the ClayCodeErasureDecodingStep.doDecodeSingle stage sequence), timed by
-    oracle/orc_bench.c on one host thread and then on one thread per CPU the lease
-    allows (the cgroup quota, else the affinity mask; independent stripes per thread,
-    SURVEY.md section 8(d)).  Following ReedSolomonBenchmark.java:25-33, the stripes
-    cycled through span at least twice the machine's L3, so the repairs stream from
-    DRAM as the reference's benchmark does.  ``value`` is the all-threads figure; the
-    1-thread figure rides along.  `sample` = (stripe, GPU repair output) of one pool
-    stripe: the oracle repairs it too, and ``oracle_check`` says whether the bytes
-    agree (the sampled byte-compare of SURVEY.md 8(d))."""
+def cpu_baseline(wl, seconds: float, sample=None, max_units=None):
+    """The oracle (C restatement of the reference JVM path, stage by stage) on this host for
+    workload `wl`, timed by oracle/orc_bench.c: one host thread, then one thread per CPU
+    the lease allows (the cgroup quota, else OMP_NUM_THREADS, else the affinity mask;
+    independent units and codec objects per thread).  Following
+    ReedSolomonBenchmark.java:25-33, the units cycled through span at least twice the
+    machine's L3, so the operations stream from DRAM as the reference's benchmark does.
+    GiB/s counts the workload's own algorithmic bytes per unit (wl.unit_bytes), as the
+    GPU line does.  ``value`` is the all-threads figure; the 1-thread figure rides along.
+    `sample` = (unit, GPU output) of one pool unit: the oracle computes it too, and
+    ``oracle_check`` says whether the bytes agree (the sampled byte-compare of 8(d))."""
     import numpy as np
     import oracle as O
 
+    spec = wl.cpu_spec()
     oracle_check = None
     if sample is not None:
-        stripe, got = sample
-        inputs = [None if (i % N_NODES) == erased else stripe[i].copy() for i in range(N_NODES * ALPHA)]
-        ref = [np.zeros(B, np.uint8) for _ in range(ALPHA)]
-        O.Clay(K, M, [erased]).perform_coding(inputs, ref, B)
-        oracle_check = all(bool((got[z] == ref[z]).all()) for z in range(ALPHA))
+        oracle_check = bool(wl.oracle_check(*sample))
 
     info = host_cpu_info()
     threads = info["cgroup_quota_cpus"] or info["omp_num_threads"] or info["affinity_cpus"]
     threads = max(1, min(threads, info["affinity_cpus"], 256))
-    # Working set: the helper + output bytes a repair touches (ALGO_BYTES), summed over
-    # every stripe cycled through, >= 2x the machine's L3 (32 MiB assumed if unknown).
+    # Working set: the bytes an operation touches (wl.unit_bytes), summed over every unit
+    # cycled through, >= 2x the machine's L3 (32 MiB assumed if unknown).
     l3 = info["l3_bytes_machine"] or (32 << 20)
-    n_stripes = max(2 * threads, -(-2 * l3 // ALGO_BYTES))
-    per_thread = -(-n_stripes // threads)
-    n_stripes = per_thread * threads
-    rng = np.random.default_rng(0)
-
-    # 8 distinct valid stripes (random data + oracle encode), tiled through one host
-    # arena of n_stripes stripes: every stripe has its own memory (the cache sees the
-    # whole working set), the bytes repeat every 8 stripes.
-    distinct = []
-    for _ in range(8):
-        data = [rng.integers(0, 256, B, dtype=np.uint8) if (i % N_NODES) < K else None
-                for i in range(N_NODES * ALPHA)]
-        par = O.clay_encode(K, M, data, B)
-        distinct.append(np.stack([data[i] if (i % N_NODES) < K else par[(i // N_NODES) * M + (i % N_NODES) - K]
-                                  for i in range(N_NODES * ALPHA)]))
-    arena = np.empty((n_stripes, N_NODES * ALPHA, B), np.uint8)
-    for s in range(n_stripes):
-        arena[s] = distinct[s % 8]
-    stripes = [[None if (i % N_NODES) == erased else arena[s, i] for i in range(N_NODES * ALPHA)]
-               for s in range(n_stripes)]
-    n1, el1 = O.bench_clay_repair(K, M, erased, B, stripes, 1, seconds / 2)
-    nn, eln = O.bench_clay_repair(K, M, erased, B, stripes, threads, seconds)
-    one = n1 * ALGO_BYTES / el1 / 2**30
-    ws = n_stripes * ALGO_BYTES
+    n_units = max(2 * threads, -(-2 * l3 // wl.unit_bytes))
+    if max_units:  # tests: a bounded arena
+        threads = min(threads, max_units)
+        n_units = max_units
+    per_thread = -(-n_units // threads)
+    n_units = per_thread * threads
+    # 8 distinct units (spec["make"]: valid stripes, or random bytes where the oracle's work
+    # does not depend on the data), tiled through one host arena of n_units units: every
+    # unit has its own memory (the cache sees the whole working set).
+    distinct = spec["make"](np.random.default_rng(0))
+    arena = np.empty((n_units,) + distinct[0].shape, np.uint8)
+    for u in range(n_units):
+        arena[u] = distinct[u % len(distinct)]
+    slot_bytes = arena.shape[-1]
+    zero = np.zeros(slot_bytes, np.uint8)  # a shared zero-filled node (shortened Clay's virtual nodes)
+    rows = np.arange(n_units, dtype=np.int64)[:, None] * arena[0].nbytes + arena.ctypes.data
+    addrs = np.where(spec["present"][None, :] == 1, rows + spec["arena_slot"][None, :] * slot_bytes,
+                     np.where(spec["present"][None, :] == 2, zero.ctypes.data, 0)).astype(np.int64)
+    op, data, parity, erased = spec["op"], spec["data"], spec["parity"], spec["erased"]
+    n1, el1 = O.bench_run(op, data, parity, erased, slot_bytes, addrs, 1, seconds / 2)
+    nn, eln = O.bench_run(op, data, parity, erased, slot_bytes, addrs, threads, seconds)
+    one = n1 * wl.unit_bytes / el1 / 2**30
+    ws = n_units * wl.unit_bytes
     return {
-        "value": round(nn * ALGO_BYTES / eln / 2**30, 3),
+        "value": round(nn * wl.unit_bytes / eln / 2**30, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
@@ -205,12 +202,12 @@ def cpu_baseline(seconds: float, erased: int, sample=None):
         "oracle_check": oracle_check,
         "working_set_bytes": ws,
         "host": info,
-        "sample": f"Clay(4,2) single repairs (e={erased}, B=32 KiB), stage-by-stage C restatement of the "
-                  f"reference JVM path (oracle/): {nn} repairs on {threads} threads (lease quota "
-                  f"{info['cgroup_quota_cpus']}, affinity {info['affinity_cpus']} of {info['cpus_present']} CPUs) "
-                  f"x {per_thread} host-resident valid stripes each, {ws / 2**20:.0f} MiB touched "
-                  f"(>= 2x the {l3 / 2**20:.0f} MiB L3), in {eln:.1f} s; single thread {n1} repairs over "
-                  f"all {n_stripes} stripes in {el1:.1f} s; {info['model']}",
+        "sample": f"{spec['what']}, stage-by-stage C restatement of the reference JVM path (oracle/): {nn} "
+                  f"operations on {threads} threads (lease quota {info['cgroup_quota_cpus']}, affinity "
+                  f"{info['affinity_cpus']} of {info['cpus_present']} CPUs) x {per_thread} host-resident "
+                  f"{spec['data_kind']} units each, {ws / 2**20:.0f} MiB of algorithmic bytes touched "
+                  f"(>= 2x the {l3 / 2**20:.0f} MiB L3), in {eln:.1f} s; single thread {n1} operations over all "
+                  f"{n_units} units in {el1:.1f} s; {info['model']}",
     }
 
 
@@ -307,6 +304,21 @@ class Workload:
     def verify(self) -> bool:
         raise NotImplementedError
 
+    def sample(self):
+        """(one pool unit, the GPU's output for it) as host arrays, for oracle_check."""
+        raise NotImplementedError
+
+    def oracle_check(self, unit, got) -> bool:
+        """The oracle's result for `unit` equals the GPU's `got`."""
+        raise NotImplementedError
+
+    def cpu_spec(self) -> dict:
+        """How cpu_baseline runs the oracle on this workload: op / data / parity / erased
+        for orc_bench_run, make(rng) -> distinct host units [slots][bytes], and per oracle
+        slot the arena slot it reads (arena_slot) and whether it is present (1), absent
+        (0) or a shared zero node (2)."""
+        raise NotImplementedError
+
 
 class Clay42(Workload):
     """Config 2 (headline): Clay(4,2), B = 32 KiB, single-node repair."""
@@ -330,6 +342,40 @@ class Clay42(Workload):
 
     def verify(self):
         return bool(self.torch.equal(self.out, self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.erased, :]))
+
+    erased_list = property(lambda self: [self.erased])
+
+    def sample(self):
+        return self.pool[self.P // 2].cpu().numpy(), self.out[self.P // 2].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import numpy as np
+        import oracle as O
+        er = self.erased_list
+        inputs = [None if (i % N_NODES) in er else stripe[i].copy() for i in range(N_NODES * ALPHA)]
+        ref = [np.zeros(B, np.uint8) for _ in range(ALPHA * len(er))]
+        O.Clay(K, M, er).perform_coding(inputs, ref, B)
+        return all(bool((got[z] == ref[z]).all()) for z in range(len(ref)))
+
+    def cpu_spec(self):
+        import numpy as np
+        import oracle as O
+        er = self.erased_list
+
+        def make(rng):  # valid stripes: random data + oracle encode
+            out = []
+            for _ in range(8):
+                data = [rng.integers(0, 256, B, dtype=np.uint8) if (i % N_NODES) < K else None
+                        for i in range(N_NODES * ALPHA)]
+                par = O.clay_encode(K, M, data, B)
+                out.append(np.stack([data[i] if (i % N_NODES) < K else par[(i // N_NODES) * M + (i % N_NODES) - K]
+                                     for i in range(N_NODES * ALPHA)]))
+            return out
+        slots = np.arange(N_NODES * ALPHA)
+        present = np.array([0 if (i % N_NODES) in er else 1 for i in slots], np.int64)
+        return {"op": O.BENCH_CLAY, "data": K, "parity": M, "erased": er, "make": make, "arena_slot": slots,
+                "present": present, "data_kind": "valid-stripe",
+                "what": "Clay(4,2) repairs of nodes %s (B=32 KiB)" % er}
 
 
 class Clay42x2(Clay42):
@@ -355,6 +401,8 @@ class Clay42x2(Clay42):
         e = len(self.ERASED)
         want = self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.ERASED, :]
         return bool(self.torch.equal(self.out.view(self.P, ALPHA, e, B), want))
+
+    erased_list = property(lambda self: list(self.ERASED))
 
 
 class Clay104(Workload):
@@ -391,6 +439,41 @@ class Clay104(Workload):
         orig = self.pool.view(self.P, self.alpha, self.n, self.b)[:, :, self.erased, :]
         return bool(self.torch.equal(self.out, orig))
 
+    def sample(self):
+        return self.pool[self.P // 2].cpu().numpy(), self.out[self.P // 2].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import oracle as O
+        n, a = self.n, self.alpha
+        inputs = [None if (i % n) == self.erased else stripe[i].copy() for i in range(n * a)]
+        ref = O.shortened_clay_perform_coding(self.k, self.m, self.v, [self.erased], inputs, self.b)
+        return all(bool((got[z] == ref[z]).all()) for z in range(a))
+
+    def cpu_spec(self):
+        """The reference cannot build Clay(10,4) (integer t = (k+m)/m): its
+        path for this config is Clay(12,4) with the 2 virtual data nodes zero-filled."""
+        import numpy as np
+        import oracle as O
+        k, m, v, a = self.k, self.m, self.v, self.alpha
+        n_r, n_u = k + m, k + v + m
+        e_u = self.erased if self.erased < k else self.erased + v
+        arena_slot, present = [], []
+        for z in range(a):
+            for u in range(n_u):
+                virtual = k <= u < k + v
+                r = u if u < k else u - v
+                arena_slot.append(0 if virtual else z * n_r + r)
+                present.append(2 if virtual else (0 if u == e_u else 1))
+
+        def make(rng):  # random bytes: the oracle's work does not depend on the data
+            return [rng.integers(0, 256, (n_r * a, self.b), dtype=np.uint8) for _ in range(2)]
+        return {"op": O.BENCH_CLAY, "data": k + v, "parity": m, "erased": [e_u], "make": make,
+                "arena_slot": np.array(arena_slot, np.int64), "present": np.array(present, np.int64),
+                "data_kind": "random-byte",
+                "what": "Clay(10,4) repairs of node %d as the reference runs them: Clay(12,4) with the 2 virtual "
+                        "data nodes zero-filled, 256 x 4 KiB sub-chunks; GiB/s over the shortened map's "
+                        "algorithmic bytes" % self.erased}
+
 
 class RS124(Workload):
     """Config 5: RS(12,4), 4 MiB shards, erasures {0,1} decoded in place (the first 12
@@ -420,6 +503,28 @@ class RS124(Workload):
 
     def verify(self):
         return bool(self.torch.equal(self.pool[:, 0:2, :self.L], self.orig))
+
+    def sample(self):
+        s = self.P // 2
+        return self.pool[s, :, :self.L].cpu().numpy(), self.pool[s, 0:2, :self.L].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import numpy as np
+        import oracle as O
+        shards = [np.zeros(self.L, np.uint8) if i < 2 else stripe[i].copy() for i in range(16)]
+        O.ReedSolomon(self.k, self.m).decode_missing(shards, [i >= 2 for i in range(16)], 0, self.L)
+        return bool((shards[0] == got[0]).all() and (shards[1] == got[1]).all())
+
+    def cpu_spec(self):
+        import numpy as np
+        import oracle as O
+
+        def make(rng):  # random bytes: decodeMissing's work does not depend on the data
+            return [rng.integers(0, 256, (16, self.L), dtype=np.uint8) for _ in range(2)]
+        return {"op": O.BENCH_RS_DECODE, "data": self.k, "parity": self.m, "erased": [0, 1], "make": make,
+                "arena_slot": np.arange(16), "present": np.ones(16, np.int64), "data_kind": "random-byte",
+                "what": "RS(12,4) decodeMissing of shards {0, 1} in place (first-k-present rule, sub-matrix "
+                        "inverted per call as ReedSolomon.java:224-244 does), 4 MiB shards"}
 
 
 class LRC(Workload):
@@ -454,6 +559,29 @@ class LRC(Workload):
 
     def verify(self):
         return bool(self.torch.equal(self.out[:, 0], self.pool[:, 2]))
+
+    def sample(self):
+        s = self.P // 2
+        return self.pool[s].cpu().numpy(), self.out[s].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import numpy as np
+        import oracle as O
+        group = [stripe[i].copy() for i in range(4)]
+        group[2] = np.zeros(self.b, np.uint8)
+        O.ReedSolomon(3, 1).decode_missing(group, [True, True, False, True], 0, self.b)
+        return bool((group[2] == got[0]).all())
+
+    def cpu_spec(self):
+        import numpy as np
+        import oracle as O
+
+        def make(rng):  # the local group of block 2 (blocks 0-3), random bytes
+            return [rng.integers(0, 256, (4, self.b), dtype=np.uint8) for _ in range(8)]
+        return {"op": O.BENCH_RS_DECODE, "data": 3, "parity": 1, "erased": [2], "make": make,
+                "arena_slot": np.arange(4), "present": np.ones(4, np.int64), "data_kind": "random-byte",
+                "what": "LRC local-group repairs of data block 2: RS(3,1).decodeMissing over its group "
+                        "(LRCErasureCodeExample.kt:100-131), 64 KiB blocks"}
 
 
 def launch_ranks(args) -> int:
@@ -563,6 +691,7 @@ def main():
     if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
+    own_el = el
     if grouped:
         t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -575,14 +704,22 @@ def main():
     value = total_stripes * wl.unit_bytes / el / 2**30
     traffic, traffic_note = pmc_traffic(args.workload, P, kernel)
 
+    # per-rank rates, so an N-GPU efficiency shortfall can be attributed to a rank
+    per_rank = [own_el]
+    if grouped:
+        g = [torch.zeros(1, dtype=torch.float64, device=dev if backend == "nccl" else "cpu") for _ in range(world)]
+        dist.all_gather(g, torch.tensor([own_el], dtype=torch.float64, device=g[0].device))
+        per_rank = [float(x.item()) for x in g]
+    per_rank_gibs = [stripes_per_step * args.steps * wl.unit_bytes / e / 2**30 for e in per_rank]
+
     sample = None
-    if args.workload == "clay42" and rank == 0 and world == 1 and args.cpu_seconds > 0:
-        sample = (wl.pool[P // 2].cpu().numpy(), wl.out[P // 2].cpu().numpy())  # one stripe for the oracle check
+    if rank == 0 and args.cpu_seconds > 0:
+        sample = wl.sample()  # one pool unit for the oracle check
     probes = memory_probes(ecx, torch, wl.region, wl.reads, wl.writes) if not args.no_probes else None
 
     cpu = None
-    if sample is not None:
-        cpu = cpu_baseline(args.cpu_seconds, args.erased, sample)
+    if sample is not None:  # rank 0 only, after the timed region (at any N)
+        cpu = cpu_baseline(wl, args.cpu_seconds, sample)
 
     if rank == 0 and args.meta:
         Path(args.meta).write_text(json.dumps({
@@ -625,6 +762,8 @@ def main():
                 "frac_of_mix_model": round(achieved / probes["mix_model_GBps"], 4) if probes else None,
             },
             "repaired_output_GiBps": round(total_stripes * wl.write_bytes / el / 2**30, 3),
+            "per_rank_GiBps": {"min": round(min(per_rank_gibs), 3), "max": round(max(per_rank_gibs), 3),
+                               "ranks": [round(v, 3) for v in per_rank_gibs]},
             "cpu_baseline": cpu,
             "verified": verified,
         }

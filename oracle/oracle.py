@@ -96,6 +96,8 @@ def _load():
         "orc_clay_get_inputs": (I, [I, I, I, P, P]),
         "orc_bench_clay_repair": (I, [I, I, I, I, PP, I, I, ctypes.c_double,
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]),
+        "orc_bench_run": (I, [I, I, I, P, I, I, P, I, I, I, ctypes.c_double,
+                              ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -323,6 +325,44 @@ def bench_clay_repair(data_units, parity_units, erased, block_size, stripes, thr
     reps, el = ctypes.c_longlong(0), ctypes.c_double(0.0)
     _check(lib().orc_bench_clay_repair(data_units, parity_units, erased, block_size, _ptrs(flat), per, threads,
                                        float(seconds), ctypes.byref(reps), ctypes.byref(el)))
+    return int(reps.value), float(el.value)
+
+
+def shortened_clay_perform_coding(k, m, v, erased_real, inputs_real, B):
+    """A shortened Clay code: the reference Clay(k+v, m)
+    (ClayCodeErasureDecodingStep.java:53-107) run with the v virtual data nodes
+    zero-filled.  inputs_real / the result use the REAL node numbering of the shortened
+    code (slot z*(k+m) + node; output z*|E| + j)."""
+    n_r, n_u = k + m, k + v + m
+    und = lambda r: r if r < k else r + v  # noqa: E731
+    c = Clay(k + v, m, [und(e) for e in erased_real])
+    a = c.alpha
+    zero = np.zeros(B, np.uint8)
+    inputs = [None] * (n_u * a)
+    for z in range(a):
+        for r in range(n_r):
+            inputs[z * n_u + und(r)] = inputs_real[z * n_r + r]
+        for u in range(k, k + v):
+            inputs[z * n_u + u] = zero
+    outs = [np.zeros(B, np.uint8) for _ in range(len(erased_real) * a)]
+    c.perform_coding(inputs, outs, B)
+    return outs
+
+
+BENCH_CLAY, BENCH_RS_DECODE, BENCH_RS_ENCODE = 0, 1, 2
+
+
+def bench_run(op, data, parity, erased, buf_size, addrs, threads, seconds):
+    """Timing harness (orc_bench.c orc_bench_run): `addrs` is an int64 array [units][slots]
+    of host addresses (0 = absent) -- Clay: n*alpha sub-chunks per unit; RS: n shards --
+    split evenly over `threads` workers.  Returns (operations, max elapsed seconds)."""
+    addrs = np.ascontiguousarray(addrs, dtype=np.int64)
+    units, slots = addrs.shape
+    per = units // threads
+    er = np.ascontiguousarray(list(erased) or [0], dtype=np.int32)
+    reps, el = ctypes.c_longlong(0), ctypes.c_double(0.0)
+    _check(lib().orc_bench_run(op, data, parity, _ptr(er), len(erased), buf_size, _ptr(addrs), slots, per, threads,
+                               float(seconds), ctypes.byref(reps), ctypes.byref(el)))
     return int(reps.value), float(el.value)
 
 

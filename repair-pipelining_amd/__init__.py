@@ -433,6 +433,14 @@ class GfMap:
         check(f(self._h, *[ctypes.byref(x) for x in v]))
         return dict(zip(["tiles", "entries", "groups", "union_total"], [x.value for x in v]))
 
+    def skew_choice(self, slot_pitch: int) -> int:
+        """The skewed-chunk choice measured for this map at an input slot pitch
+        (ecx_map_skew_choice, include/ecx_tune.h "skew_trial"): 1 skewed, 0 one chunk
+        per workgroup, -1 not measured."""
+        f = lib().ecx_map_skew_choice
+        f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_int64], ctypes.c_int
+        return f(self._h, int(slot_pitch))
+
     def _check(self, inp, iss, isl, out, oss, osl, nstripes, nbytes):
         mi, mo = self.max_slots()
         _check_layout(inp, iss, isl, mi, nstripes, nbytes, "input")

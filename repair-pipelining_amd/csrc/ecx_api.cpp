@@ -1026,6 +1026,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 4 || value == 3) return ECX_E_ILLEGAL_ARGUMENT;
         t.skew_chunks = value;
     }
+    else if (k == "skew_trial") {
+        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        t.skew_trial = value;
+    }
     else if (k == "wide_tiles") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.wide_tiles = value;
@@ -1122,6 +1126,11 @@ int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_
         if (union_total) *union_total = cm.union_total();
         return ECX_OK;
     });
+}
+
+int ecx_map_skew_choice(const ecx_map *map, int64_t slot_pitch) {
+    if (!map || slot_pitch <= 0) return ECX_E_ILLEGAL_ARGUMENT;
+    return const_cast<ecx_map *>(map)->cm.skew_choice(slot_pitch % ((int64_t)16 << 20));
 }
 
 int ecx_last_kernel(char *buf, int len) {

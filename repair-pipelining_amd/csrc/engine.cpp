@@ -648,6 +648,17 @@ MapPlanes *CompiledMap::planes() {
     return planes_.get();
 }
 
+int CompiledMap::skew_choice(int64_t pitch_key) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = skew_choice_.find(pitch_key);
+    return it == skew_choice_.end() ? -1 : it->second;
+}
+
+void CompiledMap::set_skew_choice(int64_t pitch_key, int choice) {
+    std::lock_guard<std::mutex> lk(mu_);
+    skew_choice_[pitch_key] = choice;
+}
+
 const std::vector<int> &CompiledMap::used_in_slots() {
     compact();
     return used_in_;

@@ -142,8 +142,13 @@ public:
     MapPlanes *planes();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
+    // The measured skewed-chunk choice (skew_trial) for an input slot pitch key:
+    // -1 = not measured yet, 0 = one chunk per workgroup, 1 = skewed.
+    int skew_choice(int64_t pitch_key);
+    void set_skew_choice(int64_t pitch_key, int choice);
 
 private:
+    std::map<int64_t, int> skew_choice_;
     LinearMap map_;
     std::unique_ptr<CompiledMap> compact_;
     std::unique_ptr<MapPlanes> planes_;
@@ -221,6 +226,9 @@ struct Tuning {
     // workgroup, each entry's chunk rotated; 1 = 4 when the input slot pitch is a
     // multiple of 4 MiB; 0 = off.
     int skew_chunks = 1;
+    // skew_chunks auto: 1 = measure skewed vs one-chunk launches on the first large batch
+    // per (map, input slot pitch mod 16 MiB) and keep the faster; 0 = the static rule
+    int skew_trial = 1;
     // Per-call CodingLoop entry points: compiled plans kept, by map content (0 = none).
     int plan_cache = 256;
     // Bit-sliced kernel (k_gf_bits): 2 = for every map it can run (aligned layout, 32-bit

@@ -236,9 +236,11 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
         uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)), lane16, valid, nullptr);
 }
 
-void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
-                  int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
-                  hipStream_t stream, bool accumulate) {
+namespace {
+// skew_pick: -1 = the static rule (4 MiB-multiple input slot pitch), 0 / 1 = forced off / on
+void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                       uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                       int64_t nbytes, hipStream_t stream, bool accumulate, int skew_pick) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
     const Tuning &tu = tuning();
     const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
@@ -250,7 +252,8 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     // (64) or, in auto (0), for single-tile maps of <= 2 rows over >= 8 inputs whose slot
     // pitch is not a 4 MiB multiple (RS(12,4) decode on its padded pitch: +2.4-2.8 %; every
     // other BASELINE map is 3-8 % slower on one wave, profiles/r02_block_threads.jsonl).
-    const bool skew_pitch = in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4;
+    const bool skew_pitch = skew_pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4
+                                          : skew_pick == 1;
     const bool one_wave = tu.block_threads == 64 ||
                           (tu.block_threads == 0 && cm.n_tiles() == 1 && cm.max_tile_rows() <= 2 &&
                            cm.map().n_in >= 8 && !skew_pitch && tu.bitslice != 2 && !tu.lds_lut);
@@ -479,6 +482,76 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     run(false, first, full - first);
     run(true, full, tail_chunks);
     check_hip(hipGetLastError(), "k_gf_apply launch");
+}
+}  // namespace
+
+// The slot pitch decides whether rotating the chunk order pays (k_gf_apply_skew), and no
+// simple rule predicts it beyond "4 MiB multiples gain" (pitch sweep).  So on
+// the first large batch of a map at a new pitch (mod 16 MiB), both launches run on a
+// sample of the batch's own stripes, three rounds each on the caller's stream, and the
+// faster is kept for that (map, pitch).  The trial writes the same outputs the real launch
+// then rewrites, so it is only done where that is harmless: overwrite mode, outputs not
+// aliasing inputs, no stream capture.
+void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
+                  int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
+                  hipStream_t stream, bool accumulate) {
+    const Tuning &tu = tuning();
+    const LinearMap &m = cm.map();
+    const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
+                         (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
+    const int64_t in_bytes = (int64_t)m.n_in * nbytes;  // per stripe
+    bool trial = tu.skew_chunks == 1 && tu.skew_trial && tu.block_threads == 0 && !accumulate && !tu.lds_lut &&
+                 tu.bitslice != 2 && tu.nontemporal != 0 && tu.store_scope == 0 && cm.n_tiles() == 1 &&
+                 m.n_in >= 4 && m.n_out > 0 && aligned && in_slot_stride > 0 && nbytes >= 4 * kChunkBytes &&
+                 nstripes * in_bytes >= ((int64_t)64 << 20);
+    const int64_t key = trial ? in_slot_stride % ((int64_t)16 << 20) : 0;
+    int pick = trial ? cm.skew_choice(key) : -1;
+    if (trial && pick < 0) {
+        // outputs must not alias inputs: disjoint byte ranges, or the same layout with
+        // disjoint slot sets (in-place decodeMissing)
+        const int64_t in_end = (nstripes - 1) * in_stripe_stride + (int64_t)cm.max_in_slot() * in_slot_stride + nbytes;
+        const int64_t out_end =
+            (nstripes - 1) * out_stripe_stride + (int64_t)cm.max_out_slot() * out_slot_stride + nbytes;
+        const bool disjoint = out + out_end <= in || in + in_end <= out;
+        bool same_layout_ok = in == out && in_stripe_stride == out_stripe_stride && in_slot_stride == out_slot_stride;
+        if (same_layout_ok)
+            for (int o : m.out_slot)
+                for (int j : m.in_slot) same_layout_ok = same_layout_ok && o != j;
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(stream, &cap) != hipSuccess) {
+            (void)hipGetLastError();
+            cap = hipStreamCaptureStatusActive;  // unknown: do not run the trial
+        }
+        if ((disjoint || same_layout_ok) && cap == hipStreamCaptureStatusNone) {
+            const int64_t sample = std::min<int64_t>(nstripes, std::max<int64_t>(1, ((int64_t)256 << 20) / in_bytes));
+            hipEvent_t ev[7];
+            for (auto &e : ev) check_hip(hipEventCreate(&e), "hipEventCreate");
+            float best[2] = {1e30f, 1e30f};
+            try {
+                check_hip(hipEventRecord(ev[0], stream), "hipEventRecord");
+                for (int r = 0; r < 3; ++r)
+                    for (int v = 0; v < 2; ++v) {
+                        launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
+                                          out_slot_stride, sample, nbytes, stream, false, v);
+                        check_hip(hipEventRecord(ev[1 + 2 * r + v], stream), "hipEventRecord");
+                    }
+                check_hip(hipEventSynchronize(ev[6]), "hipEventSynchronize");
+                for (int i = 1; i < 7; ++i) {
+                    float ms = 0.f;
+                    check_hip(hipEventElapsedTime(&ms, ev[i - 1], ev[i]), "hipEventElapsedTime");
+                    best[(i - 1) % 2] = std::min(best[(i - 1) % 2], ms);
+                }
+            } catch (...) {
+                for (auto &e : ev) (void)hipEventDestroy(e);
+                throw;
+            }
+            for (auto &e : ev) (void)hipEventDestroy(e);
+            pick = best[1] < best[0] ? 1 : 0;
+            cm.set_skew_choice(key, pick);
+        }
+    }
+    launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                      nbytes, stream, accumulate, pick);
 }
 
 // ---------------------------------------------------------------- synthetic data

@@ -29,25 +29,10 @@ def ecx():
 
 
 def shortened_clay_oracle(k, m, v, erased_real, inputs_real, B):
-    """Oracle of a shortened Clay code: the reference Clay(k+v, m)
-    (ClayCodeErasureDecodingStep.java:53-107, restated in oracle/ecx_oracle.c) run with
-    the v virtual data nodes zero-filled.  inputs_real / the result use the REAL node
-    numbering of the shortened code (slot z*(k+m) + node; output z*|E| + j)."""
-    import numpy as np
+    """Oracle of a shortened Clay code: oracle.shortened_clay_perform_coding (the
+    reference Clay(k+v, m) with the virtual data nodes zero-filled)."""
     import oracle as O
-    n_r, n_u = k + m, k + v + m
-    und = lambda r: r if r < k else r + v  # noqa: E731
-    c = O.Clay(k + v, m, [und(e) for e in erased_real])
-    a = c.alpha
-    inputs = [None] * (n_u * a)
-    for z in range(a):
-        for r in range(n_r):
-            inputs[z * n_u + und(r)] = inputs_real[z * n_r + r]
-        for u in range(k, k + v):
-            inputs[z * n_u + u] = np.zeros(B, np.uint8)
-    outs = [np.zeros(B, np.uint8) for _ in range(len(erased_real) * a)]
-    c.perform_coding(inputs, outs, B)
-    return outs
+    return O.shortened_clay_perform_coding(k, m, v, erased_real, inputs_real, B)
 
 
 def gf_apply_numpy(matrix, inputs):

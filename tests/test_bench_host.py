@@ -85,3 +85,56 @@ def test_self_launch_propagates_a_failing_rank():
                    {"ECX_BENCH_BACKEND": "gloo", "MASTER_ADDR": "127.0.0.1"})
     assert r.returncode != 0
     assert '"n_gpus"' not in r.stdout
+
+
+def _bare(cls, **attrs):
+    """A workload object with only the attributes its oracle hooks read (no GPU pool)."""
+    wl = object.__new__(cls)
+    for k, v in attrs.items():
+        setattr(wl, k, v)
+    return wl
+
+
+@pytest.mark.parametrize("case", ["clay42", "clay42x2", "clay104", "rs124", "lrc"])
+def test_cpu_baseline_every_workload(case):
+    """Every bench workload has an oracle baseline (the reference path
+    restated by oracle/, timed by oracle/orc_bench.c orc_bench_run), here on a bounded
+    arena: the line's fields are filled and the rate is positive."""
+    if case == "clay42":
+        wl = _bare(bench.Clay42, erased=1)
+    elif case == "clay42x2":
+        wl = _bare(bench.Clay42x2, erased=0, unit_bytes=48 * bench.B)
+    elif case == "clay104":
+        wl = _bare(bench.Clay104, erased=3, n=14, unit_bytes=1088 * 4096)
+    elif case == "rs124":
+        wl = _bare(bench.RS124)
+    else:
+        wl = _bare(bench.LRC)
+    cpu = bench.cpu_baseline(wl, 0.2, None, max_units=2)
+    assert cpu["kind"] == "port" and cpu["unit"] == "GiB/s" and cpu["cores"] >= 1
+    assert cpu["value"] > 0 and cpu["single_thread_value"] > 0
+    assert cpu["oracle_check"] is None and "oracle/" in cpu["sample"]
+
+
+def test_oracle_checks_of_the_workloads():
+    """The sampled byte-compare of each workload agrees with an oracle-made unit and
+    rejects a corrupted output byte (rs124 / lrc / clay104 on small host stand-ins)."""
+    import numpy as np
+    import oracle as O
+    rng = np.random.default_rng(1)
+    # LRC: group [d0 d1 d2 p] with p = d0 ^ d1 ^ d2; repair of block 2
+    lrc = _bare(bench.LRC, b=256)
+    st = rng.integers(0, 256, (16, 256), dtype=np.uint8)
+    st[3] = st[0] ^ st[1] ^ st[2]
+    assert lrc.oracle_check(st, st[2:3].copy())
+    bad = st[2:3].copy()
+    bad[0, 7] ^= 1
+    assert not lrc.oracle_check(st, bad)
+    # RS(12,4) decode of {0, 1}
+    rs = _bare(bench.RS124, L=512)
+    shards = [rng.integers(0, 256, 512, dtype=np.uint8) for _ in range(12)] + [np.zeros(512, np.uint8)] * 4
+    shards = [s.copy() for s in shards]
+    O.ReedSolomon(12, 4).encode_parity(shards, 0, 512)
+    stripe = np.stack(shards)
+    assert rs.oracle_check(stripe, stripe[0:2].copy())
+    assert not rs.oracle_check(stripe, stripe[1:3].copy())

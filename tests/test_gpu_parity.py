@@ -1634,3 +1634,47 @@ def test_map_planes_every_clay42_erasure_pattern(ecx, torch_dev):
             assert all((got[0][S - 1, j] == ref[j]).all() for j in range(len(ref))), erased
     finally:
         ecx.tune("map_planes", 1)
+
+
+@pytest.mark.parametrize("pitch", [(4 << 20), (1 << 20) + 4096])
+def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
+    """skew_trial: the first large RS(12,4) decode batch at a new shard pitch times the
+    skewed and the one-chunk launch on its own stripes and keeps the faster for (map,
+    pitch mod 16 MiB); the in-place results equal the static rule's and the oracle's, a
+    second batch reuses the choice, and accumulate mode never runs the trial."""
+    torch = torch_dev
+    L = 1 << 20
+    S = max(2, (96 << 20) // (12 * L))
+    rs = ecx.ReedSolomon.create(12, 4)
+    present = [False, False] + [True] * 14
+    pool = torch.empty((S, 16, pitch), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 88)
+    rs.encode_map().apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+    orig = pool[:, 0:2, :L].clone()
+    outs = {}
+    for trial in (0, 1):
+        dmap = ecx.ReedSolomon.create(12, 4).decode_map(present)  # a fresh map: nothing measured yet
+        try:
+            ecx.tune("skew_trial", trial)
+            assert dmap.skew_choice(pitch) == -1
+            pool[:, 0:2, :L] = 0
+            dmap.apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+            torch.cuda.synchronize()
+            outs[trial] = (pool[:, 0:2, :L].clone(), ecx.last_kernel(), dmap.skew_choice(pitch))
+        finally:
+            ecx.tune("skew_trial", 1)
+    assert outs[0][2] == -1 and outs[1][2] in (0, 1)
+    assert outs[1][1].startswith("k_gf_apply_skew") == (outs[1][2] == 1), outs[1][1:]
+    assert bool(torch.equal(outs[0][0], orig)) and bool(torch.equal(outs[1][0], orig))
+    # the oracle on one stripe
+    host = pool[S - 1].cpu().numpy()
+    shards = [np.zeros(L, np.uint8) if i < 2 else host[i, :L].copy() for i in range(16)]
+    O.ReedSolomon(12, 4).decode_missing(shards, [i >= 2 for i in range(16)], 0, L)
+    assert (shards[0] == orig[S - 1, 0].cpu().numpy()).all() and (shards[1] == orig[S - 1, 1].cpu().numpy()).all()
+    # accumulate mode: no trial (it would accumulate twice)
+    acc_map = ecx.ReedSolomon.create(12, 4).decode_map(present)
+    acc = torch.zeros((S, 2, pitch), dtype=torch.uint8, device="cuda")
+    acc_map.accumulate_batch(pool, 16 * pitch, pitch, acc, 2 * pitch, pitch, S, L)
+    torch.cuda.synchronize()
+    assert acc_map.skew_choice(pitch) == -1
+    assert bool(torch.equal(acc[:, :, :L], orig))
