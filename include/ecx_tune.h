@@ -40,8 +40,8 @@
  *                      rotates the chunk each input is read at; 1 = auto (default): chosen per map
  *                      and input slot pitch (mod 16 MiB) by "skew_trial", else 4 when the pitch is
  *                      a multiple of 4 MiB and one chunk per workgroup otherwise; 0 = never
- *   "skew_trial"       1 = on the first large batch (>= 64 MiB of input) of a map at a new slot
- *                      pitch, time the skewed and the one-chunk launch on a sample of its own stripes
+ *   "skew_trial"       1 = on the first large batch (>= 512 MiB of input) of a map at a new slot
+ *                      pitch, time the skewed and the one-chunk launch on up to 2 GiB of its own stripes
  *                      (3 rounds each, on the caller's stream; overwrite mode, no capture, outputs
  *                      not aliasing inputs) and keep the faster for that (map, pitch mod 16 MiB)
  *                      (default); 0 = the static 4 MiB rule only

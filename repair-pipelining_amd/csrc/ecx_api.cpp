@@ -10,6 +10,7 @@
 #include <unordered_map>
 #include <mutex>
 #include <string>
+#include <tuple>
 
 #include "clay_rtc.hpp"
 #include "map_rtc.hpp"
@@ -25,6 +26,7 @@ struct ecx_map {
 struct ecx_rs {
     explicit ecx_rs(int k, int m) : code(k, m) {}
     RsCode code;
+    bool shared = false;  // owned by the process-wide codec registry (ecx_rs_create)
     std::mutex mu;
     std::unique_ptr<ecx_map> enc, check;
     std::map<std::string, std::unique_ptr<ecx_map>> dec, partial;  // plans live as long as the codec
@@ -33,6 +35,7 @@ struct ecx_rs {
 struct ecx_clay {
     ecx_clay(int k, int m, std::vector<int> e, int v = 0) : pl(k, m, std::move(e), v) {}
     ClayPlanner pl;
+    bool shared = false;  // owned by the process-wide codec registry (ecx_clay_create)
     std::mutex mu;
     std::map<std::string, std::unique_ptr<ecx_map>> maps;
     // Single-node repair as the per-helper-plane kernel (clay_rtc.hpp), built on first use.
@@ -202,6 +205,22 @@ ecx_map *clay_standard_map(ecx_clay *c) {
 
 }  // namespace
 
+namespace {
+constexpr size_t kCodecRegistryMax = 4096;
+template <typename T, typename Key, typename Make>
+T *registry_get(const Key &key, Make make) {
+    static std::mutex mu;
+    static std::map<Key, std::unique_ptr<T>> reg;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = reg.find(key);
+    if (it != reg.end()) return it->second.get();
+    std::unique_ptr<T> obj(make());  // may throw (invalid geometry): nothing registered
+    if (reg.size() >= kCodecRegistryMax) return obj.release();
+    obj->shared = true;
+    return reg.emplace(key, std::move(obj)).first->second.get();
+}
+}  // namespace
+
 extern "C" {
 
 const char *ecx_status_string(int s) {
@@ -347,15 +366,25 @@ int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *i
 }
 
 // ---------------------------------------------------------------- ReedSolomon
+// Codec objects are immutable after creation apart from their lock-protected plan caches,
+// so equal codecs are one object: the reference builds a ReedSolomon (or a Clay decoding
+// step) per file or repair (SampleEncoder.java:83, ClayCode.java:43-51), and sharing keeps
+// the compiled, device-resident plans -- and the hiprtc-compiled Clay kernels -- of every
+// earlier call instead of rebuilding them per object.  The registry holds up to
+// kCodecRegistryMax codecs for the process lifetime; past that, creates return private
+// objects that ecx_*_destroy frees.
 int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out) {
     return guarded(__func__, [&]() -> int {
         *out = nullptr;
-        *out = new ecx_rs(data_shards, parity_shards);
+        *out = registry_get<ecx_rs>(std::make_pair(data_shards, parity_shards),
+                                    [&] { return new ecx_rs(data_shards, parity_shards); });
         return ECX_OK;
     });
 }
 
-void ecx_rs_destroy(ecx_rs *rs) { delete rs; }
+void ecx_rs_destroy(ecx_rs *rs) {
+    if (rs && !rs->shared) delete rs;
+}
 
 int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out) {
     const Matrix &m = rs->code.matrix();
@@ -670,12 +699,7 @@ int ecx_rs_encode_partial_batch(ecx_rs *rs, int input_index, const uint8_t *in, 
 
 // ---------------------------------------------------------------- Clay
 int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_erased, ecx_clay **out) {
-    return guarded(__func__, [&]() -> int {
-        *out = nullptr;
-        if (n_erased < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased");
-        *out = new ecx_clay(data_units, parity_units, std::vector<int>(erased, erased + n_erased));
-        return ECX_OK;
-    });
+    return ecx_clay_create_shortened(data_units, parity_units, 0, erased, n_erased, out);
 }
 
 int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
@@ -683,12 +707,16 @@ int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_unit
     return guarded(__func__, [&]() -> int {
         *out = nullptr;
         if (n_erased < 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased / virtual_units");
-        *out = new ecx_clay(data_units, parity_units, std::vector<int>(erased, erased + n_erased), virtual_units);
+        const std::vector<int> e(erased, erased + n_erased);  // order matters (the reference's erasedIndexes)
+        *out = registry_get<ecx_clay>(std::make_tuple(data_units, parity_units, virtual_units, e),
+                                      [&] { return new ecx_clay(data_units, parity_units, e, virtual_units); });
         return ECX_OK;
     });
 }
 
-void ecx_clay_destroy(ecx_clay *clay) { delete clay; }
+void ecx_clay_destroy(ecx_clay *clay) {
+    if (clay && !clay->shared) delete clay;
+}
 
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha) {
     if (q) *q = clay->pl.q();

@@ -487,11 +487,15 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 
 // The slot pitch decides whether rotating the chunk order pays (k_gf_apply_skew), and no
 // simple rule predicts it beyond "4 MiB multiples gain" (pitch sweep).  So on
-// the first large batch of a map at a new pitch (mod 16 MiB), both launches run on a
-// sample of the batch's own stripes, three rounds each on the caller's stream, and the
+// the first large batch (>= 512 MiB of input) of a map at a new pitch (mod 16 MiB), both
+// launches run on a sample of up to 2 GiB of the batch's own stripes, three rounds each on
+// the caller's stream, and the
 // faster is kept for that (map, pitch).  The trial writes the same outputs the real launch
 // then rewrites, so it is only done where that is harmless: overwrite mode, outputs not
 // aliasing inputs, no stream capture.
+constexpr int64_t kSkewTrialMinBytes = (int64_t)512 << 20;     // batches this large (input bytes) run the trial
+constexpr int64_t kSkewTrialSampleBytes = (int64_t)2 << 30;    // input bytes per trial launch
+
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate) {
@@ -503,7 +507,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     bool trial = tu.skew_chunks == 1 && tu.skew_trial && tu.block_threads == 0 && !accumulate && !tu.lds_lut &&
                  tu.bitslice != 2 && tu.nontemporal != 0 && tu.store_scope == 0 && cm.n_tiles() == 1 &&
                  m.n_in >= 4 && m.n_out > 0 && aligned && in_slot_stride > 0 && nbytes >= 4 * kChunkBytes &&
-                 nstripes * in_bytes >= ((int64_t)64 << 20);
+                 nstripes * in_bytes >= kSkewTrialMinBytes;
     const int64_t key = trial ? in_slot_stride % ((int64_t)16 << 20) : 0;
     int pick = trial ? cm.skew_choice(key) : -1;
     if (trial && pick < 0) {
@@ -523,7 +527,10 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             cap = hipStreamCaptureStatusActive;  // unknown: do not run the trial
         }
         if ((disjoint || same_layout_ok) && cap == hipStreamCaptureStatusNone) {
-            const int64_t sample = std::min<int64_t>(nstripes, std::max<int64_t>(1, ((int64_t)256 << 20) / in_bytes));
+            // a sample big enough to behave like the batch (a few stripes time the launch
+            // tail, not the access pattern: a 5-stripe trial picked the slower kernel for
+            // RS(12,4) at the padded pitch)
+            const int64_t sample = std::min<int64_t>(nstripes, std::max<int64_t>(1, kSkewTrialSampleBytes / in_bytes));
             hipEvent_t ev[7];
             for (auto &e : ev) check_hip(hipEventCreate(&e), "hipEventCreate");
             float best[2] = {1e30f, 1e30f};

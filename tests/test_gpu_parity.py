@@ -1644,7 +1644,7 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
     second batch reuses the choice, and accumulate mode never runs the trial."""
     torch = torch_dev
     L = 1 << 20
-    S = max(2, (96 << 20) // (12 * L))
+    S = (640 << 20) // (12 * L)  # >= 512 MiB of input: the trial runs
     rs = ecx.ReedSolomon.create(12, 4)
     present = [False, False] + [True] * 14
     pool = torch.empty((S, 16, pitch), dtype=torch.uint8, device="cuda")
@@ -1652,8 +1652,11 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
     rs.encode_map().apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
     orig = pool[:, 0:2, :L].clone()
     outs = {}
+    mat, ins_, outs_ = rs.decode_map(present).matrix()
+    fresh = lambda: ecx.GfMap.from_matrix(mat, in_slot=[int(i) for i in ins_],  # noqa: E731
+                                          out_slot=[int(o) for o in outs_])    # nothing measured yet
     for trial in (0, 1):
-        dmap = ecx.ReedSolomon.create(12, 4).decode_map(present)  # a fresh map: nothing measured yet
+        dmap = fresh()
         try:
             ecx.tune("skew_trial", trial)
             assert dmap.skew_choice(pitch) == -1
@@ -1672,7 +1675,7 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
     O.ReedSolomon(12, 4).decode_missing(shards, [i >= 2 for i in range(16)], 0, L)
     assert (shards[0] == orig[S - 1, 0].cpu().numpy()).all() and (shards[1] == orig[S - 1, 1].cpu().numpy()).all()
     # accumulate mode: no trial (it would accumulate twice)
-    acc_map = ecx.ReedSolomon.create(12, 4).decode_map(present)
+    acc_map = fresh()
     acc = torch.zeros((S, 2, pitch), dtype=torch.uint8, device="cuda")
     acc_map.accumulate_batch(pool, 16 * pitch, pitch, acc, 2 * pitch, pitch, S, L)
     torch.cuda.synchronize()
