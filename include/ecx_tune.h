@@ -72,6 +72,11 @@
  *                      every load issued at the start, bit 4 = DIAGNOSTIC data-movement-only build
  *                      (coefficients taken as 1, no transposes: the outputs are not the repair;
  *                      refused with ECX_E_ILLEGAL_ARGUMENT unless the environment has ECX_DIAGNOSTIC=1)
+ *   "rtc_diag"         the plane-group kernel's DIAGNOSTIC builds, 0 = none (default); bits remove one
+ *                      part each to price it (1 row-yc partner loads, 2 LDS exchange + barrier, 4
+ *                      lane-row exchange, 8 output stores but one, 16 bit-plane transposes): the
+ *                      outputs are not the repair, so any non-zero value is refused with
+ *                      ECX_E_ILLEGAL_ARGUMENT unless the environment has ECX_DIAGNOSTIC=1
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes

@@ -33,6 +33,12 @@ struct RtcShape {
     int xcd_local = 0;  // 1: the helper planes of one (stripe, chunk) run on one XCD (shared L2)
     int group = 0;      // 1: the plane-group kernel (k_clay_repair_grp) where the program allows it
     int persist = 0;    // plane-group kernel: > 0 = a persistent grid of this many workgroups per CU
+    // plane-group kernel, DIAGNOSTIC builds (ecx_tune "rtc_diag", needs ECX_DIAGNOSTIC=1; the
+    // outputs are not the repair): each bit removes one part of the kernel, to price it --
+    // 1 the row-yc partner loads (the partner is the node's own sub-chunk), 2 the LDS exchange
+    // and its barrier (row yb partners = own values), 4 the lane-row exchange (row ya partners
+    // = own values), 8 the output stores but one, 16 the bit-plane transposes
+    int diag = 0;
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

@@ -1094,6 +1094,11 @@ int ecx_tune(const char *key, int value) {
         t.rtc_xcd = value;
     }
     else if (k == "rtc_group") t.rtc_group = value != 0;
+    else if (k == "rtc_diag") {
+        if (value < 0 || value > 31) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value && !diagnostic_builds_allowed()) return ECX_E_ILLEGAL_ARGUMENT;  // outputs not the repair
+        t.rtc_diag = value;
+    }
     else if (k == "rtc_persist") {
         if (value < 0 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_persist = value;

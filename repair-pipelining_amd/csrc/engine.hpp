@@ -250,6 +250,7 @@ struct Tuning {
     int rtc_group = 1;      // 1: the plane-group kernel (k_clay_repair_grp) where the program allows it
                             // (+4-8 % over one plane per workgroup on Clay(10,4), profiles/r02_grp_sweep.jsonl)
     int rtc_persist = 0;    // its persistent grid: workgroups per CU (0 = one workgroup per unit)
+    int rtc_diag = 0;       // its DIAGNOSTIC builds (clay_rtc.hpp RtcShape::diag; ECX_DIAGNOSTIC=1 only)
     int rtc_xcd = 2;        // its block order: 1 = the helper planes of a (stripe, chunk) on one XCD;
                             // 2 (plane-group kernel): whole (stripe, chunk) units per XCD, +4.5 %
                             // (+1.1 % on Clay(10,4), profiles/r02_rtc_sweep.jsonl)
