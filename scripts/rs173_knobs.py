@@ -19,6 +19,11 @@ import rpamd  # noqa: E402
 K, M, SHARD = 17, 3, 200 * 1000
 KNOBS = [{}, {"depth": 4}, {"depth": 12}, {"depth": 16}, {"depth": 20}, {"block_threads": 64}, {"small_tiles": 1},
          {"small_tiles": 1, "depth": 12}, {"skew_chunks": 2}, {"skew_chunks": 4}, {"nontemporal": 0}]
+KNOBS_XCD = [{}, {"block_threads": 64}, {"xcd_group": 3, "xcd_run": 8}, {"xcd_group": 3, "xcd_run": 49},
+             {"xcd_group": 3, "xcd_run": 196}, {"block_threads": 64, "xcd_group": 3, "xcd_run": 8},
+             {"block_threads": 64, "xcd_group": 3, "xcd_run": 196}, {"chunk_major": 1}]
+DEFAULTS = {"depth": 0, "block_threads": 0, "small_tiles": 2, "skew_chunks": 1, "nontemporal": 1, "xcd_group": 0,
+            "xcd_run": 8, "chunk_major": 0}
 
 
 def main():
@@ -27,7 +32,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--pad", type=int, default=0, help="bytes between shards")
+    ap.add_argument("--set", default="knobs", choices=["knobs", "xcd", "default"])
     args = ap.parse_args()
+    knobs = {"knobs": KNOBS, "xcd": KNOBS_XCD, "default": [{}]}[args.set]
     import torch
     ecx = rpamd.load()
     p = SHARD + args.pad
@@ -37,7 +44,7 @@ def main():
     rs = ecx.ReedSolomon.create(K, M)
     res, kern, ref = {}, {}, None
     for _ in range(args.rounds):
-        for i, kn in enumerate(KNOBS):
+        for i, kn in enumerate(knobs):
             for k, v in kn.items():
                 ecx.tune(k, v)
             try:
@@ -57,10 +64,9 @@ def main():
                 torch.cuda.synchronize()
             finally:
                 for k in kn:
-                    ecx.tune(k, {"depth": 0, "block_threads": 0, "small_tiles": 2, "skew_chunks": 1,
-                                 "nontemporal": 1}[k])
+                    ecx.tune(k, DEFAULTS[k])
             res.setdefault(i, []).append((K + M) * SHARD * S / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
-    for i, kn in enumerate(KNOBS):
+    for i, kn in enumerate(knobs):
         med = statistics.median(res[i])
         print(json.dumps({"knobs": kn, "pad": args.pad, "GBps": round(med, 1), "frac": round(med / 8000, 4),
                           "kernel": kern[i]}), flush=True)
