@@ -82,6 +82,9 @@
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes
  *                      per workgroup, partners exchanged in registers and LDS; default), 0 = one
  *                      helper plane per workgroup
+ *   "rtc_units"        the plane-group kernel's 512-B slices per workgroup: 1 (default), or 2 with the
+ *                      second slice's first two rows loaded while the first slice finishes (software
+ *                      pipelining across the exchange barrier; no persistent grid)
  *   "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
  *                      a persistent grid of that many workgroups per CU walking the units
  *   "rtc_xcd"          that kernel's block order: 1 = the helper planes of one (stripe, chunk) on one

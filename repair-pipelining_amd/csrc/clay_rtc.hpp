@@ -39,6 +39,9 @@ struct RtcShape {
     // and its barrier (row yb partners = own values), 4 the lane-row exchange (row ya partners
     // = own values), 8 the output stores but one, 16 the bit-plane transposes
     int diag = 0;
+    // plane-group kernel: 512-B slices per workgroup, 1 or 2 (software-pipelined: the second
+    // slice's rows yb and ya are loaded while the first finishes; ecx_tune "rtc_units")
+    int units = 1;
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

@@ -1099,6 +1099,10 @@ int ecx_tune(const char *key, int value) {
         if (value && !diagnostic_builds_allowed()) return ECX_E_ILLEGAL_ARGUMENT;  // outputs not the repair
         t.rtc_diag = value;
     }
+    else if (k == "rtc_units") {
+        if (value < 1 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_units = value;
+    }
     else if (k == "rtc_persist") {
         if (value < 0 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_persist = value;

@@ -6,7 +6,7 @@ one, 16 the bit-plane transposes -- and are timed against the real kernel in int
 rounds on BASELINE config 4 (2,048 resident stripes, 1 MiB node blocks, repair of node 3).
 Median launch time -> algorithmic GB/s of the REAL repair's bytes, fraction of 8 TB/s.
 
-    python scripts/clay104_diag.py [--rounds 3 --reps 10]
+    python scripts/clay104_diag.py [--rounds 3 --reps 10] [--shapes]
 """
 import argparse
 import json
@@ -21,6 +21,10 @@ sys.path.insert(0, str(ROOT))
 import rpamd  # noqa: E402
 
 VARIANTS = [0, 1, 2, 4, 8, 16, 1 | 2, 1 | 2 | 4, 1 | 2 | 4 | 8, 31]
+# --shapes: real (non-diagnostic) code shapes of the same kernel, as tune dicts
+SHAPES = [{}, {"rtc_units": 2}, {"rtc_units": 2, "rtc_waves": 2}, {"rtc_waves": 2},
+          {"rtc_units": 2, "rtc_xcd": 3}, {"rtc_units": 2, "rtc_waves": 2, "rtc_xcd": 3}]
+DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0}
 
 
 def main():
@@ -29,6 +33,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=None, help="comma-separated rtc_diag values")
+    ap.add_argument("--shapes", action="store_true", help="time the SHAPES code shapes instead (all bit-exact)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     args = ap.parse_args()
     import torch
@@ -36,7 +41,10 @@ def main():
     for kv in args.tune:
         k_, _, v_ = kv.partition("=")
         ecx.tune(k_, int(v_))
-    variants = [int(v) for v in args.variants.split(",")] if args.variants else VARIANTS
+    if args.shapes:
+        variants = [dict(sh) for sh in SHAPES]
+    else:
+        variants = [{"rtc_diag": int(v)} for v in (args.variants.split(",") if args.variants else VARIANTS)]
     k, m, v, b, a = 10, 4, 2, 4096, 256
     n, P = k + m, args.pool
     pool = torch.empty((P, n * a, b), dtype=torch.uint8, device="cuda")
@@ -45,21 +53,22 @@ def main():
     info = step.map().info()
     unit = (info["n_in"] + info["n_out"]) * b
     out = torch.empty((P, a, b), dtype=torch.uint8, device="cuda")
-    times = {d: [] for d in variants}
+    times = {i: [] for i in range(len(variants))}
     ref = None
     try:
         for _ in range(args.rounds):
-            for d in variants:
-                ecx.tune("rtc_diag", d)
+            for i, d in enumerate(variants):
+                for k_, v_ in DEFAULTS.items():
+                    ecx.tune(k_, d.get(k_, v_))
                 step.performCodingBatch(pool, n * a * b, b, out, a * b, b, P, b)
                 torch.cuda.synchronize()
                 if ecx.last_kernel() != "k_clay_repair_grp":
                     raise SystemExit("ran %s" % ecx.last_kernel())
-                if d == 0:
+                if not d.get("rtc_diag"):  # every real shape must give the same repair
                     if ref is None:
                         ref = out.clone()
                     elif not torch.equal(out, ref):
-                        raise SystemExit("the real kernel's output changed between rounds")
+                        raise SystemExit("shape %s: output differs" % d)
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                        for _ in range(args.reps)]
                 for e0, e1 in evs:
@@ -67,13 +76,14 @@ def main():
                     step.performCodingBatch(pool, n * a * b, b, out, a * b, b, P, b)
                     e1.record()
                 torch.cuda.synchronize()
-                times[d].extend(e0.elapsed_time(e1) for e0, e1 in evs)
+                times[i].extend(e0.elapsed_time(e1) for e0, e1 in evs)
     finally:
-        ecx.tune("rtc_diag", 0)
-    for d in variants:
-        ms = statistics.median(times[d])
+        for k_, v_ in DEFAULTS.items():
+            ecx.tune(k_, v_)
+    for i, d in enumerate(variants):
+        ms = statistics.median(times[i])
         gbs = P * unit / (ms * 1e-3) / 1e9
-        print(json.dumps({"rtc_diag": d, "tune": args.tune, "launch_ms": round(ms, 4), "GBps": round(gbs, 1),
+        print(json.dumps({"variant": d, "tune": args.tune, "launch_ms": round(ms, 4), "GBps": round(gbs, 1),
                           "frac": round(gbs / 8000.0, 4)}), flush=True)
 
 

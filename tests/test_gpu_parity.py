@@ -1681,3 +1681,37 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
     torch.cuda.synchronize()
     assert acc_map.skew_choice(pitch) == -1
     assert bool(torch.equal(acc[:, :, :L], orig))
+
+
+@pytest.mark.parametrize("e,B,S", [(3, 4096, 5), (13, 8192 + 16, 3), (0, 4096, 17)])
+def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
+    """rtc_units 2: the plane-group kernel taking two 512-B slices per workgroup, the
+    second slice's rows loaded while the first finishes, in every block order and at 2
+    and 3 waves per SIMD, equals the one-slice kernel and the zero-filled Clay(12,4)
+    oracle (ClayCodeErasureDecodingStep.java:171-203) on a shortened Clay(10,4) repair."""
+    torch = torch_dev
+    k, m, v = 10, 4, 2
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    n, a = k + m, step.subPacketSize
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 300 + e)
+    outs = []
+    try:
+        for units, xcd, waves in [(1, 2, 3), (2, 2, 3), (2, 1, 3), (2, 3, 2), (2, 4, 3), (2, 0, 2)]:
+            ecx.tune("rtc_units", units)
+            ecx.tune("rtc_xcd", xcd)
+            ecx.tune("rtc_waves", waves)
+            o = torch.full((S, a, B), 0x6B, dtype=torch.uint8, device="cuda")
+            step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
+            torch.cuda.synchronize()
+            assert ecx.last_kernel() == "k_clay_repair_grp"
+            outs.append(o.cpu().numpy())
+    finally:
+        ecx.tune("rtc_units", 1)
+        ecx.tune("rtc_xcd", 2)
+        ecx.tune("rtc_waves", 3)
+    assert all((x == outs[0]).all() for x in outs[1:])
+    host = pool[S - 1].cpu().numpy()
+    inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
+    ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
+    assert all((outs[1][S - 1, z] == ref[z]).all() for z in range(a))
