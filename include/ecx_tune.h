@@ -40,11 +40,13 @@
  *                      rotates the chunk each input is read at; 1 = auto (default): chosen per map
  *                      and input slot pitch (mod 16 MiB) by "skew_trial", else 4 when the pitch is
  *                      a multiple of 4 MiB and one chunk per workgroup otherwise; 0 = never
- *   "skew_trial"       1 = on the first large batch (>= 512 MiB of input) of a map at a new slot
- *                      pitch, time the skewed and the one-chunk launch on up to 2 GiB of its own stripes
- *                      (3 rounds each, on the caller's stream; overwrite mode, no capture, outputs
- *                      not aliasing inputs) and keep the faster for that (map, pitch mod 16 MiB)
- *                      (default); 0 = the static 4 MiB rule only
+ *   "skew_trial"       single-tile maps with "skew_chunks" and "block_threads" on auto: 1 = on the first
+ *                      large batch (>= 512 MiB of input) of a map at a new slot pitch, time three launch
+ *                      shapes -- 256-thread workgroups over 4 KiB chunks, skewed chunks, one-wave
+ *                      workgroups over 1 KiB chunks -- on up to 2 GiB of its own stripes (3 rounds each,
+ *                      on the caller's stream; overwrite mode, no capture, outputs not aliasing inputs)
+ *                      and keep the fastest for that (map, pitch mod 16 MiB) (default); 0 = the static
+ *                      rules only (skew on 4 MiB-multiple pitches, one wave for <= 2-row maps)
  *   "wide_tiles"       multi-tile maps: pairs of 8-row tiles that share inputs in one workgroup
  *                      (16 accumulator rows, each shared input loaded once).  1 = when pairing
  *                      saves >= 1/6 of the input reads (default), 2 = always, 0 = never
@@ -135,8 +137,9 @@ int ecx_map_selftest(const struct ecx_map *map, uint64_t seed);
 /* Plan shape: row tiles, tile entries (= input loads of the one-workgroup-per-tile
  * kernel), tile groups, and the summed group unions (= input loads of the LDS kernel). */
 int ecx_map_plan_stats(const struct ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total);
-/* The skewed-chunk choice "skew_trial" measured for `map` at input slot pitch
- * `slot_pitch`: 1 = skewed, 0 = one chunk per workgroup, -1 = not measured (yet). */
+/* The launch shape "skew_trial" measured for `map` at input slot pitch `slot_pitch`:
+ * 0 = 256-thread workgroups over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups
+ * over 1 KiB chunks, -1 = not measured (yet). */
 int ecx_map_skew_choice(const struct ecx_map *map, int64_t slot_pitch);
 /* The kernel instance of the last full-chunk launch this thread enqueued, named as
  * rocprofv3 names it (e.g. "k_gf_apply<false, true, 1, 20, false, 256, 8>"), copied

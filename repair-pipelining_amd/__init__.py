@@ -434,9 +434,9 @@ class GfMap:
         return dict(zip(["tiles", "entries", "groups", "union_total"], [x.value for x in v]))
 
     def skew_choice(self, slot_pitch: int) -> int:
-        """The skewed-chunk choice measured for this map at an input slot pitch
-        (ecx_map_skew_choice, include/ecx_tune.h "skew_trial"): 1 skewed, 0 one chunk
-        per workgroup, -1 not measured."""
+        """The launch shape measured for this map at an input slot pitch
+        (ecx_map_skew_choice, include/ecx_tune.h "skew_trial"): 0 256-thread workgroups
+        over 4 KiB chunks, 1 skewed chunks, 2 one-wave workgroups, -1 not measured."""
         f = lib().ecx_map_skew_choice
         f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_int64], ctypes.c_int
         return f(self._h, int(slot_pitch))

@@ -142,8 +142,8 @@ public:
     MapPlanes *planes();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
-    // The measured skewed-chunk choice (skew_trial) for an input slot pitch key:
-    // -1 = not measured yet, 0 = one chunk per workgroup, 1 = skewed.
+    // The launch shape skew_trial measured for an input slot pitch key: -1 = not measured
+    // yet, 0 = 256-thread / 4 KiB workgroups, 1 = skewed chunks, 2 = one-wave / 1 KiB workgroups.
     int skew_choice(int64_t pitch_key);
     void set_skew_choice(int64_t pitch_key, int choice);
 

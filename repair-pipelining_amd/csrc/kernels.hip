@@ -237,10 +237,12 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
 }
 
 namespace {
-// skew_pick: -1 = the static rule (4 MiB-multiple input slot pitch), 0 / 1 = forced off / on
+// pick: -1 = the static rules (skew on 4 MiB-multiple input slot pitches, one-wave
+// workgroups for narrow maps otherwise); 0 = 256-thread workgroups over 4 KiB chunks,
+// 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB chunks (the shape trial's candidates)
 void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                        uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
-                       int64_t nbytes, hipStream_t stream, bool accumulate, int skew_pick) {
+                       int64_t nbytes, hipStream_t stream, bool accumulate, int pick) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
     const Tuning &tu = tuning();
     const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
@@ -252,11 +254,10 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     // (64) or, in auto (0), for single-tile maps of <= 2 rows over >= 8 inputs whose slot
     // pitch is not a 4 MiB multiple (RS(12,4) decode on its padded pitch: +2.4-2.8 %; every
     // other BASELINE map is 3-8 % slower on one wave, profiles/r02_block_threads.jsonl).
-    const bool skew_pitch = skew_pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4
-                                          : skew_pick == 1;
+    const bool skew_pitch = pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4 : pick == 1;
     const bool one_wave = tu.block_threads == 64 ||
-                          (tu.block_threads == 0 && cm.n_tiles() == 1 && cm.max_tile_rows() <= 2 &&
-                           cm.map().n_in >= 8 && !skew_pitch && tu.bitslice != 2 && !tu.lds_lut);
+                          (tu.block_threads == 0 && cm.n_tiles() == 1 && tu.bitslice != 2 && !tu.lds_lut &&
+                           (pick < 0 ? cm.max_tile_rows() <= 2 && cm.map().n_in >= 8 && !skew_pitch : pick == 2));
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     // Small-row kernel variants: forced (1), or auto (2) for maps of <= 2 rows over <= 4
@@ -485,14 +486,14 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 }
 }  // namespace
 
-// The slot pitch decides whether rotating the chunk order pays (k_gf_apply_skew), and no
-// simple rule predicts it beyond "4 MiB multiples gain" (pitch sweep).  So on
-// the first large batch (>= 512 MiB of input) of a map at a new pitch (mod 16 MiB), both
-// launches run on a sample of up to 2 GiB of the batch's own stripes, three rounds each on
-// the caller's stream, and the
-// faster is kept for that (map, pitch).  The trial writes the same outputs the real launch
-// then rewrites, so it is only done where that is harmless: overwrite mode, outputs not
-// aliasing inputs, no stream capture.
+// The slot pitch decides whether rotating the chunk order pays (k_gf_apply_skew) or one-wave
+// workgroups do, and no simple rule predicts it beyond "4 MiB multiples gain" (DESIGN.md 4,
+// pitch sweep; RS(17,3) on 200,000-B shards gains 7 % from one wave, profiles/r03_rs173_knobs.jsonl).
+// So on the first large batch (>= 512 MiB of input) of a single-tile map at a new pitch (mod
+// 16 MiB), the three launch shapes run on a sample of up to 2 GiB of the batch's own
+// stripes, three rounds each on the caller's stream, and the fastest is kept for that (map,
+// pitch).  The trial writes the same outputs the real launch then rewrites, so it is only
+// done where that is harmless: overwrite mode, outputs not aliasing inputs, no stream capture.
 constexpr int64_t kSkewTrialMinBytes = (int64_t)512 << 20;     // batches this large (input bytes) run the trial
 constexpr int64_t kSkewTrialSampleBytes = (int64_t)2 << 30;    // input bytes per trial launch
 
@@ -531,29 +532,32 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             // tail, not the access pattern: a 5-stripe trial picked the slower kernel for
             // RS(12,4) at the padded pitch)
             const int64_t sample = std::min<int64_t>(nstripes, std::max<int64_t>(1, kSkewTrialSampleBytes / in_bytes));
-            hipEvent_t ev[7];
+            constexpr int kCand = 3, kRounds = 3;  // 4 KiB workgroups, skewed chunks, one-wave workgroups
+            hipEvent_t ev[kCand * kRounds + 1];
             for (auto &e : ev) check_hip(hipEventCreate(&e), "hipEventCreate");
-            float best[2] = {1e30f, 1e30f};
+            float best[kCand] = {1e30f, 1e30f, 1e30f};
             try {
                 check_hip(hipEventRecord(ev[0], stream), "hipEventRecord");
-                for (int r = 0; r < 3; ++r)
-                    for (int v = 0; v < 2; ++v) {
+                for (int r = 0; r < kRounds; ++r)
+                    for (int v = 0; v < kCand; ++v) {
                         launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
                                           out_slot_stride, sample, nbytes, stream, false, v);
-                        check_hip(hipEventRecord(ev[1 + 2 * r + v], stream), "hipEventRecord");
+                        check_hip(hipEventRecord(ev[1 + kCand * r + v], stream), "hipEventRecord");
                     }
-                check_hip(hipEventSynchronize(ev[6]), "hipEventSynchronize");
-                for (int i = 1; i < 7; ++i) {
+                check_hip(hipEventSynchronize(ev[kCand * kRounds]), "hipEventSynchronize");
+                for (int i = 1; i <= kCand * kRounds; ++i) {
                     float ms = 0.f;
                     check_hip(hipEventElapsedTime(&ms, ev[i - 1], ev[i]), "hipEventElapsedTime");
-                    best[(i - 1) % 2] = std::min(best[(i - 1) % 2], ms);
+                    best[(i - 1) % kCand] = std::min(best[(i - 1) % kCand], ms);
                 }
             } catch (...) {
                 for (auto &e : ev) (void)hipEventDestroy(e);
                 throw;
             }
             for (auto &e : ev) (void)hipEventDestroy(e);
-            pick = best[1] < best[0] ? 1 : 0;
+            pick = 0;
+            for (int v = 1; v < kCand; ++v)
+                if (best[v] < best[pick]) pick = v;
             cm.set_skew_choice(key, pick);
         }
     }

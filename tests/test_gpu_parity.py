@@ -1638,10 +1638,10 @@ def test_map_planes_every_clay42_erasure_pattern(ecx, torch_dev):
 
 @pytest.mark.parametrize("pitch", [(4 << 20), (1 << 20) + 4096])
 def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
-    """skew_trial: the first large RS(12,4) decode batch at a new shard pitch times the
-    skewed and the one-chunk launch on its own stripes and keeps the faster for (map,
-    pitch mod 16 MiB); the in-place results equal the static rule's and the oracle's, a
-    second batch reuses the choice, and accumulate mode never runs the trial."""
+    """skew_trial: the first large RS(12,4) decode batch at a new shard pitch times three
+    launch shapes (4 KiB workgroups, skewed chunks, one-wave workgroups) on its own stripes
+    and keeps the fastest for (map, pitch mod 16 MiB); the in-place results equal the static
+    rule's and the oracle's, and accumulate mode never runs the trial."""
     torch = torch_dev
     L = 1 << 20
     S = (640 << 20) // (12 * L)  # >= 512 MiB of input: the trial runs
@@ -1666,8 +1666,9 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
             outs[trial] = (pool[:, 0:2, :L].clone(), ecx.last_kernel(), dmap.skew_choice(pitch))
         finally:
             ecx.tune("skew_trial", 1)
-    assert outs[0][2] == -1 and outs[1][2] in (0, 1)
+    assert outs[0][2] == -1 and outs[1][2] in (0, 1, 2)
     assert outs[1][1].startswith("k_gf_apply_skew") == (outs[1][2] == 1), outs[1][1:]
+    assert (", 64, " in outs[1][1]) == (outs[1][2] == 2), outs[1][1:]
     assert bool(torch.equal(outs[0][0], orig)) and bool(torch.equal(outs[1][0], orig))
     # the oracle on one stripe
     host = pool[S - 1].cpu().numpy()
