@@ -15,6 +15,9 @@
  *                      tiles of a unit back to back (default: see engine.hpp Tuning); 3 = (any
  *                      map) each XCD runs runs of "xcd_run" consecutive units
  *   "xcd_run"          xcd_group 3: consecutive (stripe, chunk) units per XCD run, 1..4096 (default 8)
+ *   "xcd_misaligned"   single-tile maps with "xcd_group" 0 whose input slots are not 128-B aligned
+ *                      (their chunks share boundary cache lines): 1 = use the runs of "xcd_group" 3
+ *                      (default), 0 = the identity block order
  *   "wave_groups"      multi-tile maps: one workgroup per group of tiles sharing inputs, one
  *                      wave per tile, 1 KiB chunks: 1 = the group's input union staged once
  *                      through LDS; 2 = each wave loads its own entries (no LDS, no barriers);
@@ -46,7 +49,9 @@
  *                      workgroups over 1 KiB chunks -- on up to 2 GiB of its own stripes (3 rounds each,
  *                      on the caller's stream; overwrite mode, no capture, outputs not aliasing inputs)
  *                      and keep the fastest for that (map, pitch mod 16 MiB) (default); 0 = the static
- *                      rules only (skew on 4 MiB-multiple pitches, one wave for <= 2-row maps)
+ *                      rules only (skew on 4 MiB-multiple pitches, one wave for <= 2-row maps).  The
+ *                      sample is four windows spread over the batch, and a shape replaces the static
+ *                      rules' choice only when it is >= 3 % faster
  *   "wide_tiles"       multi-tile maps: pairs of 8-row tiles that share inputs in one workgroup
  *                      (16 accumulator rows, each shared input loaded once).  1 = when pairing
  *                      saves >= 1/6 of the input reads (default), 2 = always, 0 = never

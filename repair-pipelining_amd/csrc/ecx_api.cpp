@@ -1031,6 +1031,10 @@ int ecx_tune(const char *key, int value) {
         if (value < 0 || value > 3) return ECX_E_ILLEGAL_ARGUMENT;
         t.xcd_group = value;
     }
+    else if (k == "xcd_misaligned") {
+        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        t.xcd_misaligned = value;
+    }
     else if (k == "xcd_run") {
         if (value < 1 || value > 4096) return ECX_E_ILLEGAL_ARGUMENT;
         t.xcd_run = value;

@@ -195,6 +195,7 @@ struct Tuning {
     int nontemporal = 1;      // 0 never, 1 auto (NT stores; NT loads for single-tile maps), 2 always
     int xcd_group = 0;        // multi-tile maps: tiles of a chunk on one XCD (measured slower: off)
     int xcd_run = 8;          // xcd_group 3 (any map): runs of this many consecutive units per XCD
+    int xcd_misaligned = 1;   // xcd_group 0: single-tile maps with inputs not 128-B aligned use the runs of 3
     // Multi-tile maps: 1 = k_gf_apply_lds (tile groups share inputs via LDS), 2 =
     // k_gf_apply_grp (tile groups in one workgroup, direct loads).  Off by
     // default: Clay(10,4)'s 64-row groups still need 1.23x the unique inputs and the

@@ -388,7 +388,14 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     a.out_slot_stride = out_slot_stride;
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
-    a.xcd_group = (a.n_tiles > 1 || tu.xcd_group == 3) ? tu.xcd_group : 0;
+    // Single-tile maps whose input slots are not 128-B aligned: consecutive chunks of a slot
+    // share a boundary cache line, fetched twice from HBM unless both chunks run on one XCD
+    // (one L2) -- runs of consecutive units per XCD (RS(17,3) on 200,000-B shards: reads
+    // 1.035x the algorithmic bytes, +5 % with the runs, profiles/r03_rs173_xcd_align.jsonl).
+    const bool misaligned128 = ((uintptr_t)in % 128) != 0 || in_stripe_stride % 128 != 0 || in_slot_stride % 128 != 0;
+    a.xcd_group = (a.n_tiles > 1 || tu.xcd_group == 3)
+                      ? tu.xcd_group
+                      : (tu.xcd_group == 0 && tu.xcd_misaligned && misaligned128 ? 3 : 0);
     a.xcd_run = tu.xcd_run;
     a.accumulate = accumulate ? 1 : 0;
 
@@ -495,7 +502,8 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 // pitch).  The trial writes the same outputs the real launch then rewrites, so it is only
 // done where that is harmless: overwrite mode, outputs not aliasing inputs, no stream capture.
 constexpr int64_t kSkewTrialMinBytes = (int64_t)512 << 20;     // batches this large (input bytes) run the trial
-constexpr int64_t kSkewTrialSampleBytes = (int64_t)2 << 30;    // input bytes per trial launch
+constexpr int64_t kSkewTrialSampleBytes = (int64_t)2 << 30;    // input bytes per trial shape and round
+constexpr float kTrialMargin = 0.97f;                          // a shape must be 3 % faster than the static rules' choice
 
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
@@ -528,10 +536,16 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             cap = hipStreamCaptureStatusActive;  // unknown: do not run the trial
         }
         if ((disjoint || same_layout_ok) && cap == hipStreamCaptureStatusNone) {
-            // a sample big enough to behave like the batch (a few stripes time the launch
+            // A sample big enough to behave like the batch (a few stripes time the launch
             // tail, not the access pattern: a 5-stripe trial picked the slower kernel for
-            // RS(12,4) at the padded pitch)
+            // RS(12,4) at the padded pitch), taken as kWindows windows spread over the batch's
+            // address span (a 2 GiB prefix misjudged the 1 MiB + 4 KiB pitch, where the shape
+            // that won on the prefix was 10 % slower on the whole batch).
+            constexpr int kWindows = 4;
             const int64_t sample = std::min<int64_t>(nstripes, std::max<int64_t>(1, kSkewTrialSampleBytes / in_bytes));
+            const int64_t win = std::max<int64_t>(1, sample / kWindows);
+            int64_t win_begin[kWindows];
+            for (int w = 0; w < kWindows; ++w) win_begin[w] = std::min(nstripes - win, (nstripes / kWindows) * w);
             constexpr int kCand = 3, kRounds = 3;  // 4 KiB workgroups, skewed chunks, one-wave workgroups
             hipEvent_t ev[kCand * kRounds + 1];
             for (auto &e : ev) check_hip(hipEventCreate(&e), "hipEventCreate");
@@ -540,8 +554,10 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                 check_hip(hipEventRecord(ev[0], stream), "hipEventRecord");
                 for (int r = 0; r < kRounds; ++r)
                     for (int v = 0; v < kCand; ++v) {
-                        launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
-                                          out_slot_stride, sample, nbytes, stream, false, v);
+                        for (int w = 0; w < kWindows; ++w)
+                            launch_apply_core(cm, in + win_begin[w] * in_stripe_stride, in_stripe_stride,
+                                              in_slot_stride, out + win_begin[w] * out_stripe_stride, out_stripe_stride,
+                                              out_slot_stride, win, nbytes, stream, false, v);
                         check_hip(hipEventRecord(ev[1 + kCand * r + v], stream), "hipEventRecord");
                     }
                 check_hip(hipEventSynchronize(ev[kCand * kRounds]), "hipEventSynchronize");
@@ -555,9 +571,13 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
                 throw;
             }
             for (auto &e : ev) (void)hipEventDestroy(e);
-            pick = 0;
-            for (int v = 1; v < kCand; ++v)
-                if (best[v] < best[pick]) pick = v;
+            // Run-to-run noise is a few %: another shape replaces the static rules' choice only
+            // if it beats it by kTrialMargin on the sample.
+            const bool skew_static = in_slot_stride % ((int64_t)4 << 20) == 0;
+            const int static_pick = skew_static ? 1 : (cm.max_tile_rows() <= 2 && m.n_in >= 8 ? 2 : 0);
+            pick = static_pick;
+            for (int v = 0; v < kCand; ++v)
+                if (best[v] < best[pick] && best[v] < kTrialMargin * best[static_pick]) pick = v;
             cm.set_skew_choice(key, pick);
         }
     }

@@ -24,7 +24,7 @@ fi
 if has gloo2; then
   # the multi-rank path without an external launcher, 2 ranks sharing the one GPU
   ECX_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --pool 4096 --steps 2 --warmup 1 \
-      --cpu-seconds 0 --no-probes > "$OUT/bench_gloo2.log" 2>&1
+      --cpu-seconds 4 --no-probes > "$OUT/bench_gloo2.log" 2>&1
   rc=$?; echo "bench gloo2 rc=$rc"; tail -2 "$OUT/bench_gloo2.log"; [ $rc -ne 0 ] && stop gloo2 $rc
 fi
 if has workloads; then
