@@ -227,9 +227,11 @@ struct Tuning {
     // workgroup, each entry's chunk rotated; 1 = 4 when the input slot pitch is a
     // multiple of 4 MiB; 0 = off.
     int skew_chunks = 1;
-    // skew_chunks auto: 1 = measure skewed vs one-chunk launches on the first large batch
-    // per (map, input slot pitch mod 16 MiB) and keep the faster; 0 = the static rule
-    int skew_trial = 1;
+    // skew_chunks / block_threads auto: 1 = measure the three launch shapes on the first large
+    // batch per (map, input slot pitch mod 16 MiB) and keep the fastest; 0 = the static rules
+    // (default: within 1.4 % of the best shape at every pitch measured, while the trial's
+    // sample misjudged the 1 MiB + 4 KiB pitch by 11 %, profiles/r03_shape_trial_check.jsonl)
+    int skew_trial = 0;
     // Per-call CodingLoop entry points: compiled plans kept, by map content (0 = none).
     int plan_cache = 256;
     // Bit-sliced kernel (k_gf_bits): 2 = for every map it can run (aligned layout, 32-bit

@@ -21,9 +21,10 @@ KNOBS = [{}, {"depth": 4}, {"depth": 12}, {"depth": 16}, {"depth": 20}, {"block_
          {"small_tiles": 1, "depth": 12}, {"skew_chunks": 2}, {"skew_chunks": 4}, {"nontemporal": 0}]
 KNOBS_XCD = [{}, {"block_threads": 64}, {"xcd_group": 3, "xcd_run": 8}, {"xcd_group": 3, "xcd_run": 49},
              {"xcd_group": 3, "xcd_run": 196}, {"block_threads": 64, "xcd_group": 3, "xcd_run": 8},
-             {"block_threads": 64, "xcd_group": 3, "xcd_run": 196}, {"chunk_major": 1}]
+             {"block_threads": 64, "xcd_group": 3, "xcd_run": 196}, {"chunk_major": 1}, {"xcd_misaligned": 0},
+             {"block_threads": 256}]
 DEFAULTS = {"depth": 0, "block_threads": 0, "small_tiles": 2, "skew_chunks": 1, "nontemporal": 1, "xcd_group": 0,
-            "xcd_run": 8, "chunk_major": 0}
+            "xcd_run": 8, "chunk_major": 0, "xcd_misaligned": 1}
 
 
 def main():

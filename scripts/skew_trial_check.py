@@ -1,9 +1,10 @@
 """skew_trial (include/ecx_tune.h) against the kernels it chooses between: RS(12,4)
 2-erasure decode in place at several shard pitches, each timed with the one-chunk
 launch in 256-thread and in one-wave workgroups (skew_chunks 0, block_threads 256 / 64),
-the skewed launch (skew_chunks 4), the static rules (skew_trial 0) and the default
-(skew_trial 1: measured on the first batch of a fresh map at that pitch).  Interleaved rounds, median algorithmic GB/s (12 read + 2 written
-shards); the default should match the faster of the first two at every pitch.
+the skewed launch (skew_chunks 4), the static rules (skew_trial 0, the default) and the
+trial (skew_trial 1: measured on the first batch of a fresh map at that pitch).
+Interleaved rounds, median algorithmic GB/s (12 read + 2 written shards) as a fraction of
+8 TB/s; a good rule matches the fastest of the first three at every pitch.
 
     python scripts/skew_trial_check.py [--rounds 3 --reps 3]
 """
@@ -35,8 +36,8 @@ def main():
     mat, ins, outs = ecx.ReedSolomon.create(12, 4).decode_map(present).matrix()
     res, picks = {}, {}
     variants = (("one_chunk_256", {"skew_chunks": 0, "block_threads": 256}), ("skewed", {"skew_chunks": 4}),
-                ("one_chunk_64", {"skew_chunks": 0, "block_threads": 64}), ("static_rule", {"skew_trial": 0}),
-                ("trial", {}))
+                ("one_chunk_64", {"skew_chunks": 0, "block_threads": 64}), ("static_rule", {}),
+                ("trial", {"skew_trial": 1}))
     for rnd in range(args.rounds):
         for L, pad in CASES:
             p = L + pad
@@ -58,7 +59,7 @@ def main():
                     kern = ecx.last_kernel()
                 finally:
                     ecx.tune("skew_chunks", 1)
-                    ecx.tune("skew_trial", 1)
+                    ecx.tune("skew_trial", 0)
                     ecx.tune("block_threads", 0)
                 res.setdefault((L, pad, name), []).append(14 * L * S / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
                 if name == "trial":

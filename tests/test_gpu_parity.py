@@ -1665,7 +1665,7 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
             torch.cuda.synchronize()
             outs[trial] = (pool[:, 0:2, :L].clone(), ecx.last_kernel(), dmap.skew_choice(pitch))
         finally:
-            ecx.tune("skew_trial", 1)
+            ecx.tune("skew_trial", 0)
     assert outs[0][2] == -1 and outs[1][2] in (0, 1, 2)
     assert outs[1][1].startswith("k_gf_apply_skew") == (outs[1][2] == 1), outs[1][1:]
     assert (", 64, " in outs[1][1]) == (outs[1][2] == 2), outs[1][1:]
@@ -1678,8 +1678,12 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
     # accumulate mode: no trial (it would accumulate twice)
     acc_map = fresh()
     acc = torch.zeros((S, 2, pitch), dtype=torch.uint8, device="cuda")
-    acc_map.accumulate_batch(pool, 16 * pitch, pitch, acc, 2 * pitch, pitch, S, L)
-    torch.cuda.synchronize()
+    try:
+        ecx.tune("skew_trial", 1)
+        acc_map.accumulate_batch(pool, 16 * pitch, pitch, acc, 2 * pitch, pitch, S, L)
+        torch.cuda.synchronize()
+    finally:
+        ecx.tune("skew_trial", 0)
     assert acc_map.skew_choice(pitch) == -1
     assert bool(torch.equal(acc[:, :, :L], orig))
 
