@@ -1103,6 +1103,10 @@ int ecx_tune(const char *key, int value) {
         if (value && !diagnostic_builds_allowed()) return ECX_E_ILLEGAL_ARGUMENT;  // outputs not the repair
         t.rtc_diag = value;
     }
+    else if (k == "rtc_sched") {
+        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_sched = value;
+    }
     else if (k == "rtc_units") {
         if (value < 1 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_units = value;

@@ -24,7 +24,10 @@ VARIANTS = [0, 1, 2, 4, 8, 16, 1 | 2, 1 | 2 | 4, 1 | 2 | 4 | 8, 31]
 # --shapes: real (non-diagnostic) code shapes of the same kernel, as tune dicts
 SHAPES = [{}, {"rtc_units": 2}, {"rtc_units": 2, "rtc_waves": 2}, {"rtc_waves": 2},
           {"rtc_units": 2, "rtc_xcd": 3}, {"rtc_units": 2, "rtc_waves": 2, "rtc_xcd": 3}]
-DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0}
+LEAN = [{}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 1, "rtc_waves": 4},
+        {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 2}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 3},
+        {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 3}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 1}]
+DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 0}
 
 
 def main():
@@ -34,6 +37,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=None, help="comma-separated rtc_diag values")
     ap.add_argument("--shapes", action="store_true", help="time the SHAPES code shapes instead (all bit-exact)")
+    ap.add_argument("--lean", action="store_true", help="time the LEAN schedule shapes instead (all bit-exact)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     args = ap.parse_args()
     import torch
@@ -41,8 +45,8 @@ def main():
     for kv in args.tune:
         k_, _, v_ = kv.partition("=")
         ecx.tune(k_, int(v_))
-    if args.shapes:
-        variants = [dict(sh) for sh in SHAPES]
+    if args.shapes or args.lean:
+        variants = [dict(sh) for sh in (SHAPES if args.shapes else LEAN)]
     else:
         variants = [{"rtc_diag": int(v)} for v in (args.variants.split(",") if args.variants else VARIANTS)]
     k, m, v, b, a = 10, 4, 2, 4096, 256

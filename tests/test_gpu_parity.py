@@ -1690,10 +1690,10 @@ def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
 
 @pytest.mark.parametrize("e,B,S", [(3, 4096, 5), (13, 8192 + 16, 3), (0, 4096, 17)])
 def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
-    """rtc_units 2: the plane-group kernel taking two 512-B slices per workgroup, the
-    second slice's rows loaded while the first finishes, in every block order and at 2
-    and 3 waves per SIMD, equals the one-slice kernel and the zero-filled Clay(12,4)
-    oracle (ClayCodeErasureDecodingStep.java:171-203) on a shortened Clay(10,4) repair."""
+    """rtc_units 2 (two 512-B slices per workgroup, the second slice's rows loaded while the
+    first finishes) and rtc_sched 1 (the lean load schedule, 1-4 pairs ahead), in every
+    block order and at 2-4 waves per SIMD, equal the default kernel and the zero-filled
+    Clay(12,4) oracle (ClayCodeErasureDecodingStep.java:171-203) on a shortened Clay(10,4)."""
     torch = torch_dev
     k, m, v = 10, 4, 2
     step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
@@ -1702,10 +1702,14 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
     ecx.fill_random(pool, pool.numel(), 300 + e)
     outs = []
     try:
-        for units, xcd, waves in [(1, 2, 3), (2, 2, 3), (2, 1, 3), (2, 3, 2), (2, 4, 3), (2, 0, 2)]:
+        for units, xcd, waves, sched, la in [(1, 2, 3, 0, 1), (2, 2, 3, 0, 1), (2, 1, 3, 0, 1), (2, 3, 2, 0, 1),
+                                             (2, 4, 3, 0, 1), (2, 0, 2, 0, 1), (1, 2, 4, 1, 1), (1, 2, 3, 1, 0),
+                                             (1, 3, 4, 1, 3), (2, 2, 3, 1, 2)]:
             ecx.tune("rtc_units", units)
             ecx.tune("rtc_xcd", xcd)
             ecx.tune("rtc_waves", waves)
+            ecx.tune("rtc_sched", sched)
+            ecx.tune("rtc_lookahead", la)
             o = torch.full((S, a, B), 0x6B, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
             torch.cuda.synchronize()
@@ -1715,6 +1719,8 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
         ecx.tune("rtc_units", 1)
         ecx.tune("rtc_xcd", 2)
         ecx.tune("rtc_waves", 3)
+        ecx.tune("rtc_sched", 0)
+        ecx.tune("rtc_lookahead", 1)
     assert all((x == outs[0]).all() for x in outs[1:])
     host = pool[S - 1].cpu().numpy()
     inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
