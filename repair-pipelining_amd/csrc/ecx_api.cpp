@@ -1104,7 +1104,7 @@ int ecx_tune(const char *key, int value) {
         t.rtc_diag = value;
     }
     else if (k == "rtc_sched") {
-        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_sched = value;
     }
     else if (k == "rtc_units") {

@@ -26,7 +26,9 @@ SHAPES = [{}, {"rtc_units": 2}, {"rtc_units": 2, "rtc_waves": 2}, {"rtc_waves": 
           {"rtc_units": 2, "rtc_xcd": 3}, {"rtc_units": 2, "rtc_waves": 2, "rtc_xcd": 3}]
 LEAN = [{}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 1, "rtc_waves": 4},
         {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 2}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 3},
-        {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 3}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 1}]
+        {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 3}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 1},
+        {"rtc_sched": 2, "rtc_lookahead": 0}, {"rtc_sched": 2, "rtc_waves": 4, "rtc_lookahead": 0},
+        {"rtc_sched": 2}, {"rtc_sched": 2, "rtc_lookahead": 8}]
 DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 0}
 
 

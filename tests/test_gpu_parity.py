@@ -1704,7 +1704,7 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
     try:
         for units, xcd, waves, sched, la in [(1, 2, 3, 0, 1), (2, 2, 3, 0, 1), (2, 1, 3, 0, 1), (2, 3, 2, 0, 1),
                                              (2, 4, 3, 0, 1), (2, 0, 2, 0, 1), (1, 2, 4, 1, 1), (1, 2, 3, 1, 0),
-                                             (1, 3, 4, 1, 3), (2, 2, 3, 1, 2)]:
+                                             (1, 3, 4, 1, 3), (2, 2, 3, 1, 2), (1, 2, 4, 2, 0), (1, 2, 3, 2, 8)]:
             ecx.tune("rtc_units", units)
             ecx.tune("rtc_xcd", xcd)
             ecx.tune("rtc_waves", waves)
