@@ -29,6 +29,8 @@ LEAN = [{}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 
         {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 3}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_xcd": 1},
         {"rtc_sched": 2, "rtc_lookahead": 0}, {"rtc_sched": 2, "rtc_waves": 4, "rtc_lookahead": 0},
         {"rtc_sched": 2}, {"rtc_sched": 2, "rtc_lookahead": 8}]
+FINAL = [{}, {"rtc_sched": 2, "rtc_lookahead": 8}, {"rtc_sched": 2, "rtc_lookahead": 0},
+         {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0, "rtc_xcd": 3}]
 DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 0}
 
 
@@ -40,6 +42,7 @@ def main():
     ap.add_argument("--variants", default=None, help="comma-separated rtc_diag values")
     ap.add_argument("--shapes", action="store_true", help="time the SHAPES code shapes instead (all bit-exact)")
     ap.add_argument("--lean", action="store_true", help="time the LEAN schedule shapes instead (all bit-exact)")
+    ap.add_argument("--final", action="store_true", help="time the FINAL candidates instead (all bit-exact)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     args = ap.parse_args()
     import torch
@@ -47,8 +50,8 @@ def main():
     for kv in args.tune:
         k_, _, v_ = kv.partition("=")
         ecx.tune(k_, int(v_))
-    if args.shapes or args.lean:
-        variants = [dict(sh) for sh in (SHAPES if args.shapes else LEAN)]
+    if args.shapes or args.lean or args.final:
+        variants = [dict(sh) for sh in (SHAPES if args.shapes else LEAN if args.lean else FINAL)]
     else:
         variants = [{"rtc_diag": int(v)} for v in (args.variants.split(",") if args.variants else VARIANTS)]
     k, m, v, b, a = 10, 4, 2, 4096, 256
