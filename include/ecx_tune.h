@@ -91,11 +91,12 @@
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes
  *                      per workgroup, partners exchanged in registers and LDS; default), 0 = one
  *                      helper plane per workgroup
- *   "rtc_sched"        the plane-group kernel's load schedule: 0 = rtc_lookahead's (default), 1 = lean:
- *                      no row-yc load in flight during the row-ya exchange, the row-yc (own, partner)
+ *   "rtc_sched"        the plane-group kernel's load schedule: 0 = rtc_lookahead's, 1 = lean: no
+ *                      row-yc load in flight during the row-ya exchange, the row-yc (own, partner)
  *                      pairs loaded 1 + (rtc_lookahead & 3) pairs ahead of use, the accumulators pinned
  *                      after every node -- 119 VGPRs and 4 waves per SIMD instead of 154 and 3; 2 =
- *                      rtc_lookahead's order with the accumulators pinned (132-151 VGPRs)
+ *                      every load of a unit issued up front, the accumulators pinned (151 VGPRs;
+ *                      default)
  *   "rtc_units"        the plane-group kernel's 512-B slices per workgroup: 1 (default), or 2 with the
  *                      second slice's first two rows loaded while the first slice finishes (software
  *                      pipelining across the exchange barrier; no persistent grid)

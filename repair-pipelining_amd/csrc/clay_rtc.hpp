@@ -42,9 +42,10 @@ struct RtcShape {
     // plane-group kernel: 512-B slices per workgroup, 1 or 2 (software-pipelined: the second
     // slice's rows yb and ya are loaded while the first finishes; ecx_tune "rtc_units")
     int units = 1;
-    // plane-group kernel load schedule: 0 = rtc_lookahead's, 1 = lean (row-yc pairs loaded two
-    // ahead of use, none in flight during the row-ya exchange: fewer live registers)
-    int sched = 0;
+    // plane-group kernel load schedule: 0 = rtc_lookahead's, 1 = lean (row-yc pairs loaded just
+    // ahead of use, none in flight during the row-ya exchange: 119 VGPRs, 4 waves/SIMD), 2 =
+    // every load of a unit issued up front, the accumulators pinned after every node
+    int sched = 2;
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

@@ -255,7 +255,9 @@ struct Tuning {
     int rtc_persist = 0;    // its persistent grid: workgroups per CU (0 = one workgroup per unit)
     int rtc_diag = 0;       // its DIAGNOSTIC builds (clay_rtc.hpp RtcShape::diag; ECX_DIAGNOSTIC=1 only)
     int rtc_units = 1;      // plane-group kernel: 512-B slices per workgroup, 1 or 2 (software-pipelined)
-    int rtc_sched = 0;      // plane-group kernel load schedule: 0 = rtc_lookahead's, 1 = lean
+    int rtc_sched = 2;      // plane-group kernel load schedule: 0 = rtc_lookahead's, 1 = lean, 2 = all loads
+                            // up front with pinned accumulators (+0.8-2.4 % over 0 on two boxes,
+                            // profiles/r03_clay104_final.jsonl, r03_clay104_lean_run2.jsonl)
     int rtc_xcd = 2;        // its block order: 1 = the helper planes of a (stripe, chunk) on one XCD;
                             // 2 (plane-group kernel): whole (stripe, chunk) units per XCD, +4.5 %
                             // (+1.1 % on Clay(10,4), profiles/r02_rtc_sweep.jsonl)

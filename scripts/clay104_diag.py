@@ -31,7 +31,7 @@ LEAN = [{}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 
         {"rtc_sched": 2}, {"rtc_sched": 2, "rtc_lookahead": 8}]
 FINAL = [{}, {"rtc_sched": 2, "rtc_lookahead": 8}, {"rtc_sched": 2, "rtc_lookahead": 0},
          {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0, "rtc_xcd": 3}]
-DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 0}
+DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 2}
 
 
 def main():

@@ -153,7 +153,7 @@ def test_tuning_keys(ecx):
     header = (ROOT / "include" / "ecx_tune.h").read_text()
     documented = re.findall(r'^ \*\s+"([a-z_]+)"', header, flags=re.M)
     defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "wave_groups": 0, "lds_tables": 1, "store_scope": 0,
-                "chunk_major": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "skew_trial": 0, "plan_cache": 256, "bitslice": 0, "lds_lut": 0, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_persist": 0, "rtc_units": 1, "rtc_sched": 0, "rtc_diag": 0, "xcd_run": 8, "xcd_misaligned": 1,
+                "chunk_major": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "skew_trial": 0, "plan_cache": 256, "bitslice": 0, "lds_lut": 0, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_persist": 0, "rtc_units": 1, "rtc_sched": 2, "rtc_diag": 0, "xcd_run": 8, "xcd_misaligned": 1,
                 "map_planes": 1, "planes_lookahead": 12, "planes_waves": 2,
                 "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512}
     assert sorted(documented) == sorted(defaults)

@@ -1361,6 +1361,7 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
             ecx.tune("rtc_group", grp)
             ecx.tune("rtc_persist", persist)
             ecx.tune("rtc_lookahead", la)
+            ecx.tune("rtc_sched", 2 if la == 1 else 0)  # the default schedule, and rtc_lookahead's for the rest
             o = torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda")
             step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
             torch.cuda.synchronize()
@@ -1371,6 +1372,7 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
         ecx.tune("rtc_group", 1)
         ecx.tune("rtc_persist", 0)
         ecx.tune("rtc_lookahead", 1)
+        ecx.tune("rtc_sched", 2)
     ref0 = outs[(0, 0, 0, 0, 1)][0]
     for mode in modes[1:]:
         want = "k_clay_repair_grp" if mode[2] else "k_clay_repair"
@@ -1702,9 +1704,10 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
     ecx.fill_random(pool, pool.numel(), 300 + e)
     outs = []
     try:
-        for units, xcd, waves, sched, la in [(1, 2, 3, 0, 1), (2, 2, 3, 0, 1), (2, 1, 3, 0, 1), (2, 3, 2, 0, 1),
-                                             (2, 4, 3, 0, 1), (2, 0, 2, 0, 1), (1, 2, 4, 1, 1), (1, 2, 3, 1, 0),
-                                             (1, 3, 4, 1, 3), (2, 2, 3, 1, 2), (1, 2, 4, 2, 0), (1, 2, 3, 2, 8)]:
+        for units, xcd, waves, sched, la in [(1, 2, 3, 2, 1), (1, 2, 3, 0, 1), (2, 2, 3, 0, 1), (2, 1, 3, 0, 1),
+                                             (2, 3, 2, 0, 1), (2, 4, 3, 0, 1), (2, 0, 2, 0, 1), (1, 2, 4, 1, 1),
+                                             (1, 2, 3, 1, 0), (1, 3, 4, 1, 3), (2, 2, 3, 1, 2), (1, 2, 4, 2, 0),
+                                             (2, 2, 2, 2, 1)]:
             ecx.tune("rtc_units", units)
             ecx.tune("rtc_xcd", xcd)
             ecx.tune("rtc_waves", waves)
@@ -1719,7 +1722,7 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
         ecx.tune("rtc_units", 1)
         ecx.tune("rtc_xcd", 2)
         ecx.tune("rtc_waves", 3)
-        ecx.tune("rtc_sched", 0)
+        ecx.tune("rtc_sched", 2)
         ecx.tune("rtc_lookahead", 1)
     assert all((x == outs[0]).all() for x in outs[1:])
     host = pool[S - 1].cpu().numpy()
