@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--erased", type=int, default=None, help="erased node (clay42: 1, README '1 LP 1 pipeline')")
     ap.add_argument("--pitch-pad", type=int, default=4096, help="rs124: bytes of padding per 4 MiB shard")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample; 0 = skip")
+    ap.add_argument("--cpu-protocol", default="bounded", choices=["bounded", "reference"],
+                    help="reference: BASELINE.md section 4's 2 warm-ups + 10 x 2 s per thread count (slow)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-probes", action="store_true", help="skip the in-run memory ceiling probes")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -145,7 +147,11 @@ def host_cpu_info() -> dict:
             "l3_bytes_machine": l3_all or None, "l3_bytes_affinity": l3_aff or None}
 
 
-def cpu_baseline(wl, seconds: float, sample=None, max_units=None):
+# BASELINE.md section 4's measurement protocol (ReedSolomonBenchmark.java:104-124)
+REF_WARMUPS, REF_MEASUREMENTS, REF_SECONDS = 2, 10, 2.0
+
+
+def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, protocol="bounded"):
     """The oracle (C restatement of the reference JVM path, stage by stage) on this host for
     workload `wl`, timed by oracle/orc_bench.c: one host thread, then one thread per CPU
     the lease allows (the cgroup quota, else OMP_NUM_THREADS, else the affinity mask;
@@ -155,7 +161,13 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None):
     GiB/s counts the workload's own algorithmic bytes per unit (wl.unit_bytes), as the
     GPU line does.  ``value`` is the all-threads figure; the 1-thread figure rides along.
     `sample` = (unit, GPU output) of one pool unit: the oracle computes it too, and
-    ``oracle_check`` says whether the bytes agree (the sampled byte-compare of 8(d))."""
+    ``oracle_check`` says whether the bytes agree (the sampled byte-compare of 8(d)).
+    `units` = a few units of the GPU run's own pool as host arrays (BASELINE.md section 4:
+    "the same synthetic stripes as the GPU run"), tiled through the arena; without them the
+    workload's cpu_spec() makes its own.  protocol "bounded" (the bench default, so the line
+    finishes in minutes): one sample of seconds/2 on one thread and one of `seconds` on all;
+    "reference" (ReedSolomonBenchmark.java:104-124): on each thread
+    count 2 warm-up measurements, then the mean of 10 measurements of 2 s each."""
     import numpy as np
     import oracle as O
 
@@ -179,7 +191,8 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None):
     # 8 distinct units (spec["make"]: valid stripes, or random bytes where the oracle's work
     # does not depend on the data), tiled through one host arena of n_units units: every
     # unit has its own memory (the cache sees the whole working set).
-    distinct = spec["make"](np.random.default_rng(0))
+    distinct = list(units) if units else spec["make"](np.random.default_rng(0))
+    data_kind = "GPU-pool" if units else spec["data_kind"]
     arena = np.empty((n_units,) + distinct[0].shape, np.uint8)
     for u in range(n_units):
         arena[u] = distinct[u % len(distinct)]
@@ -189,26 +202,50 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None):
     addrs = np.where(spec["present"][None, :] == 1, rows + spec["arena_slot"][None, :] * slot_bytes,
                      np.where(spec["present"][None, :] == 2, zero.ctypes.data, 0)).astype(np.int64)
     op, data, parity, erased = spec["op"], spec["data"], spec["parity"], spec["erased"]
-    n1, el1 = O.bench_run(op, data, parity, erased, slot_bytes, addrs, 1, seconds / 2)
-    nn, eln = O.bench_run(op, data, parity, erased, slot_bytes, addrs, threads, seconds)
-    one = n1 * wl.unit_bytes / el1 / 2**30
+
+    def rate(th, secs):
+        n, el = O.bench_run(op, data, parity, erased, slot_bytes, addrs, th, secs)
+        return n * wl.unit_bytes / el / 2**30, n, el
+
+    if protocol == "reference":
+        runs = {}
+        for th in (1, threads):
+            for _ in range(REF_WARMUPS):
+                rate(th, REF_SECONDS)
+            runs[th] = [rate(th, REF_SECONDS) for _ in range(REF_MEASUREMENTS)]
+        one = sum(r[0] for r in runs[1]) / REF_MEASUREMENTS
+        allv = sum(r[0] for r in runs[threads]) / REF_MEASUREMENTS
+        timing = (f"mean of {REF_MEASUREMENTS} measurements of {REF_SECONDS:g} s after {REF_WARMUPS} warm-ups on "
+                  f"{threads} threads "
+                  f"({min(r[0] for r in runs[threads]):.2f}-{max(r[0] for r in runs[threads]):.2f} GiB/s) and "
+                  f"on one ({min(r[0] for r in runs[1]):.3f}-{max(r[0] for r in runs[1]):.3f})")
+        measurements = {"threads": [round(r[0], 3) for r in runs[threads]], "one": [round(r[0], 4) for r in runs[1]]}
+    else:
+        one, n1, el1 = rate(1, seconds / 2)
+        allv, nn, eln = rate(threads, seconds)
+        timing = (f"{nn} operations on {threads} threads in {eln:.1f} s; single thread {n1} operations over all "
+                  f"{n_units} units in {el1:.1f} s")
+        measurements = None
     ws = n_units * wl.unit_bytes
-    return {
-        "value": round(nn * wl.unit_bytes / eln / 2**30, 3),
+    out = {
+        "value": round(allv, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "single_thread_value": round(one, 3),
         "oracle_check": oracle_check,
         "working_set_bytes": ws,
+        "protocol": protocol,
         "host": info,
-        "sample": f"{spec['what']}, stage-by-stage C restatement of the reference JVM path (oracle/): {nn} "
-                  f"operations on {threads} threads (lease quota {info['cgroup_quota_cpus']}, affinity "
-                  f"{info['affinity_cpus']} of {info['cpus_present']} CPUs) x {per_thread} host-resident "
-                  f"{spec['data_kind']} units each, {ws / 2**20:.0f} MiB of algorithmic bytes touched "
-                  f"(>= 2x the {l3 / 2**20:.0f} MiB L3), in {eln:.1f} s; single thread {n1} operations over all "
-                  f"{n_units} units in {el1:.1f} s; {info['model']}",
+        "sample": f"{spec['what']}, stage-by-stage C restatement of the reference JVM path (oracle/), "
+                  f"lease quota {info['cgroup_quota_cpus']} of {info['cpus_present']} CPUs (affinity "
+                  f"{info['affinity_cpus']}), {per_thread} host-resident {data_kind} units per thread, "
+                  f"{ws / 2**20:.0f} MiB of algorithmic bytes touched (>= 2x the {l3 / 2**20:.0f} MiB L3): {timing}; "
+                  f"{info['model']}",
     }
+    if measurements:
+        out["measurements_GiBps"] = measurements
+    return out
 
 
 # Sources that define what the device executes for a given map, per kernel family: the
@@ -312,6 +349,11 @@ class Workload:
         """The oracle's result for `unit` equals the GPU's `got`."""
         raise NotImplementedError
 
+    def host_units(self, k: int):
+        """k units of the resident pool (the GPU run's own data) as host arrays in the layout
+        cpu_spec() describes."""
+        raise NotImplementedError
+
     def cpu_spec(self) -> dict:
         """How cpu_baseline runs the oracle on this workload: op / data / parity / erased
         for orc_bench_run, make(rng) -> distinct host units [slots][bytes], and per oracle
@@ -344,6 +386,9 @@ class Clay42(Workload):
         return bool(self.torch.equal(self.out, self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.erased, :]))
 
     erased_list = property(lambda self: [self.erased])
+
+    def host_units(self, k):
+        return [self.pool[i].cpu().numpy() for i in range(min(k, self.P))]
 
     def sample(self):
         return self.pool[self.P // 2].cpu().numpy(), self.out[self.P // 2].cpu().numpy()
@@ -439,6 +484,9 @@ class Clay104(Workload):
         orig = self.pool.view(self.P, self.alpha, self.n, self.b)[:, :, self.erased, :]
         return bool(self.torch.equal(self.out, orig))
 
+    def host_units(self, k):
+        return [self.pool[i].cpu().numpy() for i in range(min(k, self.P))]
+
     def sample(self):
         return self.pool[self.P // 2].cpu().numpy(), self.out[self.P // 2].cpu().numpy()
 
@@ -504,6 +552,9 @@ class RS124(Workload):
     def verify(self):
         return bool(self.torch.equal(self.pool[:, 0:2, :self.L], self.orig))
 
+    def host_units(self, k):
+        return [self.pool[i, :, :self.L].cpu().numpy() for i in range(min(k, self.P))]
+
     def sample(self):
         s = self.P // 2
         return self.pool[s, :, :self.L].cpu().numpy(), self.pool[s, 0:2, :self.L].cpu().numpy()
@@ -559,6 +610,9 @@ class LRC(Workload):
 
     def verify(self):
         return bool(self.torch.equal(self.out[:, 0], self.pool[:, 2]))
+
+    def host_units(self, k):
+        return [self.pool[i, 0:4].cpu().numpy() for i in range(min(k, self.P))]
 
     def sample(self):
         s = self.P // 2
@@ -712,14 +766,15 @@ def main():
         per_rank = [float(x.item()) for x in g]
     per_rank_gibs = [stripes_per_step * args.steps * wl.unit_bytes / e / 2**30 for e in per_rank]
 
-    sample = None
+    sample = units = None
     if rank == 0 and args.cpu_seconds > 0:
         sample = wl.sample()  # one pool unit for the oracle check
+        units = wl.host_units(8 if wl.unit_bytes < (64 << 20) else 2)  # the GPU run's own stripes
     probes = memory_probes(ecx, torch, wl.region, wl.reads, wl.writes) if not args.no_probes else None
 
     cpu = None
     if sample is not None:  # rank 0 only, after the timed region (at any N)
-        cpu = cpu_baseline(wl, args.cpu_seconds, sample)
+        cpu = cpu_baseline(wl, args.cpu_seconds, sample, units=units, protocol=args.cpu_protocol)
 
     if rank == 0 and args.meta:
         Path(args.meta).write_text(json.dumps({

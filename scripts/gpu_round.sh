@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session on the MI355X box.  Modes (any of, in order): test bench gloo2 pmc prof
+# One GPU session on the MI355X box.  Modes (any of, in order): test bench gloo2 workloads refcpu pmc prof
 # Every GPU step has its own time limit; a fault/abort/timeout stops the script.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -32,6 +32,11 @@ if has workloads; then
     timeout -k 10 300 python bench.py --workload $W --steps 3 --warmup 1 > "$OUT/bench_$W.log" 2>&1
     rc=$?; echo "bench $W rc=$rc"; tail -1 "$OUT/bench_$W.log"; [ $rc -ne 0 ] && stop "bench $W" $rc
   done
+fi
+if has refcpu; then
+  # the headline line with BASELINE.md section 4's CPU protocol (2 warm-ups + 10 x 2 s)
+  timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-protocol reference > "$OUT/bench_refcpu.log" 2>&1
+  rc=$?; echo "bench refcpu rc=$rc"; tail -1 "$OUT/bench_refcpu.log"; [ $rc -ne 0 ] && stop "bench refcpu" $rc
 fi
 if has pmc; then
   bash "$ROOT/scripts/pmc.sh" || stop pmc $?

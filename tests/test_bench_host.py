@@ -116,6 +116,22 @@ def test_cpu_baseline_every_workload(case):
     assert cpu["oracle_check"] is None and "oracle/" in cpu["sample"]
 
 
+def test_cpu_baseline_on_given_units_reference_protocol(monkeypatch):
+    """The baseline runs on the units it is handed (the GPU pool's own stripes in bench.py)
+    and, under protocol "reference", reports the mean of REF_MEASUREMENTS measurements after
+    REF_WARMUPS warm-ups (shortened here)."""
+    import numpy as np
+    monkeypatch.setattr(bench, "REF_SECONDS", 0.02)
+    wl = _bare(bench.LRC)
+    shape = wl.cpu_spec()["make"](np.random.default_rng(0))[0].shape
+    units = [np.random.default_rng(i).integers(0, 256, shape, dtype=np.uint8) for i in range(3)]
+    cpu = bench.cpu_baseline(wl, 0.2, None, max_units=3, units=units, protocol="reference")
+    assert cpu["protocol"] == "reference" and "GPU-pool" in cpu["sample"]
+    assert len(cpu["measurements_GiBps"]["threads"]) == bench.REF_MEASUREMENTS
+    assert len(cpu["measurements_GiBps"]["one"]) == bench.REF_MEASUREMENTS
+    assert cpu["value"] > 0 and cpu["single_thread_value"] > 0
+
+
 def test_oracle_checks_of_the_workloads():
     """The sampled byte-compare of each workload agrees with an oracle-made unit and
     rejects a corrupted output byte (rs124 / lrc / clay104 on small host stand-ins)."""
