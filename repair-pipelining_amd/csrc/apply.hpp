@@ -49,8 +49,19 @@ __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
     else *(gu32x4 *)p = v;
 }
 
-// Byte-granular versions for the ragged tail / unaligned layouts.
+// Byte-granular versions for the ragged tail / unaligned layouts.  A lane whose 16
+// bytes all lie in range takes one 16-B access when its address is 16-B aligned, or
+// four dword accesses when it is 4-B aligned (the tail chunk of a shard that is a
+// multiple of 16 B but not of the chunk, e.g. 200,000 B); only the rest go by bytes.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
 __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, int valid) {
+    const uintptr_t al = (uintptr_t)p;
+    if (valid == 16 && (al & 15) == 0) return load16(p);
+    if (valid == 16 && (al & 3) == 0) {
+        const gu32 *d = (const gu32 *)p;
+        return (u32x4){d[0], d[1], d[2], d[3]};
+    }
     const gu8 *q = (const gu8 *)p;
     uint32_t w[4] = {0, 0, 0, 0};
     for (int b = 0; b < valid; ++b) w[b >> 2] |= (uint32_t)q[b] << (8 * (b & 3));
@@ -63,6 +74,19 @@ __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, int valid) {
 }
 
 __device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, int valid) {
+    const uintptr_t al = (uintptr_t)p;
+    if (valid == 16 && (al & 15) == 0) {
+        store16(p, v);
+        return;
+    }
+    if (valid == 16 && (al & 3) == 0) {
+        gu32 *d = (gu32 *)p;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+        return;
+    }
     gu8 *q = (gu8 *)p;
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
     for (int b = 0; b < valid; ++b) q[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));

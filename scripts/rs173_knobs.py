@@ -23,6 +23,11 @@ KNOBS_XCD = [{}, {"block_threads": 64}, {"xcd_group": 3, "xcd_run": 8}, {"xcd_gr
              {"xcd_group": 3, "xcd_run": 196}, {"block_threads": 64, "xcd_group": 3, "xcd_run": 8},
              {"block_threads": 64, "xcd_group": 3, "xcd_run": 196}, {"chunk_major": 1}, {"xcd_misaligned": 0},
              {"block_threads": 256}]
+KNOBS_SHAPES = [{}, {"block_threads": 64}, {"block_threads": 256}]
+KNOBS_T256 = [{}, {"block_threads": 256}, {"block_threads": 256, "depth": 4}, {"block_threads": 256, "depth": 12},
+              {"block_threads": 256, "depth": 16}, {"block_threads": 256, "depth": 20},
+              {"block_threads": 256, "xcd_misaligned": 0}, {"block_threads": 256, "small_tiles": 1},
+              {"block_threads": 256, "small_tiles": 1, "depth": 12}]
 DEFAULTS = {"depth": 0, "block_threads": 0, "small_tiles": 2, "skew_chunks": 1, "nontemporal": 1, "xcd_group": 0,
             "xcd_run": 8, "chunk_major": 0, "xcd_misaligned": 1}
 
@@ -33,13 +38,16 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--pad", type=int, default=0, help="bytes between shards")
-    ap.add_argument("--set", default="knobs", choices=["knobs", "xcd", "default"])
+    ap.add_argument("--shard", type=int, default=SHARD, help="shard bytes (the published benchmark: 200,000)")
+    ap.add_argument("--gib", type=float, default=None, help="size the stripe count to this many GiB of stripes")
+    ap.add_argument("--set", default="knobs", choices=["knobs", "xcd", "default", "shapes", "t256"])
     args = ap.parse_args()
-    knobs = {"knobs": KNOBS, "xcd": KNOBS_XCD, "default": [{}]}[args.set]
+    knobs = {"knobs": KNOBS, "xcd": KNOBS_XCD, "default": [{}], "shapes": KNOBS_SHAPES, "t256": KNOBS_T256}[args.set]
     import torch
     ecx = rpamd.load()
-    p = SHARD + args.pad
-    S = args.stripes
+    shard = args.shard
+    p = shard + args.pad
+    S = args.stripes if args.gib is None else max(1, int(args.gib * 2**30 / ((K + M) * p)))
     pool = torch.empty(S * (K + M) * p, dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 17)
     rs = ecx.ReedSolomon.create(K, M)
@@ -49,10 +57,10 @@ def main():
             for k, v in kn.items():
                 ecx.tune(k, v)
             try:
-                rs.encodeParityBatch(pool, (K + M) * p, p, S, 0, SHARD)
+                rs.encodeParityBatch(pool, (K + M) * p, p, S, 0, shard)
                 torch.cuda.synchronize()
                 kern[i] = ecx.last_kernel()
-                par = pool.view(S, K + M, p)[:, K:, :SHARD]
+                par = pool.view(S, K + M, p)[:, K:, :shard]
                 if ref is None:
                     ref = par.clone()
                 elif not bool(torch.equal(par, ref)):
@@ -60,16 +68,16 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.reps):
-                    rs.encodeParityBatch(pool, (K + M) * p, p, S, 0, SHARD)
+                    rs.encodeParityBatch(pool, (K + M) * p, p, S, 0, shard)
                 e1.record()
                 torch.cuda.synchronize()
             finally:
                 for k in kn:
                     ecx.tune(k, DEFAULTS[k])
-            res.setdefault(i, []).append((K + M) * SHARD * S / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
+            res.setdefault(i, []).append((K + M) * shard * S / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
     for i, kn in enumerate(knobs):
         med = statistics.median(res[i])
-        print(json.dumps({"knobs": kn, "pad": args.pad, "GBps": round(med, 1), "frac": round(med / 8000, 4),
+        print(json.dumps({"knobs": kn, "shard": shard, "pad": args.pad, "stripes": S, "GBps": round(med, 1), "frac": round(med / 8000, 4),
                           "kernel": kern[i]}), flush=True)
 
 

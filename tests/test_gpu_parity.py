@@ -989,6 +989,30 @@ def test_rs_batch_codec_entry_points(ecx, torch_dev, k, m):
     assert e.value.code == -2
 
 
+@pytest.mark.parametrize("off,pitch,cnt", [(4, 3072 + 20, 2990), (8, 4096 + 8, 4000), (1, 3072 + 17, 2983),
+                                            (0, 200000, 200000), (0, 200000 + 4, 200000 - 4)])
+def test_rs173_byte_safe_alignment_classes(ecx, torch_dev, off, pitch, cnt):
+    """RS(17,3) encodeParity over device stripes whose lanes fall in each alignment class of
+    the byte-safe kernels (apply.hpp load_partial / store_partial): 16-B aligned full lanes
+    of a tail chunk (200,000-B shards, the published benchmark's shape), dword-aligned
+    layouts (offset 4 / 8, pitch = 4 mod 16), byte-aligned ones, and ragged counts.
+    Every stripe equals the oracle's encode_parity on the same bytes."""
+    torch = torch_dev
+    k, m, S = 17, 3, 3
+    n = k + m
+    rs = ecx.ReedSolomon.create(k, m)
+    dev = torch.empty((S, n, pitch), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(dev, dev.numel(), 1703 + off)
+    host = dev.cpu().numpy()
+    rs.encodeParityBatch(dev, n * pitch, pitch, S, off, cnt)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    for s in range(S):
+        ref = [host[s, i].copy() for i in range(n)]
+        O.ReedSolomon(k, m).encode_parity(ref, off, cnt)
+        assert all((got[s, i] == ref[i]).all() for i in range(n)), s
+
+
 @pytest.mark.parametrize("n_out", [1, 2, 3, 4])
 def test_small_tile_variants(ecx, torch_dev, n_out):
     """Single-tile maps of at most 2 / 4 rows on the small-tile kernel variants
