@@ -39,12 +39,15 @@ def main():
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--pad", type=int, default=0, help="bytes between shards")
     ap.add_argument("--shard", type=int, default=SHARD, help="shard bytes (the published benchmark: 200,000)")
+    ap.add_argument("--k", type=int, default=17, help="data shards (RS(k, m) encode; default 17)")
+    ap.add_argument("--m", type=int, default=3, help="parity shards (default 3)")
     ap.add_argument("--gib", type=float, default=None, help="size the stripe count to this many GiB of stripes")
     ap.add_argument("--set", default="knobs", choices=["knobs", "xcd", "default", "shapes", "t256"])
     args = ap.parse_args()
     knobs = {"knobs": KNOBS, "xcd": KNOBS_XCD, "default": [{}], "shapes": KNOBS_SHAPES, "t256": KNOBS_T256}[args.set]
     import torch
     ecx = rpamd.load()
+    K, M = args.k, args.m
     shard = args.shard
     p = shard + args.pad
     S = args.stripes if args.gib is None else max(1, int(args.gib * 2**30 / ((K + M) * p)))
@@ -77,7 +80,7 @@ def main():
             res.setdefault(i, []).append((K + M) * shard * S / (e0.elapsed_time(e1) / args.reps * 1e-3) / 1e9)
     for i, kn in enumerate(knobs):
         med = statistics.median(res[i])
-        print(json.dumps({"knobs": kn, "shard": shard, "pad": args.pad, "stripes": S, "GBps": round(med, 1), "frac": round(med / 8000, 4),
+        print(json.dumps({"k": K, "m": M, "knobs": kn, "shard": shard, "pad": args.pad, "stripes": S, "GBps": round(med, 1), "frac": round(med / 8000, 4),
                           "kernel": kern[i]}), flush=True)
 
 
