@@ -49,7 +49,7 @@
  *                      workgroups over 1 KiB chunks -- on up to 2 GiB of its own stripes (3 rounds each,
  *                      on the caller's stream; overwrite mode, no capture, outputs not aliasing inputs)
  *                      and keep the fastest for that (map, pitch mod 16 MiB); 0 = the static rules
- *                      (skew on 4 MiB-multiple pitches, one wave for <= 3-row maps over >= 8 inputs;
+ *                      (skew on 4 MiB-multiple pitches, one wave for <= 2-row maps over >= 8 inputs;
  *                      default: within 1.4 % of the best shape at every RS(12,4) pitch measured,
  *                      while the trial's sample misjudged one pitch by 11 %).
  *                      The sample is four windows spread over the batch, and a shape replaces the

@@ -251,14 +251,16 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     const int nts = ntmode == 0 ? 0 : (tu.store_scope ? 2 : 1);
     // Launch shapes that exist (apply_launch.inc); anything else is clamped here.
     // Workgroup size: 256 threads over 4 KiB chunks; one wave over 1 KiB chunks when forced
-    // (64) or, in auto (0), for single-tile maps of <= 3 rows over >= 8 inputs whose slot
-    // pitch is not a 4 MiB multiple (RS(12,4) decode on its padded pitch: +2.4-2.8 %; RS(17,3)
-    // encode on 200,000-B shards: +4-7 %, profiles/r03_rs173_knobs.jsonl; every other BASELINE
-    // map -- LRC encode's 4 rows included -- is 3-8 % slower on one wave, profiles/r02_block_threads.jsonl).
+    // (64) or, in auto (0), for single-tile maps of <= 2 rows over >= 8 inputs whose slot
+    // pitch is not a 4 MiB multiple (RS(12,4) decode on its padded pitch: +2.4-2.8 %; every
+    // other BASELINE map -- LRC encode's 4 rows included -- is 3-8 % slower on one wave,
+    // profiles/r02_block_threads.jsonl).  3-row maps (RS(17,3) encode) run on 4 KiB
+    // workgroups: 0-4 % faster than one wave once the byte-safe tail took 16-B accesses
+    // (profiles/r03_rs_km.jsonl, r03_rs173_pitch.jsonl, r03_rs173_ab.jsonl).
     const bool skew_pitch = pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4 : pick == 1;
     const bool one_wave = tu.block_threads == 64 ||
                           (tu.block_threads == 0 && cm.n_tiles() == 1 && tu.bitslice != 2 && !tu.lds_lut &&
-                           (pick < 0 ? cm.max_tile_rows() <= 3 && cm.map().n_in >= 8 && !skew_pitch : pick == 2));
+                           (pick < 0 ? cm.max_tile_rows() <= 2 && cm.map().n_in >= 8 && !skew_pitch : pick == 2));
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     // Small-row kernel variants: forced (1), or auto (2) for maps of <= 2 rows over <= 4
@@ -496,7 +498,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 
 // The slot pitch decides whether rotating the chunk order pays (k_gf_apply_skew) or one-wave
 // workgroups do, and no simple rule predicts it beyond "4 MiB multiples gain" (DESIGN.md 4,
-// pitch sweep; RS(17,3) on 200,000-B shards gains 7 % from one wave, profiles/r03_rs173_knobs.jsonl).
+// pitch sweep; RS(12,4) decode gains 2-3 % from one wave at 4 MiB + 4 KiB, 10-17 % from skew at 4 MiB).
 // So on the first large batch (>= 512 MiB of input) of a single-tile map at a new pitch (mod
 // 16 MiB), the three launch shapes run on a sample of up to 2 GiB of the batch's own
 // stripes, three rounds each on the caller's stream, and the fastest is kept for that (map,
@@ -575,7 +577,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             // Run-to-run noise is a few %: another shape replaces the static rules' choice only
             // if it beats it by kTrialMargin on the sample.
             const bool skew_static = in_slot_stride % ((int64_t)4 << 20) == 0;
-            const int static_pick = skew_static ? 1 : (cm.max_tile_rows() <= 3 && m.n_in >= 8 ? 2 : 0);
+            const int static_pick = skew_static ? 1 : (cm.max_tile_rows() <= 2 && m.n_in >= 8 ? 2 : 0);
             pick = static_pick;
             for (int v = 0; v < kCand; ++v)
                 if (best[v] < best[pick] && best[v] < kTrialMargin * best[static_pick]) pick = v;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session on the MI355X box.  Modes (any of, in order): test bench gloo2 workloads refcpu pmc prof
+# One GPU session on the MI355X box.  Modes (any of; run in this order): test pmc bench gloo2 workloads refcpu prof
 # Every GPU step has its own time limit; a fault/abort/timeout stops the script.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -16,6 +16,13 @@ if has test; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread \
       > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && stop pytest $rc
+fi
+if has pmc; then
+  bash "$ROOT/scripts/pmc.sh" || stop pmc $?
+  # refresh this copy's profiles/pmc_traffic.json, so a bench later in the same call reports
+  # the traffic just measured (re-run scripts/pmc_summary.py on the merged gpurun_out/ to keep it)
+  python "$ROOT/scripts/pmc_summary.py" "$OUT" "$OUT/pmc_workloads_box.json" > "$OUT/pmc_summary.log" 2>&1 \
+      || stop pmc_summary $?
 fi
 if has bench; then
   timeout -k 10 600 python bench.py --steps 5 --warmup 2 > "$OUT/bench.log" 2>&1
@@ -37,9 +44,6 @@ if has refcpu; then
   # the headline line with BASELINE.md section 4's CPU protocol (2 warm-ups + 10 x 2 s)
   timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-protocol reference > "$OUT/bench_refcpu.log" 2>&1
   rc=$?; echo "bench refcpu rc=$rc"; tail -1 "$OUT/bench_refcpu.log"; [ $rc -ne 0 ] && stop "bench refcpu" $rc
-fi
-if has pmc; then
-  bash "$ROOT/scripts/pmc.sh" || stop pmc $?
 fi
 if has prof; then
   export TMPDIR=/tmp
