@@ -871,8 +871,9 @@ int ecx_clay_rtc_source(ecx_clay *clay, char *buf, int len) {
 int ecx_map_planes_compile_check(const ecx_map *map, int accumulate) {
     return guarded(__func__, [&]() -> int {
         PlanesShape sh;
-        sh.lookahead = tuning().planes_lookahead;
-        sh.waves = tuning().planes_waves;
+        const Tuning tu = tuning();
+        sh.lookahead = tu.planes_lookahead;
+        sh.waves = tu.planes_waves;
         return (int)rtc_compile_check(map_planes_source(map->cm.map(), sh, accumulate != 0));
     });
 }
@@ -880,8 +881,9 @@ int ecx_map_planes_compile_check(const ecx_map *map, int accumulate) {
 int ecx_map_planes_source(const ecx_map *map, int accumulate, char *buf, int len) {
     return guarded(__func__, [&]() -> int {
         PlanesShape sh;
-        sh.lookahead = tuning().planes_lookahead;
-        sh.waves = tuning().planes_waves;
+        const Tuning tu = tuning();
+        sh.lookahead = tu.planes_lookahead;
+        sh.waves = tu.planes_waves;
         const std::string src = map_planes_source(map->cm.map(), sh, accumulate != 0);
         if (buf && len > (int)src.size()) std::memcpy(buf, src.c_str(), src.size() + 1);
         return (int)src.size();
@@ -1012,11 +1014,9 @@ bool diagnostic_builds_allowed() {
     const char *v = std::getenv("ECX_DIAGNOSTIC");
     return v && std::strcmp(v, "1") == 0;
 }
-}  // namespace
 
-int ecx_tune(const char *key, int value) {
-    const std::string k = key ? key : "";
-    Tuning &t = tuning();
+// One ecx_tune key, under the tuning lock.
+int set_tune(Tuning &t, const std::string &k, int value) {
     if (k == "depth") {
         if (value != 0 && value != 2 && value != 4 && value != 8 && value != 10 && value != 12 && value != 16 &&
             value != 20 && value != 24)
@@ -1153,6 +1153,14 @@ int ecx_tune(const char *key, int value) {
     }
     else return ECX_E_ILLEGAL_ARGUMENT;
     return ECX_OK;
+}
+}  // namespace
+
+int ecx_tune(const char *key, int value) {
+    const std::string k = key ? key : "";
+    int rc = ECX_OK;
+    update_tuning([&](Tuning &t) { rc = set_tune(t, k, value); });
+    return rc;
 }
 
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream) {

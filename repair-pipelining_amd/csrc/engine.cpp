@@ -6,12 +6,24 @@
 #include <algorithm>
 #include <cstring>
 #include <exception>
+#include <functional>
+#include <mutex>
 
 namespace ecx {
 
-Tuning &tuning() {
-    static Tuning t;
-    return t;
+namespace {
+Tuning g_tuning;
+std::mutex g_tuning_mu;
+}  // namespace
+
+Tuning tuning() {
+    std::lock_guard<std::mutex> g(g_tuning_mu);
+    return g_tuning;
+}
+
+void update_tuning(const std::function<void(Tuning &)> &f) {
+    std::lock_guard<std::mutex> g(g_tuning_mu);
+    f(g_tuning);
 }
 
 static thread_local std::string g_last_kernel;
@@ -820,7 +832,8 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
     DrainOnUnwind drain{ctx.stream};
     const int64_t zc_pitch = (byte_count + 255) / 256 * 256;
     void *zc_dev = nullptr;
-    bool zero_copy = byte_count <= tuning().host_gather_max && tuning().host_zero_copy;
+    const Tuning tu = tuning();  // one snapshot for the whole call
+    bool zero_copy = byte_count <= tu.host_gather_max && tu.host_zero_copy;
     if (zero_copy) {
         const size_t bytes = (size_t)(zc_pitch * (int64_t)(cm.used_in_slots().size() + cm.used_out_slots().size()));
         if (hipHostGetDevicePointer(&zc_dev, ctx.ensure_pinned(bytes), 0) != hipSuccess) {
@@ -852,7 +865,7 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
             std::memcpy(outputs[outs[v]] + offset, host + (nin + v) * pitch, (size_t)byte_count);
         return;
     }
-    if (byte_count <= tuning().host_gather_max) {
+    if (byte_count <= tu.host_gather_max) {
         const std::vector<int> &outs = cm.used_out_slots();
         for (int slot : outs)
             if (!outputs[slot]) throw Error(ECX_E_NULL, "output buffer is null");

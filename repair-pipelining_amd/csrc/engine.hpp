@@ -21,6 +21,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -277,7 +278,11 @@ struct Tuning {
     int host_contexts = 1;  // per-call host APIs: 1 = a pool of contexts (streams) leased per call, 0 = one per device
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
-Tuning &tuning();
+// The process-wide tuning (include/ecx_tune.h).  tuning() returns a snapshot taken under
+// the lock update_tuning() holds while ecx_tune changes a field, so a launch reads one
+// consistent set of knobs even while another thread tunes.
+Tuning tuning();
+void update_tuning(const std::function<void(Tuning &)> &f);
 
 // The kernel instance of the last full-chunk (non-byte-safe) launch enqueued on this
 // thread, as rocprofv3 names it ("k_gf_apply<false, true, 1, 20, false, 256, 8>").
