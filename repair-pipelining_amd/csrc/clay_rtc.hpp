@@ -46,6 +46,11 @@ struct RtcShape {
     // ahead of use, none in flight during the row-ya exchange: 119 VGPRs, 4 waves/SIMD), 2 =
     // every load of a unit issued up front, the accumulators pinned after every node
     int sched = 2;
+    // non-temporal loads (ecx_tune "rtc_nt", bits): plane-group kernel -- 1 the sub-chunks read
+    // once (rows ya and yb, the column mates), 2 the row-yc own sub-chunks (re-read as partners
+    // by the neighbouring plane groups), 4 the row-yc partner loads; per-plane kernel -- any bit:
+    // every load
+    int nt = 0;
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

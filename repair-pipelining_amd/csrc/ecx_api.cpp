@@ -1107,6 +1107,10 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_sched = value;
     }
+    else if (k == "rtc_nt") {
+        if (value < 0 || value > 7) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_nt = value;
+    }
     else if (k == "rtc_units") {
         if (value < 1 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_units = value;

@@ -271,18 +271,26 @@ def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
     workgroup kernel for every code."""
     step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
     try:
-        for grp, persist in ((1, 0), (1, 2), (0, 0)):
+        for grp, persist, nt in ((1, 0, 0), (1, 2, 0), (0, 0, 0), (1, 0, 7), (1, 0, 1), (0, 0, 1)):
             ecx.tune("rtc_group", grp)
             ecx.tune("rtc_persist", persist)
+            ecx.tune("rtc_nt", nt)
             assert step.rtcCompileCheck() > 0
             src = step.rtcSource()
             name = "k_clay_repair_grp(" if grp and m == 4 else "k_clay_repair("
             assert name in src and "__launch_bounds__" in src
             if name == "k_clay_repair_grp(":
                 assert ("for (u32 b = blockIdx.x; b < n_units" in src) == (persist > 0)
+                # rtc_nt: the non-temporal loader is called only when some bit asks for it
+                assert ("    ldv2(" in src) == (nt > 0)
+                if nt & 1 == 0:
+                    assert "    ldv0(" in src
+            else:
+                assert ("(int)so, 2);" in src) == (nt > 0)
     finally:
         ecx.tune("rtc_group", 1)
         ecx.tune("rtc_persist", 0)
+        ecx.tune("rtc_nt", 0)
 
 
 def test_clay_rtc_refuses_multi_erasure(ecx):
