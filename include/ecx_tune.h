@@ -103,7 +103,7 @@
  *   "rtc_nt"           non-temporal loads in the generated Clay kernels, bits: plane-group kernel --
  *                      1 the sub-chunks read once (rows ya and yb, the column mates), 2 the row-yc
  *                      own sub-chunks (re-read as partners by the neighbouring plane groups), 4 the
- *                      row-yc partner loads; per-plane kernel -- any bit: every load; 0..7
+ *                      row-yc partner loads; per-plane kernel -- 8 every load; 0..15, default 5
  *   "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
  *                      a persistent grid of that many workgroups per CU walking the units
  *   "rtc_xcd"          that kernel's block order: 1 = the helper planes of one (stripe, chunk) on one

@@ -48,9 +48,9 @@ struct RtcShape {
     int sched = 2;
     // non-temporal loads (ecx_tune "rtc_nt", bits): plane-group kernel -- 1 the sub-chunks read
     // once (rows ya and yb, the column mates), 2 the row-yc own sub-chunks (re-read as partners
-    // by the neighbouring plane groups), 4 the row-yc partner loads; per-plane kernel -- any bit:
-    // every load
-    int nt = 0;
+    // by the neighbouring plane groups), 4 the row-yc partner loads; per-plane kernel -- 8: every
+    // load (its own sub-chunks are re-read as partners, from L2)
+    int nt = 5;
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

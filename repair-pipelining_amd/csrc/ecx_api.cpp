@@ -1108,7 +1108,7 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         t.rtc_sched = value;
     }
     else if (k == "rtc_nt") {
-        if (value < 0 || value > 7) return ECX_E_ILLEGAL_ARGUMENT;
+        if (value < 0 || value > 15) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_nt = value;
     }
     else if (k == "rtc_units") {

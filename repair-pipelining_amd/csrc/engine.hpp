@@ -259,7 +259,9 @@ struct Tuning {
     int rtc_sched = 2;      // plane-group kernel load schedule: 0 = rtc_lookahead's, 1 = lean, 2 = all loads
                             // up front with pinned accumulators (+0.8-2.4 % over 0 on two boxes,
                             // profiles/r03_clay104_final.jsonl, r03_clay104_lean_run2.jsonl)
-    int rtc_nt = 0;         // non-temporal loads in the generated Clay kernels (RtcShape::nt bits)
+    int rtc_nt = 5;         // non-temporal loads in the generated Clay kernels (RtcShape::nt bits):
+                            // 5 = the plane-group kernel's read-once rows and row-yc partner loads,
+                            // +3-6 % on Clay(10,4) over cached loads (profiles/r03_clay104_nt.jsonl)
     int rtc_xcd = 2;        // its block order: 1 = the helper planes of a (stripe, chunk) on one XCD;
                             // 2 (plane-group kernel): whole (stripe, chunk) units per XCD, +4.5 %
                             // (+1.1 % on Clay(10,4), profiles/r02_rtc_sweep.jsonl)

@@ -6,7 +6,7 @@ one, 16 the bit-plane transposes -- and are timed against the real kernel in int
 rounds on BASELINE config 4 (2,048 resident stripes, 1 MiB node blocks, repair of node 3).
 Median launch time -> algorithmic GB/s of the REAL repair's bytes, fraction of 8 TB/s.
 
-    python scripts/clay104_diag.py [--rounds 3 --reps 10] [--shapes | --lean | --final | --nt]
+    python scripts/clay104_diag.py [--rounds 3 --reps 10] [--shapes | --lean | --final | --nt | --json LIST]
 """
 import argparse
 import json
@@ -31,9 +31,10 @@ LEAN = [{}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 
         {"rtc_sched": 2}, {"rtc_sched": 2, "rtc_lookahead": 8}]
 FINAL = [{}, {"rtc_sched": 2, "rtc_lookahead": 8}, {"rtc_sched": 2, "rtc_lookahead": 0},
          {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0}, {"rtc_sched": 1, "rtc_waves": 4, "rtc_lookahead": 0, "rtc_xcd": 3}]
-# --nt: non-temporal load policies (rtc_nt bits: 1 rows read once, 2 row-yc own, 4 row-yc partners)
-NT = [{}, {"rtc_nt": 1}, {"rtc_nt": 3}, {"rtc_nt": 7}, {"rtc_nt": 5}, {"rtc_nt": 2}, {"rtc_nt": 1, "rtc_xcd": 3}]
-DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 2, "rtc_nt": 0}
+# --nt: non-temporal load policies (rtc_nt bits: 1 rows read once, 2 row-yc own, 4 row-yc partners; default 5)
+NT = [{"rtc_nt": 0}, {"rtc_nt": 1}, {"rtc_nt": 3}, {"rtc_nt": 7}, {}, {"rtc_nt": 2}, {"rtc_nt": 1, "rtc_xcd": 3}]
+# --json '[{...}, ...]': any list of bit-exact shapes
+DEFAULTS = {"rtc_units": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_lookahead": 1, "rtc_diag": 0, "rtc_sched": 2, "rtc_nt": 5}
 
 
 def main():
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--lean", action="store_true", help="time the LEAN schedule shapes instead (all bit-exact)")
     ap.add_argument("--final", action="store_true", help="time the FINAL candidates instead (all bit-exact)")
     ap.add_argument("--nt", action="store_true", help="time the NT load policies instead (all bit-exact)")
+    ap.add_argument("--json", default=None, help="a JSON list of tune dicts to time (all bit-exact)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     args = ap.parse_args()
     import torch
@@ -53,7 +55,9 @@ def main():
     for kv in args.tune:
         k_, _, v_ = kv.partition("=")
         ecx.tune(k_, int(v_))
-    if args.shapes or args.lean or args.final or args.nt:
+    if args.json:
+        variants = [dict(sh) for sh in json.loads(args.json)]
+    elif args.shapes or args.lean or args.final or args.nt:
         variants = [dict(sh) for sh in (SHAPES if args.shapes else LEAN if args.lean else FINAL if args.final else NT)]
     else:
         variants = [{"rtc_diag": int(v)} for v in (args.variants.split(",") if args.variants else VARIANTS)]

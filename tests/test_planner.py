@@ -271,7 +271,7 @@ def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
     workgroup kernel for every code."""
     step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
     try:
-        for grp, persist, nt in ((1, 0, 0), (1, 2, 0), (0, 0, 0), (1, 0, 7), (1, 0, 1), (0, 0, 1)):
+        for grp, persist, nt in ((1, 0, 0), (1, 2, 0), (0, 0, 0), (1, 0, 7), (1, 0, 1), (0, 0, 8), (0, 0, 5), (1, 0, 5)):
             ecx.tune("rtc_group", grp)
             ecx.tune("rtc_persist", persist)
             ecx.tune("rtc_nt", nt)
@@ -282,15 +282,15 @@ def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
             if name == "k_clay_repair_grp(":
                 assert ("for (u32 b = blockIdx.x; b < n_units" in src) == (persist > 0)
                 # rtc_nt: the non-temporal loader is called only when some bit asks for it
-                assert ("    ldv2(" in src) == (nt > 0)
+                assert ("    ldv2(" in src) == (nt & 7 > 0)
                 if nt & 1 == 0:
                     assert "    ldv0(" in src
             else:
-                assert ("(int)so, 2);" in src) == (nt > 0)
+                assert ("(int)so, 2);" in src) == (nt & 8 > 0)
     finally:
         ecx.tune("rtc_group", 1)
         ecx.tune("rtc_persist", 0)
-        ecx.tune("rtc_nt", 0)
+        ecx.tune("rtc_nt", 5)
 
 
 def test_clay_rtc_refuses_multi_erasure(ecx):
