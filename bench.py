@@ -30,6 +30,10 @@ contract (same launch, timing and JSON line; the default is the headline):
            data block 2 from its local group, 2^15 resident stripes per GPU
   clay42x2 SURVEY 8(f) f4: Clay(4,2), 32 KiB, two-node repair of nodes {0, 3}
            (doDecodeMulti) over the headline's pool of 2^15 stripes
+  rs173    the reference's only published benchmark (rs/README.md:53): RS(17,3)
+           encodeParity in place on 200,000-B shards, 4,096 resident stripes per GPU;
+           value in its own convention, MB/s of input data (10^6 B,
+           ReedSolomonBenchmark.java:116-121), with vs_baseline = value / 525.7 MB/s
 Every workload carries a cpu_baseline (rank 0, after the timed region, at any N): the
 oracle's restatement of the reference path for that workload on this host's cores.
 """
@@ -63,7 +67,11 @@ WORKLOADS = {
     "lrc": ("GiB/s local-group repair (device-resident), LRC(12,4) 64 KiB blocks, 1/2/4/8 GPU", 1 << 15, 1 << 18),
     "clay42x2": ("GiB/s two-node repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU", 1 << 15,
                  1 << 18),
+    "rs173": ("MB/s RS(17,3) encodeParity (device-resident), 200,000-B shards, input data bytes / 10^6 "
+              "(ReedSolomonBenchmark convention), 1/2/4/8 GPU", 4096, 1 << 15),
 }
+# the one published reference number for a workload: vs_baseline = value / it
+PUBLISHED = {"rs173": 525.7}  # MB/s, RS(17,3) encodeParity, InputOutputByteTableCodingLoop (rs/README.md:53)
 
 
 def parse():
@@ -334,6 +342,10 @@ class Workload:
     write_bytes = WRITE_BYTES         # of which written
     reads, writes = 20, 8             # equal-sized streams read / written per unit (mix model)
     description = ""
+    # the line's `value` unit: GiB/s of algorithmic bytes, or (rs173) the published benchmark's
+    # MB/s of input data bytes (metric_bytes per unit, per metric_scale bytes)
+    metric_unit, metric_scale, metric_bytes = "GiB/s", float(2**30), None
+    data_desc = "synthetic (device splitmix64 data, GPU encode -> valid stripes)"
 
     def launch(self):
         raise NotImplementedError
@@ -578,6 +590,67 @@ class RS124(Workload):
                         "inverted per call as ReedSolomon.java:224-244 does), 4 MiB shards"}
 
 
+class RS173(Workload):
+    """The reference's published benchmark shape (rs/README.md:53, ReedSolomonBenchmark.java:
+    25-33,104-124): RS(17,3) encodeParity over 200,000-byte shards, parity written in place.
+    Shards lie back to back (pitch 200,000 B): every other slot is 64 B off a 128-B line and
+    each shard ends in a 320-B partial chunk, as DESIGN.md section 4 measures."""
+    k, m, L = 17, 3, 200 * 1000
+    reads, writes = 17, 3
+    unit_bytes = 20 * 200 * 1000        # 17 shards read + 3 written (roofline bytes)
+    write_bytes = 3 * 200 * 1000
+    metric_unit, metric_scale, metric_bytes = "MB/s", 1e6, 17 * 200 * 1000  # data bytes, 10^6
+    data_desc = "synthetic (device splitmix64 data shards; the timed launch is the encode itself)"
+
+    def __init__(self, ecx, torch, dev, P, seed):
+        self.P, self.torch = P, torch
+        L = self.L
+        self.pool = torch.empty((P, 20, L), dtype=torch.uint8, device=dev)
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
+        self.rs = ecx.ReedSolomon.create(self.k, self.m)
+        self.region = self.pool
+        self.description = "RS(17,3) encodeParity in place, 200,000-B shards back to back (the published shape)"
+
+    def launch(self):
+        self.rs.encodeParityBatch(self.pool, 20 * self.L, self.L, self.P, 0, self.L)
+
+    def verify(self):
+        """The parity the GPU wrote equals the oracle's on two stripes, and re-encoding
+        leaves every stripe unchanged (isParityCorrect over the whole pool)."""
+        before = self.pool[:, self.k:, :].clone()
+        self.launch()
+        self.torch.cuda.synchronize()
+        same = bool(self.torch.equal(before, self.pool[:, self.k:, :]))
+        return same and all(self.oracle_check(self.pool[s].cpu().numpy(), self.pool[s, self.k:].cpu().numpy())
+                            for s in (0, self.P - 1))
+
+    def host_units(self, k):
+        return [self.pool[i].cpu().numpy() for i in range(min(k, self.P))]
+
+    def sample(self):
+        s = self.P // 2
+        return self.pool[s].cpu().numpy(), self.pool[s, self.k:].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import oracle as O
+        shards = [stripe[i].copy() for i in range(20)]
+        for i in range(self.k, 20):
+            shards[i][:] = 0
+        O.ReedSolomon(self.k, self.m).encode_parity(shards, 0, self.L)
+        return all(bool((shards[self.k + j] == got[j]).all()) for j in range(self.m))
+
+    def cpu_spec(self):
+        import numpy as np
+        import oracle as O
+
+        def make(rng):  # random data shards: encodeParity's work does not depend on the data
+            return [rng.integers(0, 256, (20, self.L), dtype=np.uint8) for _ in range(8)]
+        return {"op": O.BENCH_RS_ENCODE, "data": self.k, "parity": self.m, "erased": [], "make": make,
+                "arena_slot": np.arange(20), "present": np.ones(20, np.int64), "data_kind": "random-byte",
+                "what": "RS(17,3) encodeParity (InputOutputByteTableCodingLoop, ReedSolomon.java:94-108), "
+                        "200,000-B shards"}
+
+
 class LRC(Workload):
     """Config 3: LRC (LRCErasureCodeExample shapes: 12 data blocks in 4 local groups of 3,
     each with an XOR parity), 64 KiB blocks; repair of data block 2 from its group."""
@@ -710,6 +783,8 @@ def main():
         wl = Clay42x2(ecx, torch, dev, P, args.erased, seed)
     elif args.workload == "rs124":
         wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed)
+    elif args.workload == "rs173":
+        wl = RS173(ecx, torch, dev, P, seed)
     else:
         wl = LRC(ecx, torch, dev, P, seed)
 
@@ -755,7 +830,8 @@ def main():
     per_launch_bytes = P * wl.unit_bytes
     achieved = per_launch_bytes / (launch_ms * 1e-3) / 1e9
     total_stripes = stripes_per_step * args.steps * world
-    value = total_stripes * wl.unit_bytes / el / 2**30
+    metric_bytes = wl.metric_bytes or wl.unit_bytes
+    value = total_stripes * metric_bytes / el / wl.metric_scale
     traffic, traffic_note = pmc_traffic(args.workload, P, kernel)
 
     # per-rank rates, so an N-GPU efficiency shortfall can be attributed to a rank
@@ -764,7 +840,7 @@ def main():
         g = [torch.zeros(1, dtype=torch.float64, device=dev if backend == "nccl" else "cpu") for _ in range(world)]
         dist.all_gather(g, torch.tensor([own_el], dtype=torch.float64, device=g[0].device))
         per_rank = [float(x.item()) for x in g]
-    per_rank_gibs = [stripes_per_step * args.steps * wl.unit_bytes / e / 2**30 for e in per_rank]
+    per_rank_gibs = [stripes_per_step * args.steps * metric_bytes / e / wl.metric_scale for e in per_rank]
 
     sample = units = None
     if rank == 0 and args.cpu_seconds > 0:
@@ -775,6 +851,11 @@ def main():
     cpu = None
     if sample is not None:  # rank 0 only, after the timed region (at any N)
         cpu = cpu_baseline(wl, args.cpu_seconds, sample, units=units, protocol=args.cpu_protocol)
+        if wl.metric_unit != "GiB/s":  # the line's own unit: metric bytes per metric_scale
+            f = 2**30 / wl.metric_scale * metric_bytes / wl.unit_bytes
+            cpu["algorithmic_GiBps"] = cpu["value"]
+            cpu["value"], cpu["unit"] = round(cpu["value"] * f, 1), wl.metric_unit
+            cpu["single_thread_value"] = round(cpu["single_thread_value"] * f, 1)
 
     if rank == 0 and args.meta:
         Path(args.meta).write_text(json.dumps({
@@ -785,16 +866,16 @@ def main():
         line = {
             "metric": WORKLOADS[args.workload][0],
             "value": round(value, 3),
-            "unit": "GiB/s",
+            "unit": wl.metric_unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": round(value / PUBLISHED[args.workload], 1) if args.workload in PUBLISHED else None,
             "dtype": "u8",
-            "data": "synthetic (device splitmix64 data, GPU encode -> valid stripes)",
+            "data": wl.data_desc,
             "config": {
                 "workload": "%s, %d stripes per GPU per step over a resident pool of %d" % (wl.description,
                                                                                             stripes_per_step, P),
@@ -817,7 +898,7 @@ def main():
                 "frac_of_mix_model": round(achieved / probes["mix_model_GBps"], 4) if probes else None,
             },
             "repaired_output_GiBps": round(total_stripes * wl.write_bytes / el / 2**30, 3),
-            "per_rank_GiBps": {"min": round(min(per_rank_gibs), 3), "max": round(max(per_rank_gibs), 3),
+            "per_rank_%s" % ("GiBps" if wl.metric_unit == "GiB/s" else "MBps"): {"min": round(min(per_rank_gibs), 3), "max": round(max(per_rank_gibs), 3),
                                "ranks": [round(v, 3) for v in per_rank_gibs]},
             "cpu_baseline": cpu,
             "verified": verified,

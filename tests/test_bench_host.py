@@ -42,8 +42,9 @@ def test_committed_pmc_profile_matches_current_sources():
         traffic, note = bench.pmc_traffic(w, e["pool_stripes"], e["kernel"])
         assert note is None and traffic == e["hbm_bytes_per_launch"], (w, note)
         # within 0.1 % of the algorithmic bytes on the composed maps; Clay(10,4)'s plane-group
-        # kernel measures 1.019-1.021x across rounds
-        bound = 1.03 if w == "clay104" else 1.001
+        # kernel measures 1.004-1.021x across rounds; RS(17,3)'s 200,000-B
+        # shards leave every other slot 64 B off a 128-B line (reads ~1.035x)
+        bound = {"clay104": 1.03, "rs173": 1.05}.get(w, 1.001)
         assert 1.0 <= traffic / e["algorithmic_bytes_per_launch"] < bound, w
 
 
@@ -97,7 +98,7 @@ def _bare(cls, **attrs):
     return wl
 
 
-@pytest.mark.parametrize("case", ["clay42", "clay42x2", "clay104", "rs124", "lrc"])
+@pytest.mark.parametrize("case", ["clay42", "clay42x2", "clay104", "rs124", "lrc", "rs173"])
 def test_cpu_baseline_every_workload(case):
     """Every bench workload has an oracle baseline (the reference path
     restated by oracle/, timed by oracle/orc_bench.c orc_bench_run), here on a bounded
@@ -110,6 +111,8 @@ def test_cpu_baseline_every_workload(case):
         wl = _bare(bench.Clay104, erased=3, n=14, unit_bytes=1088 * 4096)
     elif case == "rs124":
         wl = _bare(bench.RS124)
+    elif case == "rs173":
+        wl = _bare(bench.RS173)
     else:
         wl = _bare(bench.LRC)
     cpu = bench.cpu_baseline(wl, 0.2, None, max_units=2)
@@ -156,3 +159,23 @@ def test_oracle_checks_of_the_workloads():
     stripe = np.stack(shards)
     assert rs.oracle_check(stripe, stripe[0:2].copy())
     assert not rs.oracle_check(stripe, stripe[1:3].copy())
+    # RS(17,3) encodeParity (the published benchmark's shape, shortened shards)
+    r17 = _bare(bench.RS173, L=640)
+    shards = [rng.integers(0, 256, 640, dtype=np.uint8) for _ in range(17)] + [np.zeros(640, np.uint8)] * 3
+    shards = [s.copy() for s in shards]
+    O.ReedSolomon(17, 3).encode_parity(shards, 0, 640)
+    stripe = np.stack(shards)
+    assert r17.oracle_check(stripe, stripe[17:20].copy())
+    bad = stripe[17:20].copy()
+    bad[2, 639] ^= 0x80
+    assert not r17.oracle_check(stripe, bad)
+
+
+def test_published_metric_conversion():
+    """rs173 reports the published benchmark's own unit (MB/s of input data bytes,
+    ReedSolomonBenchmark.java:116-121) and vs_baseline against rs/README.md:53's 525.7."""
+    wl = bench.RS173
+    assert wl.metric_unit == "MB/s" and wl.metric_scale == 1e6 and wl.metric_bytes == 17 * 200000
+    assert wl.unit_bytes == 20 * 200000 and bench.PUBLISHED == {"rs173": 525.7}
+    assert bench.WORKLOADS["rs173"][0].startswith("MB/s RS(17,3) encodeParity")
+    assert all(getattr(bench, c).metric_unit == "GiB/s" for c in ("Clay42", "Clay104", "RS124", "LRC"))
