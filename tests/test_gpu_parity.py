@@ -1753,3 +1753,35 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
     inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
     ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
     assert all((outs[1][S - 1, z] == ref[z]).all() for z in range(a))
+
+
+@pytest.mark.parametrize("e,B,S", [(3, 4096, 5), (11, 4096 + 48, 3)])
+def test_clay_rtc_nontemporal_policies_vs_oracle(ecx, torch_dev, e, B, S):
+    """Every non-temporal load policy (ecx_tune rtc_nt: cached, the read-once rows, the
+    row-yc own / partner loads, the default 5, all; bit 8 the per-plane kernel's loads)
+    gives the same repair on both generated Clay kernels, equal to the zero-filled
+    Clay(12,4) oracle (ClayCodeErasureDecodingStep.java:171-203) on a shortened Clay(10,4)."""
+    torch = torch_dev
+    k, m, v = 10, 4, 2
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    n, a = k + m, step.subPacketSize
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 500 + e)
+    outs = []
+    try:
+        for grp, nt in [(1, 5), (1, 0), (1, 1), (1, 2), (1, 3), (1, 4), (1, 7), (1, 15), (0, 0), (0, 8), (0, 5)]:
+            ecx.tune("rtc_group", grp)
+            ecx.tune("rtc_nt", nt)
+            o = torch.full((S, a, B), 0x3C, dtype=torch.uint8, device="cuda")
+            step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
+            torch.cuda.synchronize()
+            assert ecx.last_kernel() == ("k_clay_repair_grp" if grp else "k_clay_repair")
+            outs.append(o.cpu().numpy())
+    finally:
+        ecx.tune("rtc_group", 1)
+        ecx.tune("rtc_nt", 5)
+    assert all((x == outs[0]).all() for x in outs[1:])
+    host = pool[S - 1].cpu().numpy()
+    inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
+    ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
+    assert all((outs[0][S - 1, z] == ref[z]).all() for z in range(a))
