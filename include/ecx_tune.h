@@ -27,6 +27,10 @@
  *                      in LDS, for multi-tile maps (default); 2 = for every map
  *   "store_scope"      0 = non-temporal output stores (`nt`, default); 1 = `nt sc0 sc1`
  *                      (system scope: written through, dropped from L2)
+ *   "occ_lds"          extra dynamic LDS bytes per k_gf_apply workgroup, which caps the workgroups
+ *                      resident per CU at floor(160 KiB / bytes): 0 = no cap (default), -1 = the
+ *                      single-tile maps over >= 8 inputs on rings of <= 8 loads at 4 waves per
+ *                      SIMD, 1..65536 = that many bytes
  *   "chunk_major"      block order of the one-workgroup-per-tile kernel: 0 = stripe-major
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
  *   "block_threads"    one-workgroup-per-tile kernel: 256 threads over 4 KiB chunks or 64 threads

@@ -1044,6 +1044,10 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         t.wave_groups = value;
     }
     else if (k == "store_scope") t.store_scope = value != 0;
+    else if (k == "occ_lds") {
+        if (value < -1 || value > 65536) return ECX_E_ILLEGAL_ARGUMENT;
+        t.occ_lds = value;
+    }
     else if (k == "chunk_major") t.chunk_major = value != 0;
     else if (k == "small_tiles") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;

@@ -35,6 +35,9 @@ constexpr int kEntryDwords = 48;
 constexpr int kTileDwords = 16;
 constexpr int kChunkBytes = 4096;  // one 256-thread workgroup x 16 bytes per lane
 constexpr int kBlockThreads = 256;
+constexpr size_t kLdsPerCu = 160 * 1024;  // MI355X (gfx950) LDS per CU
+constexpr int kSimdsPerCu = 4;
+constexpr int kOccWavesPerSimd = 4;       // the residency cap of the many-stream single-tile maps
 constexpr int kWaveGroup = 8;       // k_gf_apply_lds: up to 8 tiles (one wave each) per workgroup
 constexpr int kGroupDwords = 16;    // group: [0..7] tiles (kNoTile = none), [8] union begin, [9] union count
 constexpr int kWaveChunkBytes = 1024;  // k_gf_apply_lds: 64 lanes x 16 bytes per wave
@@ -209,6 +212,12 @@ struct Tuning {
     // Non-temporal output stores: 0 = `nt`; 1 = `nt sc0 sc1` (written through, dropped
     // from L2; scripts/copy_probe.hip).
     int store_scope = 0;
+    // k_gf_apply: extra dynamic LDS bytes per workgroup, which caps the workgroups resident
+    // per CU (160 KiB of LDS each) without touching the kernel.  0 = no cap (default); -1 =
+    // single-tile maps over >= 8 inputs on rings of <= 8 loads held to 4 waves per SIMD; > 0 =
+    // that many bytes.  Measured mixed on the RS maps (+2 % in fresh-process A/B runs, -2 to
+    // -5 % in one-process interleaved sweeps; profiles/r03_occupancy.jsonl, r03_occ_bench.jsonl).
+    int occ_lds = 0;
     // k_gf_apply block order: 0 = stripe-major (a stripe's chunks back to back), 1 = chunk-major.
     int chunk_major = 0;
     // k_gf_apply workgroup: 256 threads over 4 KiB chunks (default) or 64 threads (one

@@ -458,7 +458,13 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                      (tu.lds_tables == 2 || (tu.lds_tables == 1 && a.n_tiles > 1));
             s.threads = threads;
             s.rows = rows;
-            const size_t lds = s.tlds ? (size_t)plan.max_tile_entries * kAtabDwords * 4 : 0;
+            // Residency cap (ecx_tune "occ_lds"): dummy LDS per workgroup.  Auto: the many-stream
+            // single-tile maps (>= 8 inputs, rings of <= 8 loads) at 4 waves per SIMD -- 4
+            // 256-thread or 16 one-wave workgroups per CU -- instead of the 5 their registers allow.
+            size_t occ = tu.occ_lds > 0 ? (size_t)tu.occ_lds : 0;
+            if (tu.occ_lds < 0 && !safe && a.n_tiles == 1 && cm.map().n_in >= 8 && depth <= 8)
+                occ = kLdsPerCu / (kOccWavesPerSimd * kSimdsPerCu / (threads / 64));
+            const size_t lds = (s.tlds ? (size_t)plan.max_tile_entries * kAtabDwords * 4 : 0) + occ;
             if (threads == 64) launch_shape_t<64>(s, grid, lds, stream, a);
             else launch_shape_t<kBlockThreads>(s, grid, lds, stream, a);
         }
