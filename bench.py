@@ -30,6 +30,8 @@ contract (same launch, timing and JSON line; the default is the headline):
            data block 2 from its local group, 2^15 resident stripes per GPU
   clay42x2 SURVEY 8(f) f4: Clay(4,2), 32 KiB, two-node repair of nodes {0, 3}
            (doDecodeMulti) over the headline's pool of 2^15 stripes
+  lrcenc   config 3's other half: LRC encode (4 XOR local parities of 3 blocks each, written in
+           place, LRCErasureCodeExample.kt:30-60), 64 KiB blocks, 2^15 resident stripes per GPU
   rs173    the reference's only published benchmark (rs/README.md:53): RS(17,3)
            encodeParity in place on 200,000-B shards, 4,096 resident stripes per GPU;
            value in its own convention, MB/s of input data (10^6 B,
@@ -67,6 +69,7 @@ WORKLOADS = {
     "lrc": ("GiB/s local-group repair (device-resident), LRC(12,4) 64 KiB blocks, 1/2/4/8 GPU", 1 << 15, 1 << 18),
     "clay42x2": ("GiB/s two-node repair-decode (device-resident), Clay(4,2) 32 KiB blocks, 1/2/4/8 GPU", 1 << 15,
                  1 << 18),
+    "lrcenc": ("GiB/s local-parity encode (device-resident), LRC(12,4) 64 KiB blocks, 1/2/4/8 GPU", 1 << 15, 1 << 18),
     "rs173": ("MB/s RS(17,3) encodeParity (device-resident), 200,000-B shards, input data bytes / 10^6 "
               "(ReedSolomonBenchmark convention), 1/2/4/8 GPU", 4096, 1 << 15),
 }
@@ -187,10 +190,11 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
     info = host_cpu_info()
     threads = info["cgroup_quota_cpus"] or info["omp_num_threads"] or info["affinity_cpus"]
     threads = max(1, min(threads, info["affinity_cpus"], 256))
-    # Working set: the bytes an operation touches (wl.unit_bytes), summed over every unit
-    # cycled through, >= 2x the machine's L3 (32 MiB assumed if unknown).
+    # Working set: the bytes an operation touches (the workload's algorithmic bytes per CPU
+    # unit), summed over every unit cycled through, >= 2x the machine's L3 (32 MiB assumed if unknown).
+    unit_bytes = spec.get("unit_bytes", wl.unit_bytes)
     l3 = info["l3_bytes_machine"] or (32 << 20)
-    n_units = max(2 * threads, -(-2 * l3 // wl.unit_bytes))
+    n_units = max(2 * threads, -(-2 * l3 // unit_bytes))
     if max_units:  # tests: a bounded arena
         threads = min(threads, max_units)
         n_units = max_units
@@ -213,7 +217,7 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
 
     def rate(th, secs):
         n, el = O.bench_run(op, data, parity, erased, slot_bytes, addrs, th, secs)
-        return n * wl.unit_bytes / el / 2**30, n, el
+        return n * unit_bytes / el / 2**30, n, el
 
     if protocol == "reference":
         runs = {}
@@ -234,7 +238,7 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
         timing = (f"{nn} operations on {threads} threads in {eln:.1f} s; single thread {n1} operations over all "
                   f"{n_units} units in {el1:.1f} s")
         measurements = None
-    ws = n_units * wl.unit_bytes
+    ws = n_units * unit_bytes
     out = {
         "value": round(allv, 3),
         "unit": "GiB/s",
@@ -651,6 +655,73 @@ class RS173(Workload):
                         "200,000-B shards"}
 
 
+class LRCEncode(Workload):
+    """Config 3, encode half (LRCErasureCodeExample.kt:30-60): each local group of 3 data
+    blocks gets its XOR parity (RS(3,1) encodeParity, parity row [1, 1, 1]), written in place
+    into the stripe's [d d d p] x 4 layout, 64 KiB blocks."""
+    b = 65536
+    reads, writes = 12, 4
+    unit_bytes = 16 * 65536
+    write_bytes = 4 * 65536
+    data_desc = "synthetic (device splitmix64 data blocks; the timed launch is the encode itself)"
+
+    def __init__(self, ecx, torch, dev, P, seed):
+        import numpy as np
+        b = self.b
+        self.P, self.torch = P, torch
+        self.pool = torch.empty((P, 16, b), dtype=torch.uint8, device=dev)
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
+        enc = np.zeros((4, 16), np.uint8)
+        for g in range(4):
+            enc[g, 4 * g:4 * g + 3] = 1
+        self.emap = ecx.GfMap.from_matrix(enc, in_slot=list(range(16)), out_slot=[3, 7, 11, 15])
+        self.region = self.pool
+        self.description = "LRC(12 data, 4 XOR local parities) encode in place, 64 KiB blocks"
+
+    def launch(self):
+        b = self.b
+        self.emap.apply_batch(self.pool, 16 * b, b, self.pool, 16 * b, b, self.P, b)
+
+    def verify(self):
+        """Re-encoding leaves every stripe unchanged, and two stripes' parities equal the oracle's."""
+        before = self.pool[:, 3::4].clone()
+        self.launch()
+        self.torch.cuda.synchronize()
+        same = bool(self.torch.equal(before, self.pool[:, 3::4]))
+        return same and all(self.oracle_check(self.pool[s].cpu().numpy(), self.pool[s, 3::4].cpu().numpy())
+                            for s in (0, self.P - 1))
+
+    def host_units(self, k):
+        # CPU units are local groups (3 data blocks + parity), as the reference encodes them
+        return [self.pool[i // 4, 4 * (i % 4):4 * (i % 4) + 4].cpu().numpy() for i in range(min(k, 4 * self.P))]
+
+    def sample(self):
+        s = self.P // 2
+        return self.pool[s].cpu().numpy(), self.pool[s, 3::4].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import numpy as np
+        import oracle as O
+        for g in range(4):
+            group = [stripe[4 * g + i].copy() for i in range(3)] + [np.zeros(self.b, np.uint8)]
+            O.ReedSolomon(3, 1).encode_parity(group, 0, self.b)
+            if not (group[3] == got[g]).all():
+                return False
+        return True
+
+    def cpu_spec(self):
+        import numpy as np
+        import oracle as O
+
+        def make(rng):  # one local group (3 data blocks + parity), random bytes
+            return [rng.integers(0, 256, (4, self.b), dtype=np.uint8) for _ in range(8)]
+        return {"op": O.BENCH_RS_ENCODE, "data": 3, "parity": 1, "erased": [], "make": make,
+                "arena_slot": np.arange(4), "present": np.ones(4, np.int64), "data_kind": "random-byte",
+                "unit_bytes": 4 * self.b,
+                "what": "LRC local-parity encodes: RS(3,1).encodeParity per local group (LRCErasureCodeExample.kt:30-60), "
+                        "64 KiB blocks"}
+
+
 class LRC(Workload):
     """Config 3: LRC (LRCErasureCodeExample shapes: 12 data blocks in 4 local groups of 3,
     each with an XOR parity), 64 KiB blocks; repair of data block 2 from its group."""
@@ -785,6 +856,8 @@ def main():
         wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed)
     elif args.workload == "rs173":
         wl = RS173(ecx, torch, dev, P, seed)
+    elif args.workload == "lrcenc":
+        wl = LRCEncode(ecx, torch, dev, P, seed)
     else:
         wl = LRC(ecx, torch, dev, P, seed)
 

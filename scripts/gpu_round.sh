@@ -35,7 +35,7 @@ if has gloo2; then
   rc=$?; echo "bench gloo2 rc=$rc"; tail -2 "$OUT/bench_gloo2.log"; [ $rc -ne 0 ] && stop gloo2 $rc
 fi
 if has workloads; then
-  for W in clay104 rs124 lrc clay42x2 rs173; do
+  for W in clay104 rs124 lrc clay42x2 rs173 lrcenc; do
     timeout -k 10 300 python bench.py --workload $W --steps 3 --warmup 1 > "$OUT/bench_$W.log" 2>&1
     rc=$?; echo "bench $W rc=$rc"; tail -1 "$OUT/bench_$W.log"; [ $rc -ne 0 ] && stop "bench $W" $rc
   done

@@ -13,11 +13,11 @@ OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-WORKLOADS="${*:-clay42 clay104 rs124 lrc clay42x2 rs173}"
+WORKLOADS="${*:-clay42 clay104 rs124 lrc clay42x2 rs173 lrcenc}"
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
 for W in $WORKLOADS; do
   case $W in
-    clay42|clay42x2) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; rs173) POOL=4096 ;; lrc) POOL=32768 ;;
+    clay42|clay42x2) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; rs173) POOL=4096 ;; lrcenc) POOL=32768 ;; lrc) POOL=32768 ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
   i=0

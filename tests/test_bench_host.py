@@ -98,7 +98,7 @@ def _bare(cls, **attrs):
     return wl
 
 
-@pytest.mark.parametrize("case", ["clay42", "clay42x2", "clay104", "rs124", "lrc", "rs173"])
+@pytest.mark.parametrize("case", ["clay42", "clay42x2", "clay104", "rs124", "lrc", "rs173", "lrcenc"])
 def test_cpu_baseline_every_workload(case):
     """Every bench workload has an oracle baseline (the reference path
     restated by oracle/, timed by oracle/orc_bench.c orc_bench_run), here on a bounded
@@ -113,6 +113,8 @@ def test_cpu_baseline_every_workload(case):
         wl = _bare(bench.RS124)
     elif case == "rs173":
         wl = _bare(bench.RS173)
+    elif case == "lrcenc":
+        wl = _bare(bench.LRCEncode)
     else:
         wl = _bare(bench.LRC)
     cpu = bench.cpu_baseline(wl, 0.2, None, max_units=2)
@@ -169,6 +171,13 @@ def test_oracle_checks_of_the_workloads():
     bad = stripe[17:20].copy()
     bad[2, 639] ^= 0x80
     assert not r17.oracle_check(stripe, bad)
+    # LRC encode: parity p_g = d_3g ^ d_3g+1 ^ d_3g+2 in slots 3, 7, 11, 15
+    le = _bare(bench.LRCEncode, b=256)
+    st = rng.integers(0, 256, (16, 256), dtype=np.uint8)
+    par = np.stack([st[4 * g] ^ st[4 * g + 1] ^ st[4 * g + 2] for g in range(4)])
+    assert le.oracle_check(st, par)
+    par[1, 0] ^= 4
+    assert not le.oracle_check(st, par)
 
 
 def test_published_metric_conversion():
