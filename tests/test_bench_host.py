@@ -188,3 +188,21 @@ def test_published_metric_conversion():
     assert wl.unit_bytes == 20 * 200000 and bench.PUBLISHED == {"rs173": 525.7}
     assert bench.WORKLOADS["rs173"][0].startswith("MB/s RS(17,3) encodeParity")
     assert all(getattr(bench, c).metric_unit == "GiB/s" for c in ("Clay42", "Clay104", "RS124", "LRC"))
+
+
+def test_round_scripts_cover_every_workload():
+    """scripts/pmc.sh (the PMC traffic behind roofline.traffic) and scripts/gpu_round.sh
+    (the per-workload bench lines) name every bench.py workload, and pmc.sh profiles each
+    at the pool size bench.py uses by default, so no workload's line loses its traffic."""
+    import re
+    pmc = (ROOT / "scripts" / "pmc.sh").read_text()
+    rnd = (ROOT / "scripts" / "gpu_round.sh").read_text()
+    default = re.search(r'WORKLOADS="\$\{\*:-([^}]*)\}"', pmc).group(1).split()
+    assert sorted(default) == sorted(bench.WORKLOADS)
+    loop = re.search(r"for W in ([a-z0-9 ]+); do", rnd).group(1).split()
+    assert sorted(loop + ["clay42"]) == sorted(bench.WORKLOADS)
+    pools = {}
+    for names, pool in re.findall(r"((?:[a-z0-9]+\|?)+)\) POOL=(\d+)", pmc):
+        for w in names.split("|"):
+            pools[w] = int(pool)
+    assert pools == {w: v[1] for w, v in bench.WORKLOADS.items()}
