@@ -88,6 +88,11 @@ int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *i
 
 /* ---------------------------------------------------------------- ReedSolomon.java */
 typedef struct ecx_rs ecx_rs;
+/* Codec objects: equal codecs (same k, m -- for Clay also virtual nodes and erased list)
+ * are one shared, reference-counted object, so per-file / per-repair creates reuse the
+ * compiled device plans.  Every create must be paired with one destroy; the last destroy
+ * parks the codec in a bounded cache of 64 idle codecs, and one evicted from it frees its
+ * device state.  Do not destroy a codec while batch work enqueued with it is in flight. */
 int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out); /* ReedSolomon.create :34-61 */
 void ecx_rs_destroy(ecx_rs *rs);
 int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out /* total x data */); /* buildMatrix :373-385 */
@@ -120,6 +125,11 @@ int ecx_map_create(const uint8_t *matrix /* n_out x n_in */, int n_out, int n_in
 void ecx_map_destroy(ecx_map *map);
 int ecx_map_info(const ecx_map *map, int *n_out, int *n_in, int *nnz);
 int ecx_map_matrix(const ecx_map *map, uint8_t *matrix /* n_out x n_in */, int *in_slot, int *out_slot);
+/* Largest input and output slot index the map reads / writes (-1 = none).  A batch over
+ * nstripes stripes of byte_count bytes touches (nstripes-1)*stripe_stride +
+ * max_slot*slot_stride + byte_count bytes of each buffer: the extent a binding checks
+ * against the caller's buffer (a Java ByteBuffer's capacity) before any device work. */
+int ecx_map_slot_extent(const ecx_map *map, int *max_in_slot, int *max_out_slot);
 int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                         uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                         int64_t byte_count, void *stream);
@@ -177,7 +187,7 @@ int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_e
  * results equal the reference Clay(12,4) run with the virtual nodes zero-filled. */
 int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
                               ecx_clay **out);
-void ecx_clay_destroy(ecx_clay *clay);
+void ecx_clay_destroy(ecx_clay *clay); /* drops one reference (see ecx_rs_create) */
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha); /* ClayCodeUtil :690-695 */
 int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out /* alpha */); /* :924-941 */
 /* The step's real node count n (= data + parity; virtual nodes excluded), its number of

@@ -33,6 +33,10 @@
  *                      SIMD, 1..65536 = that many bytes
  *   "chunk_major"      block order of the one-workgroup-per-tile kernel: 0 = stripe-major
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
+ *   "stagger"          unit order of the single-tile kernels (k_gf_apply, k_gf_apply_skew): 0 = none
+ *                      (default); G = 2..64: G stripes interleaved unit by unit, stripe j of a group
+ *                      starting at chunk j*C/G of its C chunks, so the streams in flight sit at G
+ *                      different shard offsets (scripts/addr_probe.hip)
  *   "block_threads"    one-workgroup-per-tile kernel: 256 threads over 4 KiB chunks or 64 threads
  *                      (one wave) over 1 KiB chunks; 0 = auto (default): one wave for single-tile
  *                      maps of <= 2 rows over >= 8 inputs on slot pitches that are not 4 MiB multiples
@@ -44,20 +48,18 @@
  *                      ecx_rs_encode_parity_single, ecx_rs_decode_missing_single): compiled plans
  *                      kept, by matrix content (default 256; 0 = compile every call)
  *   "skew_chunks"      single-tile maps: 2 / 4 = each workgroup takes that many 4 KiB chunks and
- *                      rotates the chunk each input is read at; 1 = auto (default): chosen per map
- *                      and input slot pitch (mod 16 MiB) by "skew_trial", else 4 when the pitch is
- *                      a multiple of 4 MiB and one chunk per workgroup otherwise; 0 = never
- *   "skew_trial"       single-tile maps with "skew_chunks" and "block_threads" on auto: 1 = on the first
- *                      large batch (>= 512 MiB of input) of a map at a new slot pitch, time three launch
- *                      shapes -- 256-thread workgroups over 4 KiB chunks, skewed chunks, one-wave
- *                      workgroups over 1 KiB chunks -- on up to 2 GiB of its own stripes (3 rounds each,
- *                      on the caller's stream; overwrite mode, no capture, outputs not aliasing inputs)
- *                      and keep the fastest for that (map, pitch mod 16 MiB); 0 = the static rules
- *                      (skew on 4 MiB-multiple pitches, one wave for <= 2-row maps over >= 8 inputs;
- *                      default: within 1.4 % of the best shape at every RS(12,4) pitch measured,
- *                      while the trial's sample misjudged one pitch by 11 %).
- *                      The sample is four windows spread over the batch, and a shape replaces the
- *                      static rules' choice only when it is >= 3 % faster
+ *                      rotates the chunk each input is read at; 1 = auto (default): per layout by the
+ *                      layout selection ("layout_select"), else 4 when the pitch is a multiple of 4 MiB
+ *                      and one chunk per workgroup otherwise; 0 = never
+ *   "layout_select"    single-tile maps over >= 8 inputs with <= 4 rows (the many-stream RS maps), with the
+ *                      knobs "skew_chunks", "block_threads" and "stagger" on auto, on batches of >= 256 MiB of
+ *                      input: 1 = the launch shape is chosen per batch layout (map, strides, byte and
+ *                      stripe count, device) by timing the caller's own first launches -- the static
+ *                      rules' shape, 4 KiB and one-wave workgroups, skewed chunks, staggered stripes,
+ *                      3 timings each, events read without blocking on later calls -- and the fastest
+ *                      median is kept (default; every candidate computes the same bytes, nothing extra
+ *                      is launched); 0 = the static rules only (skew on 4 MiB-multiple pitches, one
+ *                      wave for <= 2-row maps over >= 8 inputs)
  *   "wide_tiles"       multi-tile maps: pairs of 8-row tiles that share inputs in one workgroup
  *                      (16 accumulator rows, each shared input loaded once).  1 = when pairing
  *                      saves >= 1/6 of the input reads (default), 2 = always, 0 = never
@@ -158,10 +160,14 @@ int ecx_map_selftest(const struct ecx_map *map, uint64_t seed);
 /* Plan shape: row tiles, tile entries (= input loads of the one-workgroup-per-tile
  * kernel), tile groups, and the summed group unions (= input loads of the LDS kernel). */
 int ecx_map_plan_stats(const struct ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total);
-/* The launch shape "skew_trial" measured for `map` at input slot pitch `slot_pitch`:
- * 0 = 256-thread workgroups over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups
- * over 1 KiB chunks, -1 = not measured (yet). */
-int ecx_map_skew_choice(const struct ecx_map *map, int64_t slot_pitch);
+/* The launch shape "layout_select" kept for the most recently selected batch layout of
+ * `map` with input slot pitch `slot_pitch`: -1 = none chosen yet (still exploring, or not
+ * eligible); else the static rules' shape (-1 is never returned for that: see below) is
+ * reported as 0x100, and any other as shape + 8 * stagger, shape 0 = 256-thread workgroups
+ * over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB chunks.  With
+ * median_ms (n entries), the median launch time of each candidate in the selector's order
+ * (-1 = unsampled). */
+int ecx_map_layout_choice(const struct ecx_map *map, int64_t slot_pitch, float *median_ms, int n);
 /* The kernel instance of the last full-chunk launch this thread enqueued, named as
  * rocprofv3 names it (e.g. "k_gf_apply<false, true, 1, 20, false, 256, 8>"), copied
  * NUL-terminated into buf.  Returns its length (0 = no launch yet), or
@@ -184,6 +190,9 @@ int ecx_clay_rtc_source(struct ecx_clay *clay, char *buf, int len);
  * map does not fit the kernel (more than 16 rows), ECX_E_DEVICE if hiprtc fails. */
 int ecx_map_planes_compile_check(const struct ecx_map *map, int accumulate);
 int ecx_map_planes_source(const struct ecx_map *map, int accumulate, char *buf, int len);
+/* The process-wide codec registry (ecx.h, ecx_rs_create): codecs with live references and
+ * idle cached ones, for RS and Clay.  Any pointer may be NULL. */
+int ecx_codec_stats(int *rs_live, int *rs_idle, int *clay_live, int *clay_idle);
 #ifdef __cplusplus
 }
 #endif

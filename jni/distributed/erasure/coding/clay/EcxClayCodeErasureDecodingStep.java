@@ -85,11 +85,59 @@ public class EcxClayCodeErasureDecodingStep {
                 outSubStride, nstripes, bufSize, stream));
     }
 
-    /** The same from direct host ByteBuffers (pipelined over PCIe; synchronous). */
+    /**
+     * The same from direct host ByteBuffers (pipelined over PCIe; synchronous), addressed
+     * from each buffer's start.  Each buffer must hold (nstripes-1)*stripeStride +
+     * maxSlot*subStride + bufSize bytes, maxSlot being the highest sub-chunk slot the
+     * repair reads (inputs) or writes (outputs): a shorter buffer throws
+     * ArrayIndexOutOfBoundsException before anything is read, as the reference's
+     * ByteBuffer get/put would (ClayCoordinator.kt:378-390); a heap (non-direct) buffer
+     * throws NullPointerException.  The check is repeated natively from the buffers'
+     * capacities (EcxNative.clayPerformCodingBatchHostBuffer).
+     */
     public void performCodingBatchHost(ByteBuffer in, long inStripeStride, long inSubStride, ByteBuffer out,
                                        long outStripeStride, long outSubStride, long nstripes, long bufSize) {
-        Ecx.check(EcxNative.clayPerformCodingBatchHost(clay, EcxNative.directAddress(in), inStripeStride,
-                inSubStride, EcxNative.directAddress(out), outStripeStride, outSubStride, nstripes, bufSize));
+        if (nstripes < 0 || bufSize < 0 || inStripeStride < 0 || inSubStride < 0 || outStripeStride < 0
+                || outSubStride < 0) {
+            throw new IllegalArgumentException("negative batch count, size or stride");
+        }
+        if (numErased > 0 && nstripes > 0 && bufSize > 0) {
+            int[] slots = maxSlots();
+            checkExtent(in, "input", inStripeStride, inSubStride, slots[0], nstripes, bufSize);
+            checkExtent(out, "output", outStripeStride, outSubStride, slots[1], nstripes, bufSize);
+        }
+        Ecx.check(EcxNative.clayPerformCodingBatchHostBuffer(clay, in, inStripeStride, inSubStride, out,
+                outStripeStride, outSubStride, nstripes, bufSize));
+    }
+
+    /** Highest input and output sub-chunk slot of the repair (ecx_map_slot_extent). */
+    private int[] maxSlots() {
+        long[] m = new long[1];
+        Ecx.check(EcxNative.clayMap(clay, m));
+        int[] in = new int[1], out = new int[1];
+        Ecx.check(EcxNative.mapSlotExtent(m[0], in, out));
+        return new int[] {in[0], out[0]};
+    }
+
+    private static void checkExtent(ByteBuffer b, String what, long stripeStride, long subStride, int maxSlot,
+                                    long nstripes, long bufSize) {
+        if (b == null || !b.isDirect()) {
+            throw new NullPointerException(what + ": a direct ByteBuffer is required");
+        }
+        if (maxSlot < 0) {
+            return;
+        }
+        long need;
+        try {
+            need = Math.addExact(Math.addExact(Math.multiplyExact(nstripes - 1, stripeStride),
+                    Math.multiplyExact((long) maxSlot, subStride)), bufSize);
+        } catch (ArithmeticException e) {
+            throw new ArrayIndexOutOfBoundsException(what + ": batch extent overflows");
+        }
+        if (need > b.capacity()) {
+            throw new ArrayIndexOutOfBoundsException(what + ": the batch addresses " + need
+                    + " bytes but the buffer holds " + b.capacity());
+        }
     }
 
     public int numErased() {

@@ -60,6 +60,7 @@ NULLABLE = {("ecx_check_some_shards", "temp_buffer"), ("ecx_rs_is_parity_correct
             ("ecx_lrc_map", "block_present"), ("ecx_map_create", "in_slot"), ("ecx_map_create", "out_slot"),
             ("ecx_map_info", "n_out"), ("ecx_map_info", "n_in"), ("ecx_map_info", "nnz"),
             ("ecx_map_matrix", "matrix"), ("ecx_map_matrix", "in_slot"), ("ecx_map_matrix", "out_slot"),
+            ("ecx_map_slot_extent", "max_in_slot"), ("ecx_map_slot_extent", "max_out_slot"),
             ("ecx_clay_geometry", "q"), ("ecx_clay_geometry", "t"), ("ecx_clay_geometry", "alpha"),
             ("ecx_clay_shape", "nodes"), ("ecx_clay_shape", "n_erased"), ("ecx_clay_shape", "alpha"),
             ("ecx_rs_shape", "data_shards"), ("ecx_rs_shape", "parity_shards"),
@@ -129,6 +130,7 @@ RULES = {
     "ecx_map_info": ((), [A("n_out", "1"), A("n_in", "1"), A("nnz", "1")]),
     "ecx_map_matrix": (("map",), [A("matrix", "(int64_t)mp_out * mp_in"), A("in_slot", "mp_in"),
                                   A("out_slot", "mp_out")]),
+    "ecx_map_slot_extent": ((), [A("max_in_slot", "1"), A("max_out_slot", "1")]),
     "ecx_rs_decode_map": (("rs",), [A("shard_present", RS_N)]),
     "ecx_rs_decode_missing_batch": (("rs",), [A("shard_present", RS_N)]),
     "ecx_rs_decode_partial_batch": (("rs",), [A("shard_present", RS_N)]),
@@ -150,6 +152,64 @@ RULES = {
     "ecx_lrc_map": ((), [A("block_present", "16")]),
     "ecx_lrc_decode_batch": ((), [A("block_present", "16")]),
 }
+
+
+# Host-batch exports that also get a ByteBuffer forwarder, <camel>Buffer: the buffers are
+# direct ByteBuffers whose address AND capacity the forwarder reads itself, so the extent
+# check cannot be skipped from Java.  export -> (handle query, extent source, condition
+# under which the export touches the buffers at all).
+BUFFER_VARIANTS = {
+    "ecx_map_apply_batch_host": ("map", "    if (st == ECX_OK) st = ecx_map_slot_extent((const ecx_map *)(intptr_t)map, &max_in, &max_out);",
+                                 None),
+    # performCoding returns before its checks when nothing is erased (ClayCodeErasureDecodingStep.java:54-56)
+    "ecx_clay_perform_coding_batch_host": ("clay", "    if (st == ECX_OK && cl_ne > 0) {\n"
+                                           "        const ecx_map *cm = NULL;\n"
+                                           "        st = ecx_clay_map((ecx_clay *)(intptr_t)clay, &cm);\n"
+                                           "        if (st == ECX_OK) st = ecx_map_slot_extent(cm, &max_in, &max_out);\n"
+                                           "    }", "cl_ne > 0"),
+}
+
+
+def buffer_variant(ret, name, params):
+    """The <camel>Buffer forwarder of a host-batch export (BUFFER_VARIANTS)."""
+    query, extent, when = BUFFER_VARIANTS[name]
+    names = [p for _, p in params]
+    handle, length = names[0], names[-1]
+    jparams, cparams, args, bufs = [], ["JNIEnv *env", "jclass cls"], [], []
+    for i, (t, p) in enumerate(params):
+        kind = classify(name, t, p)[0]
+        if kind == "addr":
+            jparams.append("ByteBuffer %s" % camel("ecx_" + p))
+            cparams.append("jobject %s" % p)
+            bufs.append((p, names[i + 1], names[i + 2]))
+            args.append("(%s)%s_p" % (t.strip(), p))
+        elif kind == "handle":
+            jparams.append("long %s" % camel("ecx_" + p))
+            cparams.append("jlong %s" % p)
+            args.append("(%s)(intptr_t)%s" % (t.strip(), p))
+        else:
+            jparams.append("long %s" % camel("ecx_" + p))
+            cparams.append("jlong %s" % p)
+            args.append("(int64_t)%s" % p)
+    body = ["    (void)cls;", "    jint st = ECX_OK;", "    if (!%s) st = ECX_E_NULL;" % handle,
+            "    if (st == ECX_OK && (nstripes < 0 || %s < 0)) st = ECX_E_ILLEGAL_ARGUMENT;" % length,
+            QUERIES[query], "    int max_in = -1, max_out = -1;", extent]
+    for p, _, _ in bufs:
+        body.append("    uint8_t *%s_p = NULL;" % p)
+    cond = "st == ECX_OK" + (" && (%s)" % when if when else "")
+    for p, ss, sl in bufs:
+        body.append("    if (%s) st = direct_check(env, %s, %s, %s, %s, nstripes, %s, &%s_p);"
+                    % (cond, p, ss, sl, "max_in" if p == "in" else "max_out", length, p))
+    body.append("    if (st == ECX_OK) st = %s(%s);" % (name, ", ".join(args)))
+    body.append("    return st;")
+    jname = camel(name) + "Buffer"
+    c = ("\n/* %s over direct ByteBuffers, extent-checked from their capacity */\n"
+         "JNIEXPORT jint JNICALL Java_%s_%s(%s) {\n%s\n}\n"
+         % (name, JCLASS, jname, ", ".join(cparams), "\n".join(body)))
+    java = ("\n    /** %s over direct ByteBuffers: the forwarder checks each buffer's capacity against the\n"
+            "     *  batch extent (ecx_map_slot_extent) and refuses heap buffers (NullPointerException). */\n"
+            "    public static native int %s(%s);\n" % (name, jname, ", ".join(jparams)))
+    return c, java
 
 
 def exports():
@@ -306,6 +366,29 @@ static void buflist_free(JNIEnv *env, ecx_jni_buflist *b) {
 #define PIN(arr) ((arr) ? (*env)->GetPrimitiveArrayCritical(env, (arr), NULL) : NULL)
 #define UNPIN(arr, p, mode) do { if ((arr) && (p)) (*env)->ReleasePrimitiveArrayCritical(env, (arr), (p), (mode)); } while (0)
 
+/* A direct ByteBuffer a host-batch call reads or writes (nstripes-1)*stripe_stride +
+ * max_slot*slot_stride + nbytes bytes of, from its address (ecx_map_slot_extent): null or a
+ * heap buffer (no address, capacity -1) -> NullPointerException; negative strides ->
+ * IllegalArgumentException; shorter than that -> ArrayIndexOutOfBoundsException, as the
+ * reference's ByteBuffer get/put would throw (ClayCoordinator.kt:378-390). */
+static int direct_check(JNIEnv *env, jobject buf, int64_t stripe_stride, int64_t slot_stride, int max_slot,
+                        int64_t nstripes, int64_t nbytes, uint8_t **addr) {
+    *addr = NULL;
+    if (!buf) return ECX_E_NULL;
+    uint8_t *p = (uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (!p || cap < 0) return ECX_E_NULL;
+    *addr = p;
+    if (nstripes <= 0 || nbytes <= 0 || max_slot < 0) return ECX_OK;
+    if (stripe_stride < 0 || slot_stride < 0) return ECX_E_ILLEGAL_ARGUMENT;
+    int64_t a = 0, b = 0, need = 0;
+    if (__builtin_mul_overflow(nstripes - 1, stripe_stride, &a) ||
+        __builtin_mul_overflow((int64_t)max_slot, slot_stride, &b) || __builtin_add_overflow(a, b, &need) ||
+        __builtin_add_overflow(need, nbytes, &need))
+        return ECX_E_INDEX;
+    return need > (int64_t)cap ? ECX_E_INDEX : ECX_OK;
+}
+
 /* Address of a direct ByteBuffer (host-batch calls take addresses). */
 JNIEXPORT jlong JNICALL Java_%(J)s_directAddress(JNIEnv *env, jclass cls, jobject buffer) {
     (void)cls;
@@ -450,6 +533,10 @@ public final class EcxNative {
             body.append("    return st;")
         c.append("\n/* %s */\nJNIEXPORT %s JNICALL Java_%s_%s(%s) {\n%s\n}\n"
                  % (name, cret, JCLASS, jname, ", ".join(cparams), "\n".join(body)))
+        if name in BUFFER_VARIANTS:
+            bc, bj = buffer_variant(ret, name, params)
+            c.append(bc)
+            java.append(bj)
     java.append("}\n")
     return "".join(c), "".join(java)
 

@@ -433,13 +433,20 @@ class GfMap:
         check(f(self._h, *[ctypes.byref(x) for x in v]))
         return dict(zip(["tiles", "entries", "groups", "union_total"], [x.value for x in v]))
 
-    def skew_choice(self, slot_pitch: int) -> int:
-        """The launch shape measured for this map at an input slot pitch
-        (ecx_map_skew_choice, include/ecx_tune.h "skew_trial"): 0 256-thread workgroups
-        over 4 KiB chunks, 1 skewed chunks, 2 one-wave workgroups, -1 not measured."""
-        f = lib().ecx_map_skew_choice
-        f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_int64], ctypes.c_int
-        return f(self._h, int(slot_pitch))
+    def layout_choice(self, slot_pitch: int, with_times: bool = False):
+        """The launch shape "layout_select" kept for the latest selected batch layout of this
+        map at an input slot pitch (ecx_map_layout_choice, include/ecx_tune.h): -1 none yet,
+        0x100 the static rules' shape, else shape + 8 * stagger (shape 0 256-thread / 4 KiB
+        workgroups, 1 skewed chunks, 2 one-wave / 1 KiB workgroups).  with_times: also the
+        per-candidate median launch times (ms, -1 unsampled)."""
+        f = lib().ecx_map_layout_choice
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        f.restype = ctypes.c_int
+        ms = (ctypes.c_float * 8)()
+        c = f(self._h, int(slot_pitch), ms if with_times else None, 8 if with_times else 0)
+        if c < -1:
+            check(c)
+        return (c, [round(float(x), 4) for x in ms]) if with_times else c
 
     def _check(self, inp, iss, isl, out, oss, osl, nstripes, nbytes):
         mi, mo = self.max_slots()

@@ -99,6 +99,7 @@ SIGNATURES = {
     "ecx_map_destroy": (None, [P]),
     "ecx_map_info": (I, [P, PI, PI, PI]),
     "ecx_map_matrix": (I, [P, P, P, P]),
+    "ecx_map_slot_extent": (I, [P, PI, PI]),
     "ecx_map_apply_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
     "ecx_map_accumulate_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),

@@ -186,6 +186,34 @@ __device__ __forceinline__ uint32_t logical_block(int xcd_group, uint32_t n_tile
     return ((j / R) * 8 + xcd) * R + (j % R);
 }
 
+// (stripe, chunk) of logical unit u of a launch over nst stripes x nc chunks (a bijection
+// for every setting; a speed choice only):
+//   stagger G > 1: G stripes interleaved unit by unit, stripe j of each group starting at
+//                  chunk j*nc/G and wrapping, so the units in flight sit at G different
+//                  offsets of their shards instead of one (many-stream maps whose shard
+//                  pitch makes same-offset streams collide in HBM: scripts/addr_probe.hip);
+//                  stripes past the last whole group keep the stripe-major order;
+//   chunk_major:   chunk c of every stripe, then c + 1;
+//   otherwise      stripe-major, a stripe's chunks back to back.
+__device__ __forceinline__ void unit_of(uint32_t u, uint32_t nc, uint32_t nst, int chunk_major, uint32_t G,
+                                        int64_t &s, int64_t &c) {
+    if (G > 1) {
+        const uint32_t span = G * nc, full = (nst / G) * span;
+        if (u < full) {
+            const uint32_t grp = u / span, w = u % span, j = w % G, k = w / G;
+            s = (int64_t)grp * G + j;
+            c = (int64_t)((k + (uint32_t)((uint64_t)j * nc / G)) % nc);
+            return;
+        }
+    } else if (chunk_major) {
+        s = u % nst;
+        c = u / nst;
+        return;
+    }
+    s = u / nc;
+    c = u % nc;
+}
+
 // One output tile over the workgroup's (or wave's) lanes x 16 bytes of one stripe.
 // `ib` / `ob` point at this lane's 16 bytes of slot 0; `zoff` is this lane's offset
 // into the zero page (recomputed at each padding load rather than kept live).
@@ -303,11 +331,12 @@ __global__ void __launch_bounds__(THREADS, ROWS < kTileRows ? (DEPTH >= 12 ? 5 :
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles, (uint32_t)a.xcd_run);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
-    // chunk_major: consecutive units take the same chunk of consecutive stripes
-    // (a launch covers whole stripes, so gridDim.x / (n_tiles * n_chunks) is its stripe count).
+    // (a launch covers whole stripes, so gridDim.x / (n_tiles * n_chunks) is its stripe count)
     const uint32_t nst = gridDim.x / ((uint32_t)a.n_tiles * (uint32_t)a.n_chunks);
-    const int64_t c = a.chunk_begin + (int64_t)(a.chunk_major ? rest / nst : rest % (uint32_t)a.n_chunks);
-    const int64_t s = a.stripe_begin + (int64_t)(a.chunk_major ? rest % nst : rest / (uint32_t)a.n_chunks);
+    int64_t s, c;
+    unit_of(rest, (uint32_t)a.n_chunks, nst, a.chunk_major, (uint32_t)a.stagger, s, c);
+    s += a.stripe_begin;
+    c += a.chunk_begin;
     const int64_t cbase = c * (THREADS * 16);
     int valid = 16;
     if (SAFE) {

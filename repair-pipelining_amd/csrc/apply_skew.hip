@@ -19,9 +19,10 @@ namespace ecx {
 template <bool NTL, int DEPTH, int ROWS, int K>
 __global__ void __launch_bounds__(kBlockThreads, ROWS * K <= 8 ? 5 : 4) k_gf_apply_skew(ApplyArgs a) {
     static_assert(DEPTH % K == 0, "the ring must hold whole rotations");
-    const uint32_t rest = blockIdx.x;
-    const int64_t g = a.chunk_begin + (int64_t)(rest % (uint32_t)a.n_chunks);  // chunk group
-    const int64_t s = a.stripe_begin + (int64_t)(rest / (uint32_t)a.n_chunks);
+    int64_t s, g;  // stripe, chunk group
+    unit_of(blockIdx.x, (uint32_t)a.n_chunks, gridDim.x / (uint32_t)a.n_chunks, 0, (uint32_t)a.stagger, s, g);
+    s += a.stripe_begin;
+    g += a.chunk_begin;
     const int64_t cbase = g * (int64_t)(K * kChunkBytes);
     const uint32_t lane16 = threadIdx.x * 16;
     cu32 *tile = plan_ptr(a.tiles);

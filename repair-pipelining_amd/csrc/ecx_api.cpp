@@ -1,5 +1,6 @@
 // ecx_api.cpp -- the C ABI (include/ecx.h).  Translates planner/HIP errors into
 // ecx_status codes; every arithmetic entry point executes on the HIP device.
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -206,18 +207,92 @@ ecx_map *clay_standard_map(ecx_clay *c) {
 }  // namespace
 
 namespace {
+// Process-wide codec registry: equal codecs are one reference-counted object.
+// ecx_*_create takes a reference, ecx_*_destroy drops it.  A codec nobody references
+// stays registered, idle, so that the next create of the same codec (the reference builds
+// one per file or repair) finds its compiled plans and generated kernels; at most
+// kCodecIdleMax idle codecs are kept, least recently released first out, and an evicted
+// codec frees its device state.  Past kCodecRegistryMax registered codecs, creates return
+// private objects that destroy frees at once.
 constexpr size_t kCodecRegistryMax = 4096;
-template <typename T, typename Key, typename Make>
-T *registry_get(const Key &key, Make make) {
-    static std::mutex mu;
-    static std::map<Key, std::unique_ptr<T>> reg;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = reg.find(key);
-    if (it != reg.end()) return it->second.get();
-    std::unique_ptr<T> obj(make());  // may throw (invalid geometry): nothing registered
-    if (reg.size() >= kCodecRegistryMax) return obj.release();
-    obj->shared = true;
-    return reg.emplace(key, std::move(obj)).first->second.get();
+constexpr size_t kCodecIdleMax = 64;
+
+template <typename T, typename Key>
+struct Registry {
+    std::mutex mu;
+    std::map<Key, std::unique_ptr<T>> reg;
+    std::map<const T *, Key> key_of;
+    std::list<const T *> idle;  // front = most recently released
+    std::map<const T *, typename std::list<const T *>::iterator> idle_pos;
+    std::map<const T *, int> refs;
+
+    template <typename Make>
+    T *get(const Key &key, Make make) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = reg.find(key);
+        if (it != reg.end()) {
+            T *obj = it->second.get();
+            auto ip = idle_pos.find(obj);
+            if (ip != idle_pos.end()) {
+                idle.erase(ip->second);
+                idle_pos.erase(ip);
+            }
+            ++refs[obj];
+            return obj;
+        }
+        std::unique_ptr<T> obj(make());  // may throw (invalid geometry): nothing registered
+        if (reg.size() >= kCodecRegistryMax) return obj.release();
+        obj->shared = true;
+        T *p = obj.get();
+        reg.emplace(key, std::move(obj));
+        key_of.emplace(p, key);
+        refs[p] = 1;
+        return p;
+    }
+
+    // Drops one reference; frees a private object, parks a shared one as idle.
+    void release(T *obj) {
+        if (!obj) return;
+        if (!obj->shared) {
+            delete obj;
+            return;
+        }
+        std::vector<std::unique_ptr<T>> evicted;  // destroyed outside the lock (hipFree syncs)
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto r = refs.find(obj);
+            if (r == refs.end() || r->second <= 0) return;  // not a live reference: ignore
+            if (--r->second > 0) return;
+            idle.push_front(obj);
+            idle_pos[obj] = idle.begin();
+            while (idle.size() > kCodecIdleMax) {
+                const T *victim = idle.back();
+                idle.pop_back();
+                idle_pos.erase(victim);
+                refs.erase(victim);
+                auto k = key_of.find(victim);
+                auto e = reg.find(k->second);
+                evicted.push_back(std::move(e->second));
+                reg.erase(e);
+                key_of.erase(k);
+            }
+        }
+    }
+
+    void stats(int *live, int *idle_n) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (live) *live = (int)(reg.size() - idle.size());
+        if (idle_n) *idle_n = (int)idle.size();
+    }
+};
+
+Registry<ecx_rs, std::pair<int, int>> &rs_registry() {
+    static Registry<ecx_rs, std::pair<int, int>> r;
+    return r;
+}
+Registry<ecx_clay, std::tuple<int, int, int, std::vector<int>>> &clay_registry() {
+    static Registry<ecx_clay, std::tuple<int, int, int, std::vector<int>>> r;
+    return r;
 }
 }  // namespace
 
@@ -370,21 +445,18 @@ int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *i
 // so equal codecs are one object: the reference builds a ReedSolomon (or a Clay decoding
 // step) per file or repair (SampleEncoder.java:83, ClayCode.java:43-51), and sharing keeps
 // the compiled, device-resident plans -- and the hiprtc-compiled Clay kernels -- of every
-// earlier call instead of rebuilding them per object.  The registry holds up to
-// kCodecRegistryMax codecs for the process lifetime; past that, creates return private
-// objects that ecx_*_destroy frees.
+// earlier call instead of rebuilding them per object.  Shared codecs are reference-
+// counted; up to kCodecIdleMax unreferenced ones stay cached (Registry above).
 int ecx_rs_create(int data_shards, int parity_shards, ecx_rs **out) {
     return guarded(__func__, [&]() -> int {
         *out = nullptr;
-        *out = registry_get<ecx_rs>(std::make_pair(data_shards, parity_shards),
-                                    [&] { return new ecx_rs(data_shards, parity_shards); });
+        *out = rs_registry().get(std::make_pair(data_shards, parity_shards),
+                                 [&] { return new ecx_rs(data_shards, parity_shards); });
         return ECX_OK;
     });
 }
 
-void ecx_rs_destroy(ecx_rs *rs) {
-    if (rs && !rs->shared) delete rs;
-}
+void ecx_rs_destroy(ecx_rs *rs) { rs_registry().release(rs); }
 
 int ecx_rs_matrix(const ecx_rs *rs, uint8_t *out) {
     const Matrix &m = rs->code.matrix();
@@ -597,6 +669,19 @@ int ecx_map_matrix(const ecx_map *map, uint8_t *matrix, int *in_slot, int *out_s
     return ECX_OK;
 }
 
+int ecx_map_slot_extent(const ecx_map *map, int *max_in_slot, int *max_out_slot) {
+    return guarded(__func__, [&]() -> int {
+        if (!map) throw Error(ECX_E_NULL, "null map");
+        const LinearMap &m = map->cm.map();
+        int mi = -1, mo = -1;
+        for (int s : m.in_slot) mi = std::max(mi, s);
+        for (int s : m.out_slot) mo = std::max(mo, s);
+        if (max_in_slot) *max_in_slot = mi;
+        if (max_out_slot) *max_out_slot = mo;
+        return ECX_OK;
+    });
+}
+
 int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                         uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                         int64_t byte_count, void *stream) {
@@ -708,14 +793,18 @@ int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_unit
         *out = nullptr;
         if (n_erased < 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased / virtual_units");
         const std::vector<int> e(erased, erased + n_erased);  // order matters (the reference's erasedIndexes)
-        *out = registry_get<ecx_clay>(std::make_tuple(data_units, parity_units, virtual_units, e),
-                                      [&] { return new ecx_clay(data_units, parity_units, e, virtual_units); });
+        *out = clay_registry().get(std::make_tuple(data_units, parity_units, virtual_units, e),
+                                   [&] { return new ecx_clay(data_units, parity_units, e, virtual_units); });
         return ECX_OK;
     });
 }
 
-void ecx_clay_destroy(ecx_clay *clay) {
-    if (clay && !clay->shared) delete clay;
+void ecx_clay_destroy(ecx_clay *clay) { clay_registry().release(clay); }
+
+int ecx_codec_stats(int *rs_live, int *rs_idle, int *clay_live, int *clay_idle) {
+    rs_registry().stats(rs_live, rs_idle);
+    clay_registry().stats(clay_live, clay_idle);
+    return ECX_OK;
 }
 
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha) {
@@ -1049,6 +1138,10 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         t.occ_lds = value;
     }
     else if (k == "chunk_major") t.chunk_major = value != 0;
+    else if (k == "stagger") {
+        if (value < 0 || value > 64) return ECX_E_ILLEGAL_ARGUMENT;
+        t.stagger = value;
+    }
     else if (k == "small_tiles") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.small_tiles = value;
@@ -1062,9 +1155,9 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         if (value < 0 || value > 4 || value == 3) return ECX_E_ILLEGAL_ARGUMENT;
         t.skew_chunks = value;
     }
-    else if (k == "skew_trial") {
+    else if (k == "layout_select") {
         if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
-        t.skew_trial = value;
+        t.layout_select = value;
     }
     else if (k == "wide_tiles") {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
@@ -1189,9 +1282,15 @@ int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_
     });
 }
 
-int ecx_map_skew_choice(const ecx_map *map, int64_t slot_pitch) {
-    if (!map || slot_pitch <= 0) return ECX_E_ILLEGAL_ARGUMENT;
-    return const_cast<ecx_map *>(map)->cm.skew_choice(slot_pitch % ((int64_t)16 << 20));
+int ecx_map_layout_choice(const ecx_map *map, int64_t slot_pitch, float *median_ms, int n) {
+    if (!map || slot_pitch <= 0 || n < 0) return ECX_E_ILLEGAL_ARGUMENT;
+    std::vector<float> ms;
+    const int c = const_cast<ecx_map *>(map)->cm.layout_choice(slot_pitch, median_ms ? &ms : nullptr);
+    if (median_ms)
+        for (int i = 0; i < n; ++i) median_ms[i] = i < (int)ms.size() ? ms[i] : -1.f;
+    if (c < 0) return -1;
+    const int code = layout_candidate_code(c);
+    return code == -1 ? 0x100 : code;  // 0x100 = the static rules' shape
 }
 
 int ecx_last_kernel(char *buf, int len) {

@@ -401,6 +401,11 @@ const uint8_t *zero_page_for_current_device() {
 }
 
 CompiledMap::~CompiledMap() {
+    for (auto &kv : layout_sel_)
+        for (auto &p : kv.second.pending) {
+            (void)hipEventDestroy(p.e0);
+            (void)hipEventDestroy(p.e1);
+        }
     for (auto &kv : dev_) {
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) continue;
@@ -660,15 +665,83 @@ MapPlanes *CompiledMap::planes() {
     return planes_.get();
 }
 
-int CompiledMap::skew_choice(int64_t pitch_key) {
+namespace {
+constexpr float kLayoutMargin = 0.98f;  // another shape replaces the static rules' only if 2 % faster
+
+float median_of(std::vector<float> v) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? -1.f : v[v.size() / 2];
+}
+}  // namespace
+
+int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, bool *time) {
     std::lock_guard<std::mutex> lk(mu_);
-    auto it = skew_choice_.find(pitch_key);
-    return it == skew_choice_.end() ? -1 : it->second;
+    LayoutSel &s = layout_sel_[key];
+    if ((int)s.ms.size() != n_cand) s.ms.assign(n_cand, {});
+    *time = false;
+    if (s.chosen >= 0) return s.chosen;
+    for (auto it = s.pending.begin(); it != s.pending.end();) {
+        const hipError_t q = hipEventQuery(it->e1);
+        if (q == hipErrorNotReady) {
+            ++it;
+            continue;
+        }
+        float ms = 0.f;
+        if (q == hipSuccess && hipEventElapsedTime(&ms, it->e0, it->e1) == hipSuccess && ms > 0.f)
+            s.ms[it->cand].push_back(ms);
+        else
+            (void)hipGetLastError();  // a failed probe is dropped; its candidate is timed again
+        (void)hipEventDestroy(it->e0);
+        (void)hipEventDestroy(it->e1);
+        it = s.pending.erase(it);
+    }
+    std::vector<int> queued(n_cand, 0);
+    bool done = true;
+    for (int c = 0; c < n_cand; ++c) {
+        queued[c] = (int)s.ms[c].size();
+        done = done && queued[c] >= samples;
+    }
+    if (done) {
+        const float base = median_of(s.ms[0]);
+        int best = 0;
+        float best_ms = base;
+        for (int c = 1; c < n_cand; ++c) {
+            const float m = median_of(s.ms[c]);
+            if (m < best_ms && m < kLayoutMargin * base) {
+                best = c;
+                best_ms = m;
+            }
+        }
+        s.chosen = best;
+        s.serial = ++layout_serial_;
+        return best;
+    }
+    for (const auto &p : s.pending) ++queued[p.cand];
+    int c = 0;
+    for (int k = 1; k < n_cand; ++k)
+        if (queued[k] < queued[c]) c = k;
+    if (queued[c] >= samples) return 0;  // every probe is in flight: the static rules, untimed
+    *time = true;
+    return c;
 }
 
-void CompiledMap::set_skew_choice(int64_t pitch_key, int choice) {
+void CompiledMap::add_layout_probe(const std::array<int64_t, 8> &key, int cand, hipEvent_t e0, hipEvent_t e1) {
     std::lock_guard<std::mutex> lk(mu_);
-    skew_choice_[pitch_key] = choice;
+    layout_sel_[key].pending.push_back({cand, e0, e1});
+}
+
+int CompiledMap::layout_choice(int64_t pitch, std::vector<float> *ms) {
+    std::lock_guard<std::mutex> lk(mu_);
+    const LayoutSel *latest = nullptr;
+    for (const auto &kv : layout_sel_)
+        if (kv.first[0] == pitch && kv.second.chosen >= 0 && (!latest || kv.second.serial > latest->serial))
+            latest = &kv.second;
+    if (!latest) return -1;
+    if (ms) {
+        ms->clear();
+        for (const auto &v : latest->ms) ms->push_back(median_of(v));
+    }
+    return latest->chosen;
 }
 
 const std::vector<int> &CompiledMap::used_in_slots() {

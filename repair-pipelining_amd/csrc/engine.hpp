@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -146,13 +147,33 @@ public:
     MapPlanes *planes();
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
-    // The launch shape skew_trial measured for an input slot pitch key: -1 = not measured
-    // yet, 0 = 256-thread / 4 KiB workgroups, 1 = skewed chunks, 2 = one-wave / 1 KiB workgroups.
-    int skew_choice(int64_t pitch_key);
-    void set_skew_choice(int64_t pitch_key, int choice);
+    // Per-layout launch-shape selection (kernels.hip launch_apply, ecx_tune "layout_select"):
+    // the candidate to run for this call of the batch layout `key`.  Finished timing probes
+    // are harvested first (non-blocking); once every one of the n_cand candidates has
+    // `samples` timings the fastest median is kept (candidate 0 -- the static rules --
+    // unless another is faster by kLayoutMargin).  While exploring, the least-sampled
+    // candidate is returned with *time set: the caller brackets that launch with two
+    // events on its stream and hands them to add_layout_probe.
+    int next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, bool *time);
+    void add_layout_probe(const std::array<int64_t, 8> &key, int cand, hipEvent_t e0, hipEvent_t e1);
+    // The candidate kept for the most recently selected layout with input slot pitch
+    // `pitch`, -1 if none yet; with `ms`, the per-candidate median launch times (ms, -1 =
+    // unsampled) of that layout.
+    int layout_choice(int64_t pitch, std::vector<float> *ms = nullptr);
 
 private:
-    std::map<int64_t, int> skew_choice_;
+    struct LayoutSel {
+        struct Probe {
+            int cand;
+            hipEvent_t e0, e1;
+        };
+        std::vector<std::vector<float>> ms;  // per candidate: launch times of its probes
+        std::vector<Probe> pending;          // probes whose end event has not completed yet
+        int chosen = -1;
+        uint64_t serial = 0;                 // order of the choices (layout_choice reports the latest)
+    };
+    std::map<std::array<int64_t, 8>, LayoutSel> layout_sel_;
+    uint64_t layout_serial_ = 0;
     LinearMap map_;
     std::unique_ptr<CompiledMap> compact_;
     std::unique_ptr<MapPlanes> planes_;
@@ -190,6 +211,7 @@ struct ApplyArgs {
     int accumulate;       // 1: out ^= M * in (partial sums along a repair chain), 0: out = M * in
     int lane_zero;        // always 0 (keeps k_gf_apply's LDS table base in a VGPR)
     int chunk_major;      // k_gf_apply block order: 0 = stripe by stripe, 1 = chunk c of every stripe, then c + 1
+    int stagger;          // k_gf_apply / _skew unit order: > 1 = groups of that many stripes interleaved (unit_of)
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -220,6 +242,9 @@ struct Tuning {
     int occ_lds = 0;
     // k_gf_apply block order: 0 = stripe-major (a stripe's chunks back to back), 1 = chunk-major.
     int chunk_major = 0;
+    // k_gf_apply / k_gf_apply_skew unit order: 0 / 1 = none; G >= 2 = G stripes interleaved,
+    // each starting at a different chunk offset (apply.hpp unit_of).
+    int stagger = 0;
     // k_gf_apply workgroup: 256 threads over 4 KiB chunks (default) or 64 threads (one
     // wave) over 1 KiB chunks.
     int block_threads = 0;  // 0 = auto (launch_apply), 256 or 64 forced
@@ -237,11 +262,10 @@ struct Tuning {
     // workgroup, each entry's chunk rotated; 1 = 4 when the input slot pitch is a
     // multiple of 4 MiB; 0 = off.
     int skew_chunks = 1;
-    // skew_chunks / block_threads auto: 1 = measure the three launch shapes on the first large
-    // batch per (map, input slot pitch mod 16 MiB) and keep the fastest; 0 = the static rules
-    // (default: within 1.4 % of the best shape at every pitch measured, while the trial's
-    // sample misjudged the 1 MiB + 4 KiB pitch by 11 %, profiles/r03_shape_trial_check.jsonl)
-    int skew_trial = 0;
+    // Many-stream single-tile maps (>= 8 inputs, <= 4 rows) with the shape knobs on auto: 1 =
+    // the launch shape chosen per batch layout by timing the caller's own first launches
+    // (kernels.hip launch_apply; default), 0 = the static rules only.
+    int layout_select = 1;
     // Per-call CodingLoop entry points: compiled plans kept, by map content (0 = none).
     int plan_cache = 256;
     // Bit-sliced kernel (k_gf_bits): 2 = for every map it can run (aligned layout, 32-bit
@@ -314,6 +338,10 @@ void note_kernel(const char *name, P... params) {
 }
 
 // Enqueue out = M * in over nstripes stripes (kernels.hip).
+// The launch_apply_core pick of per-layout candidate `cand` (kernels.hip kLayoutCand):
+// -1 = the static rules, else shape (0 = 256-thread / 4 KiB, 1 = skewed chunks, 2 = one-wave
+// / 1 KiB) + 8 * stagger; -2 for an index out of range.
+int layout_candidate_code(int cand);
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate = false);

@@ -238,8 +238,9 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
 
 namespace {
 // pick: -1 = the static rules (skew on 4 MiB-multiple input slot pitches, one-wave
-// workgroups for narrow maps otherwise); 0 = 256-thread workgroups over 4 KiB chunks,
-// 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB chunks (the shape trial's candidates)
+// workgroups for narrow maps otherwise); else shape + 8 * stagger with shape 0 = 256-thread
+// workgroups over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB
+// chunks, and stagger the unit order (apply.hpp unit_of) -- the per-layout candidates
 void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                        uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                        int64_t nbytes, hipStream_t stream, bool accumulate, int pick) {
@@ -257,10 +258,11 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     // profiles/r02_block_threads.jsonl).  3-row maps (RS(17,3) encode) run on 4 KiB
     // workgroups: 0-4 % faster than one wave once the byte-safe tail took 16-B accesses
     // (profiles/r03_rs_km.jsonl, r03_rs173_pitch.jsonl, r03_rs173_ab.jsonl).
-    const bool skew_pitch = pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4 : pick == 1;
+    const int shape = pick < 0 ? -1 : pick & 7;
+    const bool skew_pitch = pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4 : shape == 1;
     const bool one_wave = tu.block_threads == 64 ||
                           (tu.block_threads == 0 && cm.n_tiles() == 1 && tu.bitslice != 2 && !tu.lds_lut &&
-                           (pick < 0 ? cm.max_tile_rows() <= 2 && cm.map().n_in >= 8 && !skew_pitch : pick == 2));
+                           (pick < 0 ? cm.max_tile_rows() <= 2 && cm.map().n_in >= 8 && !skew_pitch : shape == 2));
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     // Small-row kernel variants: forced (1), or auto (2) for maps of <= 2 rows over <= 4
@@ -383,6 +385,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     a.n_wide = cm.n_wide_tiles();
     a.lane_zero = 0;
     a.chunk_major = tu.chunk_major;
+    a.stagger = pick < 0 ? tu.stagger : pick >> 3;
     a.n_groups = cm.n_groups();
     a.zero_page = zero_page_for_current_device();
     a.in_stripe_stride = in_stripe_stride;
@@ -502,17 +505,27 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 }
 }  // namespace
 
-// The slot pitch decides whether rotating the chunk order pays (k_gf_apply_skew) or one-wave
-// workgroups do, and no simple rule predicts it beyond "4 MiB multiples gain" (DESIGN.md 4,
-// pitch sweep; RS(12,4) decode gains 2-3 % from one wave at 4 MiB + 4 KiB, 10-17 % from skew at 4 MiB).
-// So on the first large batch (>= 512 MiB of input) of a single-tile map at a new pitch (mod
-// 16 MiB), the three launch shapes run on a sample of up to 2 GiB of the batch's own
-// stripes, three rounds each on the caller's stream, and the fastest is kept for that (map,
-// pitch).  The trial writes the same outputs the real launch then rewrites, so it is only
-// done where that is harmless: overwrite mode, outputs not aliasing inputs, no stream capture.
-constexpr int64_t kSkewTrialMinBytes = (int64_t)512 << 20;     // batches this large (input bytes) run the trial
-constexpr int64_t kSkewTrialSampleBytes = (int64_t)2 << 30;    // input bytes per trial shape and round
-constexpr float kTrialMargin = 0.97f;                          // a shape must be 3 % faster than the static rules' choice
+// Launch shape per batch layout, measured on the caller's own launches.  The many-stream
+// single-tile maps (RS decode / encode: >= 8 input streams, <= 4 rows) move 0.63-0.79 of
+// HBM depending only on where their streams sit: same-offset streams whose addresses differ
+// in the bits the HBM interleave does not spread (a 4 MiB shard pitch, or 1 MiB + 4 KiB,
+// whose stripes collide) queue on one bank (scripts/addr_probe.hip), and
+// no static rule predicts which shape -- 4 KiB or one-wave workgroups, skewed chunks,
+// staggered stripes -- is fastest at a given pitch (scripts/layout_sweep.py).  So for a
+// new layout (map, strides, byte count, stripe count, device) the first calls run the
+// candidates in turn, each launch bracketed by two events on the caller's stream; the
+// events are read without blocking on later calls, and once every candidate has
+// kLayoutSamples timings the fastest median is kept for that layout.  Every candidate
+// computes the same bytes, and nothing is launched that the caller did not ask for: the
+// exploration costs only the slower candidates' launches.  Batches under kLayoutMinBytes of
+// input, streams being captured and forced shapes use the static rules.
+constexpr int64_t kLayoutMinBytes = (int64_t)256 << 20;
+constexpr int kLayoutSamples = 3;
+// candidate 0 = the static rules, then shape + 8 * stagger (launch_apply_core's pick)
+constexpr int kLayoutCand[] = {-1, 0, 1, 2, 2 + 8 * 2, 2 + 8 * 8, 0 + 8 * 4};
+constexpr int kLayoutNCand = (int)(sizeof(kLayoutCand) / sizeof(kLayoutCand[0]));
+
+int layout_candidate_code(int cand) { return cand >= 0 && cand < kLayoutNCand ? kLayoutCand[cand] : -2; }
 
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
@@ -522,76 +535,59 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const bool aligned = aligned16(in) && aligned16(out) && (in_stripe_stride % 16 == 0) &&
                          (in_slot_stride % 16 == 0) && (out_stripe_stride % 16 == 0) && (out_slot_stride % 16 == 0);
     const int64_t in_bytes = (int64_t)m.n_in * nbytes;  // per stripe
-    bool trial = tu.skew_chunks == 1 && tu.skew_trial && tu.block_threads == 0 && !accumulate && !tu.lds_lut &&
-                 tu.bitslice != 2 && tu.nontemporal != 0 && tu.store_scope == 0 && cm.n_tiles() == 1 &&
-                 m.n_in >= 4 && m.n_out > 0 && aligned && in_slot_stride > 0 && nbytes >= 4 * kChunkBytes &&
-                 nstripes * in_bytes >= kSkewTrialMinBytes;
-    const int64_t key = trial ? in_slot_stride % ((int64_t)16 << 20) : 0;
-    int pick = trial ? cm.skew_choice(key) : -1;
-    if (trial && pick < 0) {
-        // outputs must not alias inputs: disjoint byte ranges, or the same layout with
-        // disjoint slot sets (in-place decodeMissing)
-        const int64_t in_end = (nstripes - 1) * in_stripe_stride + (int64_t)cm.max_in_slot() * in_slot_stride + nbytes;
-        const int64_t out_end =
-            (nstripes - 1) * out_stripe_stride + (int64_t)cm.max_out_slot() * out_slot_stride + nbytes;
-        const bool disjoint = out + out_end <= in || in + in_end <= out;
-        bool same_layout_ok = in == out && in_stripe_stride == out_stripe_stride && in_slot_stride == out_slot_stride;
-        if (same_layout_ok)
-            for (int o : m.out_slot)
-                for (int j : m.in_slot) same_layout_ok = same_layout_ok && o != j;
+    bool select = tu.layout_select && tu.skew_chunks == 1 && tu.block_threads == 0 && tu.stagger == 0 &&
+                  !tu.lds_lut && tu.bitslice != 2 && tu.nontemporal == 1 && tu.store_scope == 0 &&
+                  cm.n_tiles() == 1 && m.n_in >= 8 && cm.max_tile_rows() <= 4 && aligned && in_slot_stride > 0 &&
+                  nbytes >= 4 * kChunkBytes && nstripes * in_bytes >= kLayoutMinBytes;
+    if (select) {
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(stream, &cap) != hipSuccess) {
             (void)hipGetLastError();
-            cap = hipStreamCaptureStatusActive;  // unknown: do not run the trial
+            cap = hipStreamCaptureStatusActive;  // unknown: no events
         }
-        if ((disjoint || same_layout_ok) && cap == hipStreamCaptureStatusNone) {
-            // A sample big enough to behave like the batch (a few stripes time the launch
-            // tail, not the access pattern: a 5-stripe trial picked the slower kernel for
-            // RS(12,4) at the padded pitch), taken as kWindows windows spread over the batch's
-            // address span (a 2 GiB prefix misjudged the 1 MiB + 4 KiB pitch, where the shape
-            // that won on the prefix was 10 % slower on the whole batch).
-            constexpr int kWindows = 4;
-            const int64_t sample = std::min<int64_t>(nstripes, std::max<int64_t>(1, kSkewTrialSampleBytes / in_bytes));
-            const int64_t win = std::max<int64_t>(1, sample / kWindows);
-            int64_t win_begin[kWindows];
-            for (int w = 0; w < kWindows; ++w) win_begin[w] = std::min(nstripes - win, (nstripes / kWindows) * w);
-            constexpr int kCand = 3, kRounds = 3;  // 4 KiB workgroups, skewed chunks, one-wave workgroups
-            hipEvent_t ev[kCand * kRounds + 1];
-            for (auto &e : ev) check_hip(hipEventCreate(&e), "hipEventCreate");
-            float best[kCand] = {1e30f, 1e30f, 1e30f};
-            try {
-                check_hip(hipEventRecord(ev[0], stream), "hipEventRecord");
-                for (int r = 0; r < kRounds; ++r)
-                    for (int v = 0; v < kCand; ++v) {
-                        for (int w = 0; w < kWindows; ++w)
-                            launch_apply_core(cm, in + win_begin[w] * in_stripe_stride, in_stripe_stride,
-                                              in_slot_stride, out + win_begin[w] * out_stripe_stride, out_stripe_stride,
-                                              out_slot_stride, win, nbytes, stream, false, v);
-                        check_hip(hipEventRecord(ev[1 + kCand * r + v], stream), "hipEventRecord");
-                    }
-                check_hip(hipEventSynchronize(ev[kCand * kRounds]), "hipEventSynchronize");
-                for (int i = 1; i <= kCand * kRounds; ++i) {
-                    float ms = 0.f;
-                    check_hip(hipEventElapsedTime(&ms, ev[i - 1], ev[i]), "hipEventElapsedTime");
-                    best[(i - 1) % kCand] = std::min(best[(i - 1) % kCand], ms);
-                }
-            } catch (...) {
-                for (auto &e : ev) (void)hipEventDestroy(e);
-                throw;
-            }
-            for (auto &e : ev) (void)hipEventDestroy(e);
-            // Run-to-run noise is a few %: another shape replaces the static rules' choice only
-            // if it beats it by kTrialMargin on the sample.
-            const bool skew_static = in_slot_stride % ((int64_t)4 << 20) == 0;
-            const int static_pick = skew_static ? 1 : (cm.max_tile_rows() <= 2 && m.n_in >= 8 ? 2 : 0);
-            pick = static_pick;
-            for (int v = 0; v < kCand; ++v)
-                if (best[v] < best[pick] && best[v] < kTrialMargin * best[static_pick]) pick = v;
-            cm.set_skew_choice(key, pick);
+        select = cap == hipStreamCaptureStatusNone;
+    }
+    if (!select) {
+        launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                          nbytes, stream, accumulate, -1);
+        return;
+    }
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    const std::array<int64_t, 8> key{in_slot_stride, in_stripe_stride, out_slot_stride, out_stripe_stride,
+                                     nbytes, nstripes, (int64_t)accumulate, (int64_t)dev};
+    bool time = false;
+    const int cand = cm.next_layout_pick(key, kLayoutNCand, kLayoutSamples, &time);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (time) {
+        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
+            hipEventRecord(e0, stream) != hipSuccess) {
+            (void)hipGetLastError();
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+            e0 = e1 = nullptr;
+            time = false;
         }
     }
-    launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
-                      nbytes, stream, accumulate, pick);
+    try {
+        launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                          nbytes, stream, accumulate, kLayoutCand[cand]);
+    } catch (...) {
+        if (time) {
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+        }
+        throw;
+    }
+    if (time) {
+        if (hipEventRecord(e1, stream) == hipSuccess) {
+            cm.add_layout_probe(key, cand, e0, e1);
+        } else {
+            (void)hipGetLastError();
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- synthetic data

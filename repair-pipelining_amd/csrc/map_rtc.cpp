@@ -196,7 +196,7 @@ struct MapPlanes::Impl {
     std::map<std::string, std::string> source;                  // shape key -> source
     std::map<std::string, std::vector<char>> code;              // arch + source -> code object (compiled once)
     std::map<std::pair<std::string, int>, Loaded> dev;          // (source, device) -> module
-    std::map<std::pair<std::string, int>, std::string> failed;  // (source, device) -> why (not retried)
+    std::map<std::pair<std::string, int>, std::string> failed;  // (source, device) -> why (deterministic: not retried)
 };
 
 MapPlanes::MapPlanes(LinearMap m) : map_(std::move(m)), impl_(new Impl) {
@@ -242,15 +242,18 @@ bool MapPlanes::load(const PlanesShape &sh, bool accumulate, hipFunction_t *fn, 
             return false;
         }
         Impl::Loaded n;
+        bool deterministic = true;  // as ClayRtc::prepare: load errors are retried, compile errors not
         try {
             const std::string arch = rtc_offload_arch();
             auto ci = impl_->code.find(arch + "\n" + src);
             if (ci == impl_->code.end()) ci = impl_->code.emplace(arch + "\n" + src, rtc_compile(src, arch)).first;
-            check_hip(hipModuleLoadData(&n.mod, ci->second.data()), "hipModuleLoadData(k_map_planes)");
+            const hipError_t le = hipModuleLoadData(&n.mod, ci->second.data());
+            deterministic = le != hipErrorOutOfMemory;
+            check_hip(le, "hipModuleLoadData(k_map_planes)");
             check_hip(hipModuleGetFunction(&n.fn, n.mod, kernel_name()), "hipModuleGetFunction(k_map_planes)");
         } catch (const Error &e) {
             if (n.mod) (void)hipModuleUnload(n.mod);
-            impl_->failed[dk] = e.what();
+            if (deterministic) impl_->failed[dk] = e.what();
             if (why) *why = e.what();
             return false;
         }

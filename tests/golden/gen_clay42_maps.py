@@ -1,0 +1,232 @@
+"""Closed-form Clay(4,2) maps, derived WITHOUT running the reference's stage sequence:
+an independent pin for the planner (csrc/codes.cpp) and the oracle (oracle/ecx_oracle.c),
+which both restate ClayCodeErasureDecodingStep.java stage by stage and so could share a
+misreading of it.  Writes tests/golden/clay42_closed_form.json (data only); run by
+gen_golden.py, or alone -- it needs only the Galois tables already in reference_kats.json.
+
+What is used, and nothing else:
+  * GF(2^8) from the reference's LOG_TABLE / EXP_TABLE literals (Galois.java:59-170);
+  * ReedSolomon.buildMatrix (ReedSolomon.java:373-385): vandermonde(n, k) times the
+    inverse of its top k x k square, for RS(2,2) (the pair transform) and RS(4,2) (the
+    per-plane code);
+  * the Clay geometry of ClayCodeUtil (:690-941): q = m = 2, t = (k+m)/m = 3,
+    alpha = q^t = 8, node i = (x, y) = (i % q, i / q), plane z = sum zvec[i] q^(t-1-i),
+    helper planes of node (x, y) = the planes with zvec[y] == x, couple plane of (x, y)
+    in z = z with zvec[y] := x;
+  * the pair transform as equations: for a vertex (node a, plane z) that is not a dot
+    (zvec[y_a] != x_a) and its couple (node b = (zvec[y_a], y_a), plane z[y_a := x_a]),
+    [U_a, U_b] = P [C_a, C_b] with P the RS(2,2) parity rows [[3, 2], [2, 3]]
+    (getPairWiseCouple :630-666: shards (C_a, C_b, U_a, U_b)); a dot has U = C;
+  * per plane, the uncoupled symbols form an RS(4,2) codeword, and exactly k = 4 of the 6
+    are known in every plane used below, so the unknown ones are the unique solution
+    (data = inverse of the known rows' submatrix times the known values; parity = the
+    parity rows times the data) -- no first-k choice arises.
+
+Single repair of node e = (ex, ey): in each helper plane z the four nodes outside column ey
+are decoupled from helper sub-chunks, the column's two U follow from the RS(4,2) equations,
+C(e, z) = U(e, z) (a dot), and for the column mate m = (x', ey) the couple of (e, z[ey := x'])
+is (m, z), so C(e, z[ey := x']) solves [U_m, ...] from (C_m, U_m):
+C_e = (3/2) C_m + (1/2) U_m.
+Encode (erasing the parity column {4, 5}): U of the data nodes from the pair transform, U of
+the parity nodes = RS(4,2) parity rows times them, C of the parity nodes = P^-1 (U_p, U_p').
+
+Slots are the reference's: input z*n + node (ClayCodeErasureDecodingStep.java:84-97),
+output z*|E| + j.  Maps are stored as {"out": [...], "in": [...], "coef": [...]} triples.
+"""
+import json
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+
+K, M = 4, 2
+N = K + M
+Q, T = M, N // M
+ALPHA = Q ** T
+
+
+class GF:
+    def __init__(self, log_table, exp_table):
+        self.log, self.exp = log_table, exp_table
+
+    def mul(self, a, b):
+        return 0 if a == 0 or b == 0 else self.exp[self.log[a] + self.log[b]]
+
+    def inv(self, a):
+        assert a != 0
+        return self.exp[255 - self.log[a]]
+
+    def div(self, a, b):
+        return self.mul(a, self.inv(b))
+
+    def power(self, a, n):  # Galois.exp: a^0 = 1 for every a
+        r = 1
+        for _ in range(n):
+            r = self.mul(r, a)
+        return r
+
+    def mat_mul(self, A, B):
+        return [[self._dot(row, [B[r][c] for r in range(len(B))]) for c in range(len(B[0]))] for row in A]
+
+    def _dot(self, u, v):
+        s = 0
+        for a, b in zip(u, v):
+            s ^= self.mul(a, b)
+        return s
+
+    def mat_inv(self, A):
+        n = len(A)
+        W = [list(A[r]) + [1 if c == r else 0 for c in range(n)] for r in range(n)]
+        for c in range(n):
+            p = next(r for r in range(c, n) if W[r][c])
+            W[c], W[p] = W[p], W[c]
+            f = self.inv(W[c][c])
+            W[c] = [self.mul(f, x) for x in W[c]]
+            for r in range(n):
+                if r != c and W[r][c]:
+                    g = W[r][c]
+                    W[r] = [x ^ self.mul(g, y) for x, y in zip(W[r], W[c])]
+        return [row[n:] for row in W]
+
+    def rs_matrix(self, k, m):
+        """ReedSolomon.buildMatrix: vandermonde(k+m, k) x inverse(top k x k)."""
+        V = [[self.power(r, c) for c in range(k)] for r in range(k + m)]
+        return self.mat_mul(V, self.mat_inv(V[:k]))
+
+
+# ---- symbolic values: {input slot: coefficient} (a linear form over the map's inputs)
+def lin_add(*terms):
+    out = {}
+    for t in terms:
+        for k, v in t.items():
+            out[k] = out.get(k, 0) ^ v
+    return {k: v for k, v in out.items() if v}
+
+
+def lin_scale(gf, c, t):
+    return {k: gf.mul(c, v) for k, v in t.items() if gf.mul(c, v)}
+
+
+def zvec(z):
+    v = [0] * T
+    for i in range(T - 1, -1, -1):
+        v[i] = z % Q
+        z //= Q
+    return v
+
+
+def zidx(v):
+    z = 0
+    for d in v:
+        z = z * Q + d
+    return z
+
+
+def node(x, y):
+    return x + Q * y
+
+
+def coords(i):
+    return i % Q, i // Q
+
+
+def C(z, j):
+    """The coupled (stored) sub-chunk of node j in plane z: an input slot."""
+    return {z * N + j: 1}
+
+
+def decoupled(gf, z, j):
+    """U(j, z) from stored sub-chunks: a dot, or the pair transform with its couple."""
+    x, y = coords(j)
+    v = zvec(z)
+    if v[y] == x:
+        return C(z, j)
+    partner = node(v[y], y)
+    v2 = list(v)
+    v2[y] = x
+    return lin_add(lin_scale(gf, 3, C(z, j)), lin_scale(gf, 2, C(zidx(v2), partner)))
+
+
+def solve_plane(gf, rs, U, missing):
+    """RS(4,2) per plane: fill U[j] for the two `missing` nodes from the four known."""
+    known = [j for j in range(N) if j not in missing]
+    assert len(known) == K
+    sub_inv = gf.mat_inv([rs[j] for j in known])
+    data = [lin_add(*[lin_scale(gf, sub_inv[d][c], U[known[c]]) for c in range(K)]) for d in range(K)]
+    for j in missing:
+        U[j] = data[j] if j < K else lin_add(*[lin_scale(gf, rs[j][d], data[d]) for d in range(K)])
+    return U
+
+
+def repair_map(gf, rs, e):
+    ex, ey = coords(e)
+    helpers = [z for z in range(ALPHA) if zvec(z)[ey] == ex]
+    column = [node(x, ey) for x in range(Q)]
+    out = {}
+    for z in helpers:
+        U = {j: decoupled(gf, z, j) for j in range(N) if j not in column}
+        solve_plane(gf, rs, U, column)
+        out[z] = U[e]  # a dot in its helper plane: C(e, z) = U(e, z)
+        for mate in column:
+            if mate == e:
+                continue
+            v = zvec(z)
+            v[ey] = coords(mate)[0]
+            # couple of (e, z[ey := x']) is (mate, z): shards (C_e, C_m, U_e, U_m), C_m and U_m known
+            out[zidx(v)] = lin_add(lin_scale(gf, gf.div(3, 2), C(z, mate)), lin_scale(gf, gf.div(1, 2), U[mate]))
+    return out  # output slot z (|E| = 1) -> linear form
+
+
+def encode_map(gf, rs):
+    parity = [node(x, T - 1) for x in range(Q)]  # the parity column {4, 5}
+    U = {}
+    for z in range(ALPHA):
+        Uz = {j: decoupled(gf, z, j) for j in range(K)}
+        for p in parity:
+            Uz[p] = lin_add(*[lin_scale(gf, rs[p][d], Uz[d]) for d in range(K)])
+        U[z] = Uz
+    out = {}
+    for z in range(ALPHA):
+        v = zvec(z)
+        for jj, p in enumerate(parity):
+            x, y = coords(p)
+            if v[y] == x:
+                out[z * len(parity) + jj] = U[z][p]
+            else:
+                partner = node(v[y], y)
+                v2 = list(v)
+                v2[y] = x
+                # [C_p, C_p'] = P^-1 [U_p, U_p'] with P = [[3, 2], [2, 3]] (its own inverse)
+                pinv = gf.mat_inv([[3, 2], [2, 3]])
+                out[z * len(parity) + jj] = lin_add(lin_scale(gf, pinv[0][0], U[z][p]),
+                                                    lin_scale(gf, pinv[0][1], U[zidx(v2)][partner]))
+    return out
+
+
+def triples(m):
+    o, i, c = [], [], []
+    for out_slot in sorted(m):
+        for in_slot in sorted(m[out_slot]):
+            o.append(out_slot)
+            i.append(in_slot)
+            c.append(m[out_slot][in_slot])
+    return {"out": o, "in": i, "coef": c, "nnz": len(c)}
+
+
+def main():
+    kats = json.loads((HERE / "reference_kats.json").read_text())
+    gf = GF(kats["galois"]["log_table"], kats["galois"]["exp_table"])
+    rs = gf.rs_matrix(K, M)
+    assert rs[K:] == kats["rs_parity_rows"]["4,2"], rs[K:]
+    assert gf.rs_matrix(2, 2)[2:] == [[3, 2], [2, 3]]
+    doc = {
+        "source": "closed-form Clay(4,2) maps (tests/golden/gen_clay42_maps.py); no reference stage sequence run",
+        "repair_e1": triples(repair_map(gf, rs, 1)),
+        "repair_e4": triples(repair_map(gf, rs, 4)),
+        "encode_45": triples(encode_map(gf, rs)),
+    }
+    (HERE / "clay42_closed_form.json").write_text(json.dumps(doc) + "\n")
+    print("wrote", HERE / "clay42_closed_form.json", {k: v["nnz"] for k, v in doc.items() if k != "source"})
+
+
+if __name__ == "__main__":
+    main()

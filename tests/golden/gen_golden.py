@@ -13,8 +13,11 @@ GPU box sees.  Contents are data only:
     (the input file of SampleEncoder / LRCErasureCodeExample, configs 1 and 3).
 
 The SURVEY.md A.4 cross-check digests (sha256, first 16 hex chars) are kept
-as independent expected values for the oracle restatement.
+as independent expected values for the oracle restatement.  gen_clay42_maps.py then
+derives the Clay(4,2) e=1 / e=4 repair maps and the encode map in closed form from the
+pair-transform and RS equations alone (clay42_closed_form.json).
 """
+import sys
 import json
 import re
 import shutil
@@ -22,6 +25,7 @@ from pathlib import Path
 
 REF = Path("/root/reference")
 HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
 
 
 def parse_java_array(text: str, name: str):
@@ -87,6 +91,9 @@ def main():
     (HERE / "reference_kats.json").write_text(json.dumps(kats, indent=1) + "\n")
     shutil.copyfile(REF / "LP-block.jpg", HERE / "LP-block.jpg")
     print("wrote", HERE / "reference_kats.json", "and LP-block.jpg")
+    # the closed-form Clay(4,2) maps (an independent pin of the planner and the oracle)
+    import gen_clay42_maps
+    gen_clay42_maps.main()
 
 
 if __name__ == "__main__":

@@ -43,13 +43,14 @@ class Jni:
         # the forwarders bind to that same library instance
         import rpamd
         rpamd.load()
-        if not LIB.exists():
-            build()
+        build()  # make is incremental: rebuilds when the forwarders or the fakes changed
         self.lib = ctypes.CDLL(str(LIB))
         L = self.lib
         L.fake_env.restype = ctypes.c_void_p
         L.fake_array.restype = ctypes.c_void_p
         L.fake_array.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        L.fake_direct_buffer.restype = ctypes.c_void_p
+        L.fake_direct_buffer.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         L.fake_object_array.restype = ctypes.c_void_p
         L.fake_object_array.argtypes = [ctypes.c_int32]
         L.fake_set_element.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
@@ -71,6 +72,15 @@ class Jni:
         a = np.ascontiguousarray(a)
         self._keep.append(a)
         o = self.lib.fake_array(a.ctypes.data, int(a.size), int(a.itemsize))  # non-null even when empty
+        self._fakes.append(o)
+        return o
+
+    def direct(self, a, capacity=None):
+        """A direct java.nio.ByteBuffer over the numpy array `a` (no copy), of `capacity`
+        bytes (default: all of `a`)."""
+        a = np.ascontiguousarray(a)
+        self._keep.append(a)
+        o = self.lib.fake_direct_buffer(a.ctypes.data, int(a.nbytes if capacity is None else capacity))
         self._fakes.append(o)
         return o
 

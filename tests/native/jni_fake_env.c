@@ -17,10 +17,11 @@
 #include <string.h>
 
 struct _jobject {
-    int kind;       /* 1 = primitive array, 2 = object array, 3 = string */
+    int kind;       /* 1 = primitive array, 2 = object array, 3 = string, 4 = direct ByteBuffer */
     jsize len;      /* elements */
     int elem_size;  /* bytes per element (primitive arrays) */
-    void *data;     /* primitive: caller memory; object: jobject[len]; string: char[] */
+    void *data;     /* primitive / direct buffer: caller memory; object: jobject[len]; string: char[] */
+    jlong capacity; /* direct buffer: bytes */
 };
 
 static int64_t g_pins_now, g_pins_total, g_unpins_total, g_violations, g_deleted, g_jni_calls_pinned;
@@ -110,19 +111,27 @@ static jstring f_NewStringUTF(JNIEnv *env, const char *s) {
     return o;
 }
 
+/* As the JNI specification: NULL / -1 for a buffer that is not direct (a heap ByteBuffer,
+ * modelled here by any non-direct object). */
 static void *f_GetDirectBufferAddress(JNIEnv *env, jobject b) {
     (void)env;
     jni_call();
-    return b ? b->data : NULL;
+    return b && b->kind == 4 ? b->data : NULL;
+}
+
+static jlong f_GetDirectBufferCapacity(JNIEnv *env, jobject b) {
+    (void)env;
+    jni_call();
+    return b && b->kind == 4 ? b->capacity : -1;
 }
 
 static jobject f_NewDirectByteBuffer(JNIEnv *env, void *address, jlong capacity) {
     (void)env;
     jni_call();
     struct _jobject *o = (struct _jobject *)calloc(1, sizeof(*o));
-    o->kind = 1;
+    o->kind = 4;
     o->elem_size = 1;
-    o->len = (jsize)capacity;
+    o->capacity = capacity;
     o->data = address;
     return o;
 }
@@ -130,7 +139,7 @@ static jobject f_NewDirectByteBuffer(JNIEnv *env, void *address, jlong capacity)
 static const struct JNINativeInterface_ g_table = {
     f_GetArrayLength,          f_GetObjectArrayElement, f_GetIntArrayRegion,    f_SetLongArrayRegion,
     f_GetPrimitiveArrayCritical, f_ReleasePrimitiveArrayCritical, f_DeleteLocalRef, f_NewStringUTF,
-    f_GetDirectBufferAddress,  f_NewDirectByteBuffer,
+    f_GetDirectBufferAddress,  f_NewDirectByteBuffer,    f_GetDirectBufferCapacity,
 };
 static JNIEnv g_env = &g_table;
 
@@ -142,6 +151,16 @@ jobject fake_array(void *data, int32_t len, int32_t elem_size) {
     o->kind = 1;
     o->len = len;
     o->elem_size = elem_size;
+    o->data = data;
+    return o;
+}
+
+/* A direct ByteBuffer over caller memory (ByteBuffer.allocateDirect / wrapAddress). */
+jobject fake_direct_buffer(void *data, int64_t capacity) {
+    struct _jobject *o = (struct _jobject *)calloc(1, sizeof(*o));
+    o->kind = 4;
+    o->elem_size = 1;
+    o->capacity = capacity;
     o->data = data;
     return o;
 }

@@ -42,5 +42,6 @@ struct JNINativeInterface_ {
     jstring (*NewStringUTF)(JNIEnv *env, const char *utf);
     void *(*GetDirectBufferAddress)(JNIEnv *env, jobject buf);
     jobject (*NewDirectByteBuffer)(JNIEnv *env, void *address, jlong capacity);
+    jlong (*GetDirectBufferCapacity)(JNIEnv *env, jobject buf);
 };
 #endif

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(ecx):
     assert headers == ["ecx.h", "ecx_tune.h"]
     missing = [s for h in headers for s in declared_symbols(h) if not hasattr(lib, s)]
     assert not missing, missing
-    assert len(declared_symbols("ecx_tune.h")) == 10
+    assert len(declared_symbols("ecx_tune.h")) == 11
 
 
 def test_binding_table_matches_header(ecx):
@@ -153,7 +153,7 @@ def test_tuning_keys(ecx):
     header = (ROOT / "include" / "ecx_tune.h").read_text()
     documented = re.findall(r'^ \*\s+"([a-z_]+)"', header, flags=re.M)
     defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "wave_groups": 0, "lds_tables": 1, "store_scope": 0, "occ_lds": 0,
-                "chunk_major": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "skew_trial": 0, "plan_cache": 256, "bitslice": 0, "lds_lut": 0, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_persist": 0, "rtc_units": 1, "rtc_sched": 2, "rtc_nt": 5, "rtc_diag": 0, "xcd_run": 8, "xcd_misaligned": 1,
+                "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "bitslice": 0, "lds_lut": 0, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_persist": 0, "rtc_units": 1, "rtc_sched": 2, "rtc_nt": 5, "rtc_diag": 0, "xcd_run": 8, "xcd_misaligned": 1,
                 "map_planes": 1, "planes_lookahead": 12, "planes_waves": 2,
                 "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512}
     assert sorted(documented) == sorted(defaults)
@@ -162,7 +162,7 @@ def test_tuning_keys(ecx):
     for key, val in defaults.items():
         assert tune(key.encode(), val) == 0, key
     assert tune(b"no_such_knob", 1) == -1
-    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("xcd_misaligned", 2), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("skew_trial", 2), ("plan_cache", -1), ("bitslice", 3), ("lds_lut", 3), ("lds_lut", -1), ("roctx", 2), ("host_contexts", 2), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("rtc_units", 0), ("rtc_units", 3), ("rtc_sched", 3), ("rtc_nt", -1), ("rtc_nt", 16), ("occ_lds", -2), ("occ_lds", 65537), ("rtc_diag", 1), ("rtc_diag", 32), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5)):
+    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("xcd_misaligned", 2), ("stagger", -1), ("stagger", 65), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("layout_select", 2), ("plan_cache", -1), ("bitslice", 3), ("lds_lut", 3), ("lds_lut", -1), ("roctx", 2), ("host_contexts", 2), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("rtc_units", 0), ("rtc_units", 3), ("rtc_sched", 3), ("rtc_nt", -1), ("rtc_nt", 16), ("occ_lds", -2), ("occ_lds", 65537), ("rtc_diag", 1), ("rtc_diag", 32), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5)):
         assert tune(key.encode(), bad) == -1, key
     for key, val in defaults.items():  # restore
         tune(key.encode(), val)
@@ -176,3 +176,51 @@ def test_last_kernel_label_before_any_launch(ecx):
     f.argtypes, f.restype = [C.c_char_p, C.c_int], C.c_int
     assert f(C.create_string_buffer(8), 8) == 0
     assert f(None, 0) == -1
+
+
+def test_codec_registry_refcounts_and_bounds_idle(ecx):
+    """ecx_rs_create / ecx_clay_create share one reference-counted codec per key (ecx.h):
+    creates of an equal codec return the same object, destroy drops one reference, the
+    last one parks the codec in a bounded idle cache (a later create revives it with its
+    plans), and past 64 idle codecs the least recently released are freed -- so a caller
+    cycling through many distinct codecs (one Clay decoding step per erasure pattern) does
+    not grow the process without bound.  Host-only: codec creation needs no device."""
+    lib = ecx.lib()
+    stats = lib.ecx_codec_stats
+    stats.argtypes, stats.restype = [ctypes.POINTER(ctypes.c_int)] * 4, ctypes.c_int
+    create, destroy = lib.ecx_rs_create, lib.ecx_rs_destroy
+
+    def counts():
+        v = [ctypes.c_int() for _ in range(4)]
+        assert stats(*[ctypes.byref(x) for x in v]) == 0
+        return [x.value for x in v]
+
+    def rs(k, m):
+        h = ctypes.c_void_p()
+        assert create(k, m, ctypes.byref(h)) == 0
+        return h.value
+
+    live0, idle0, _, _ = counts()
+    a, b = rs(29, 3), rs(29, 3)
+    assert a == b and counts()[0] == live0 + 1
+    destroy(a)
+    assert counts()[:2] == [live0 + 1, idle0]        # one reference left
+    destroy(b)
+    assert counts()[:2] == [live0, idle0 + 1]        # parked idle, not freed
+    assert rs(29, 3) == a and counts()[:2] == [live0 + 1, idle0]  # revived: same object
+    destroy(a)
+    # many distinct codecs created and released: the idle cache stays bounded
+    for k in range(100):
+        destroy(rs(30 + k, 2))
+    live, idle, _, _ = counts()
+    assert live == live0 and idle == 64
+    # Clay steps: the same rules per (k, m, virtual nodes, erased list)
+    er = (ctypes.c_int * 1)(3)
+    h1, h2 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.ecx_clay_create(4, 2, er, 1, ctypes.byref(h1)) == 0
+    assert lib.ecx_clay_create(4, 2, er, 1, ctypes.byref(h2)) == 0
+    assert h1.value == h2.value
+    cl_live = counts()[2]
+    lib.ecx_clay_destroy(h1)
+    lib.ecx_clay_destroy(h2)
+    assert counts()[2] == cl_live - 1

@@ -122,10 +122,11 @@ def test_rs_decode_all_subsets(ecx):
 def test_rs_big_encode_decode(ecx):
     """ReedSolomonTest.testBigEncodeDecode (:90-103) on the device: RS(64,64) with
     200-B shards of java.util.Random(0).nextInt(256) -- a multi-tile map (8 row tiles
-    of 64 entries each).  The encode equals the oracle's; decoding every erasure
-    subset of size <= 2 among shards [0, 10) restores the stripe (the reference's
-    subsets), and so do random 64-shard erasures; on non-codeword shards decodeMissing
-    equals the oracle's map."""
+    of 64 entries each).  The encode equals the oracle's; decoding every erasure subset
+    the reference's runEncodeDecode / tryAllSubsetsMissing (:111-169) tries -- every
+    subset of shards [0, 10), sizes 0..10, 1,024 subsets, on one set of test shards that
+    each decode restores for the next -- restores the stripe, and so do random 64-shard
+    erasures; on non-codeword shards decodeMissing equals the oracle's map."""
     import itertools
     r = O.JavaRandom(0)
     data = [np.array([r.next_int(256) for _ in range(200)], np.uint8) for _ in range(64)]
@@ -136,10 +137,11 @@ def test_rs_big_encode_decode(ecx):
     O.ReedSolomon(64, 64).encode_parity(ref, 0, 200)
     assert all((a == b).all() for a, b in zip(allsh, ref))
     rng = np.random.default_rng(64)
-    subsets = [s for n in range(3) for s in itertools.combinations(range(10), n)]
+    subsets = [s for n in range(64 + 1) for s in itertools.combinations(range(10), n)]
+    assert len(subsets) == 1024
     subsets += [tuple(int(i) for i in rng.choice(128, 64, replace=False)) for _ in range(4)]
+    test = [s.copy() for s in allsh]
     for subset in subsets:
-        test = [s.copy() for s in allsh]
         present = [True] * 128
         for s in subset:
             test[s][:] = 0
@@ -1443,6 +1445,64 @@ def test_clay104_shipped_repair_kernel_vs_shortened_oracle(ecx, torch_dev, e):
         assert not bad, (e, s, bad[:8])
 
 
+def test_clay_rtc_first_use_from_two_streams(ecx, torch_dev):
+    """The per-helper-plane kernel's program table is uploaded synchronously before the
+    loaded module is published (ClayRtc::prepare), so a second thread that launches the
+    kernel on another stream right after first use never reads a table still queued
+    behind the first caller's stream.  Two threads, two streams, one fresh shortened
+    Clay(9,4) step (Clay(12,4) with 3 virtual nodes, rtc_group 0): the first thread's
+    stream is kept busy with a large fill when it reaches the kernel; both repairs equal
+    the composed-map kernel and the oracle."""
+    import threading
+    torch = torch_dev
+    k, m, v, e, B, S = 9, 4, 3, 2, 4096, 8
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    n, a = k + m, step.subPacketSize
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 77)
+    busy = torch.empty(2 << 30, dtype=torch.uint8, device="cuda")
+    outs = [torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    barrier, errors = threading.Barrier(2), []
+
+    def worker(i):
+        try:
+            st = streams[i]
+            mine = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)  # the same shared codec
+            if i == 0:
+                for _ in range(4):
+                    ecx.fill_random(busy, busy.numel(), 3, stream=st)
+            barrier.wait()
+            mine.performCodingBatch(pool, n * a * B, B, outs[i], a * B, B, S, B, stream=st)
+            st.synchronize()
+        except Exception as err:  # pragma: no cover - reported below
+            errors.append(err)
+
+    ecx.tune("clay_rtc", 2)
+    ecx.tune("rtc_group", 0)
+    try:
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors
+        ecx.tune("clay_rtc", 0)
+        ref0 = torch.zeros((S, a, B), dtype=torch.uint8, device="cuda")
+        step.performCodingBatch(pool, n * a * B, B, ref0, a * B, B, S, B)
+        torch.cuda.synchronize()
+    finally:
+        ecx.tune("clay_rtc", 1)
+        ecx.tune("rtc_group", 1)
+    assert bool(torch.equal(outs[0], ref0)) and bool(torch.equal(outs[1], ref0))
+    host = pool[S - 1].cpu().numpy()
+    inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
+    ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
+    got = ref0[S - 1].cpu().numpy()
+    assert all((got[z] == ref[z]).all() for z in range(a))
+
+
 _NO_HIPRTC_SCRIPT = r"""
 import sys
 import numpy as np
@@ -1663,55 +1723,64 @@ def test_map_planes_every_clay42_erasure_pattern(ecx, torch_dev):
 
 
 @pytest.mark.parametrize("pitch", [(4 << 20), (1 << 20) + 4096])
-def test_skew_trial_choice_is_measured_and_exact(ecx, torch_dev, pitch):
-    """skew_trial: the first large RS(12,4) decode batch at a new shard pitch times three
-    launch shapes (4 KiB workgroups, skewed chunks, one-wave workgroups) on its own stripes
-    and keeps the fastest for (map, pitch mod 16 MiB); the in-place results equal the static
-    rule's and the oracle's, and accumulate mode never runs the trial."""
+def test_layout_select_is_measured_and_exact(ecx, torch_dev, pitch):
+    """layout_select (include/ecx_tune.h): the first calls of a large RS(12,4) decode batch at
+    a new layout run the candidate launch shapes in turn (static rules, 4 KiB and one-wave
+    workgroups, skewed chunks, staggered stripes), each timed with events on the caller's
+    stream, and the fastest median is then kept for that layout.  Every call's in-place
+    output equals the erased originals (and the oracle on one stripe), in overwrite and in
+    accumulate mode; with layout_select 0 nothing is selected."""
     torch = torch_dev
     L = 1 << 20
-    S = (640 << 20) // (12 * L)  # >= 512 MiB of input: the trial runs
+    S = (320 << 20) // (12 * L) + 1  # >= 256 MiB of input: selection runs
     rs = ecx.ReedSolomon.create(12, 4)
     present = [False, False] + [True] * 14
     pool = torch.empty((S, 16, pitch), dtype=torch.uint8, device="cuda")
     ecx.fill_random(pool, pool.numel(), 88)
     rs.encode_map().apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
     orig = pool[:, 0:2, :L].clone()
-    outs = {}
     mat, ins_, outs_ = rs.decode_map(present).matrix()
     fresh = lambda: ecx.GfMap.from_matrix(mat, in_slot=[int(i) for i in ins_],  # noqa: E731
-                                          out_slot=[int(o) for o in outs_])    # nothing measured yet
-    for trial in (0, 1):
-        dmap = fresh()
-        try:
-            ecx.tune("skew_trial", trial)
-            assert dmap.skew_choice(pitch) == -1
-            pool[:, 0:2, :L] = 0
-            dmap.apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
-            torch.cuda.synchronize()
-            outs[trial] = (pool[:, 0:2, :L].clone(), ecx.last_kernel(), dmap.skew_choice(pitch))
-        finally:
-            ecx.tune("skew_trial", 0)
-    assert outs[0][2] == -1 and outs[1][2] in (0, 1, 2)
-    assert outs[1][1].startswith("k_gf_apply_skew") == (outs[1][2] == 1), outs[1][1:]
-    assert (", 64, " in outs[1][1]) == (outs[1][2] == 2), outs[1][1:]
-    assert bool(torch.equal(outs[0][0], orig)) and bool(torch.equal(outs[1][0], orig))
+                                          out_slot=[int(o) for o in outs_])    # nothing selected yet
+    dmap = fresh()
+    kernels = set()
+    for call in range(26):  # 7 candidates x 3 timings, harvested on later calls
+        assert dmap.layout_choice(pitch) == -1 or call > 21
+        pool[:, 0:2, :L] = 0
+        dmap.apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+        torch.cuda.synchronize()
+        kernels.add(ecx.last_kernel())
+        assert bool(torch.equal(pool[:, 0:2, :L], orig)), call
+    choice, ms = dmap.layout_choice(pitch, with_times=True)
+    assert choice != -1, ms
+    assert all(t > 0 for t in ms[:7]), ms
+    assert any(k.startswith("k_gf_apply_skew") for k in kernels) and any(", 64, " in k for k in kernels), kernels
+    static_ms = ms[0]
+    assert min(ms[:7]) <= static_ms
     # the oracle on one stripe
     host = pool[S - 1].cpu().numpy()
     shards = [np.zeros(L, np.uint8) if i < 2 else host[i, :L].copy() for i in range(16)]
     O.ReedSolomon(12, 4).decode_missing(shards, [i >= 2 for i in range(16)], 0, L)
     assert (shards[0] == orig[S - 1, 0].cpu().numpy()).all() and (shards[1] == orig[S - 1, 1].cpu().numpy()).all()
-    # accumulate mode: no trial (it would accumulate twice)
+    # accumulate mode: every candidate XOR-accumulates exactly once per call
     acc_map = fresh()
     acc = torch.zeros((S, 2, pitch), dtype=torch.uint8, device="cuda")
-    try:
-        ecx.tune("skew_trial", 1)
+    for _ in range(25):
         acc_map.accumulate_batch(pool, 16 * pitch, pitch, acc, 2 * pitch, pitch, S, L)
         torch.cuda.synchronize()
+    assert acc_map.layout_choice(pitch) != -1
+    assert bool(torch.equal(acc[:, :, :L], orig))  # 25 accumulations: an odd count leaves M * in
+    # off: the static rules only
+    off_map = fresh()
+    try:
+        ecx.tune("layout_select", 0)
+        for _ in range(4):
+            off_map.apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+        torch.cuda.synchronize()
     finally:
-        ecx.tune("skew_trial", 0)
-    assert acc_map.skew_choice(pitch) == -1
-    assert bool(torch.equal(acc[:, :, :L], orig))
+        ecx.tune("layout_select", 1)
+    assert off_map.layout_choice(pitch) == -1
+    assert bool(torch.equal(pool[:, 0:2, :L], orig))
 
 
 @pytest.mark.parametrize("e,B,S", [(3, 4096, 5), (13, 8192 + 16, 3), (0, 4096, 17)])

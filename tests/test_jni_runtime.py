@@ -9,9 +9,12 @@ ArrayIndexOutOfBoundsException of the CodingLoop byte loop, InputOutputByteTable
 .java:34-41) without reaching the export, null Clay sub-chunks pass, the planner entry
 points return the reference's values through the binding, and every pin is released
 with no JNI call made inside a critical region.
-GPU: codeSomeShards (RS(4,2) parity rows), the RS codec calls, decodeMissingSingle and
-clayPerformCoding (Clay(4,2), e = 1) through the binding equal the oracle, with array
-positions (ByteBuffer.arrayOffset + position) applied."""
+The host batches over direct ByteBuffers (clayPerformCodingBatchHostBuffer,
+mapApplyBatchHostBuffer): a buffer shorter than the batch's extent, a heap buffer or a
+null one is refused before anything is pinned or read.
+GPU: codeSomeShards (RS(4,2) parity rows), the RS codec calls, decodeMissingSingle,
+clayPerformCoding (Clay(4,2), e = 1) and the two ByteBuffer host batches through the
+binding equal the oracle, with array positions (ByteBuffer.arrayOffset + position) applied."""
 import numpy as np
 import pytest
 
@@ -228,6 +231,93 @@ def test_valid_per_call_reaches_the_export(J):
     assert c["pins"] == 1 + 4 + 2 and c["last_mode"] == 2  # matrixRows released last, JNI_ABORT
 
 
+# ---------------------------------------------------------------- host batches over direct ByteBuffers
+# EcxNative.clayPerformCodingBatchHostBuffer / mapApplyBatchHostBuffer read each buffer's
+# address and capacity themselves (GetDirectBufferAddress / GetDirectBufferCapacity) and
+# refuse a layout that addresses past the capacity, as the reference's ByteBuffer get/put
+# would throw (ClayCoordinator.kt:378-390), before anything reaches the device.
+def clay_batch_layout(S, B, n=6, a=8, ne=1):
+    """Stripe-major Clay(4,2) host batch: [S][n*a][B] in, [S][ne*a][B] out."""
+    return n * a * B, B, ne * a * B, B, S, B
+
+
+def test_clay_batch_host_buffer_extent_checks(J):
+    clay = handle(J, "clayCreate", 4, 2, J.ints([1]), 1)
+    try:
+        S, B = 3, 256
+        iss, isl, oss, osl, _, _ = clay_batch_layout(S, B)
+        inp, out = rnd(S * iss, 1), np.zeros(S * oss, np.uint8)
+        mi, mo = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        cm = np.zeros(1, np.int64)
+        assert J.call("clayMap", clay, J.array(cm)) == OK
+        assert J.call("mapSlotExtent", int(cm[0]), J.array(mi), J.array(mo)) == OK
+        # node 1 erased: the last slot read is plane 7's node 5 (47), the last written plane 7's (7)
+        assert (int(mi[0]), int(mo[0])) == (47, 7)
+        need_in = (S - 1) * iss + 47 * isl + B
+        need_out = (S - 1) * oss + 7 * osl + B
+        J.reset()  # count the pins of the batch calls below only
+        call = lambda i, o, **kw: J.call("clayPerformCodingBatchHostBuffer", clay, i, kw.get("iss", iss), isl, o,  # noqa: E731
+                                         oss, osl, kw.get("S", S), kw.get("B", B))
+        assert call(J.direct(inp, need_in - 1), J.direct(out)) == IDX      # input one byte short
+        assert call(J.direct(inp), J.direct(out, need_out - 1)) == IDX     # output one byte short
+        assert call(J.direct(inp), J.direct(out), S=4) == IDX              # one stripe too many
+        assert call(J.direct(inp), J.direct(out), B=B + 1) == IDX          # sub-chunks past the stride
+        assert call(J.direct(inp), J.direct(out), iss=1 << 62) == IDX      # extent overflows int64
+        assert call(J.direct(inp), J.direct(out), iss=-1) == ILL           # negative stride
+        assert call(J.direct(inp), J.direct(out), S=-1) == ILL
+        assert call(J.array(inp), J.direct(out)) == NUL                    # heap buffer: no address
+        assert call(None, J.direct(out)) == NUL
+        assert call(J.direct(inp), None) == NUL
+        assert J.call("clayPerformCodingBatchHostBuffer", 0, J.direct(inp), iss, isl, J.direct(out), oss, osl,
+                      S, B) == NUL
+        assert J.counters()["pins"] == 0 and (out == 0).all()  # nothing pinned, nothing written
+        # exactly the extent: reaches the export (the device, or ECX_E_DEVICE without one)
+        st = call(J.direct(inp, need_in), J.direct(out, need_out))
+        assert st == (OK if has_device(J) else DEV), st
+        assert call(J.direct(inp), J.direct(out), S=0) == OK  # an empty batch touches nothing
+    finally:
+        J.call("clayDestroy", clay)
+    # nothing erased: performCoding returns before any check (ClayCodeErasureDecodingStep.java:54-56)
+    none = handle(J, "clayCreate", 4, 2, J.ints([]), 0)
+    try:
+        assert J.call("clayPerformCodingBatchHostBuffer", none, None, 0, 0, None, 0, 0, 3, 64) == OK
+    finally:
+        J.call("clayDestroy", none)
+
+
+def test_map_batch_host_buffer_extent_checks(J):
+    mat = np.arange(1, 13, dtype=np.uint8).reshape(3, 4)
+    mp = handle(J, "mapCreate", J.array(mat), 3, 4, J.ints([0, 2, 4, 6]), J.ints([1, 3, 5]))
+    try:
+        S, L, pitch = 5, 100, 128
+        inp, out = rnd(S * 8 * pitch, 2), np.zeros(S * 8 * pitch, np.uint8)
+        need_in, need_out = (S - 1) * 8 * pitch + 6 * pitch + L, (S - 1) * 8 * pitch + 5 * pitch + L
+        J.reset()
+        call = lambda i, o: J.call("mapApplyBatchHostBuffer", mp, i, 8 * pitch, pitch, o, 8 * pitch, pitch, S, L)  # noqa: E731
+        assert call(J.direct(inp, need_in - 1), J.direct(out)) == IDX
+        assert call(J.direct(inp), J.direct(out, need_out - 1)) == IDX
+        assert call(J.array(inp), J.direct(out)) == NUL
+        assert J.counters()["pins"] == 0 and (out == 0).all()
+        st = call(J.direct(inp, need_in), J.direct(out, need_out))
+        assert st == (OK if has_device(J) else DEV), st
+    finally:
+        J.call("mapDestroy", mp)
+
+
+def test_java_wrapper_uses_the_checked_variant():
+    """EcxClayCodeErasureDecodingStep.performCodingBatchHost goes through the capacity-checked
+    native and checks the same extent in Java first (ArrayIndexOutOfBoundsException /
+    NullPointerException), so a short or heap buffer never reaches the address-taking path."""
+    from pathlib import Path
+    src = (Path(__file__).resolve().parents[1] / "jni" / "distributed" / "erasure" / "coding" / "clay" /
+           "EcxClayCodeErasureDecodingStep.java").read_text()
+    body = src[src.index("public void performCodingBatchHost"):]
+    body = body[:body.index("\n    }\n")]
+    assert "clayPerformCodingBatchHostBuffer" in body and "directAddress" not in body
+    assert "checkExtent(in" in body and "checkExtent(out" in body
+    assert "ArrayIndexOutOfBoundsException" in src and "isDirect()" in src
+
+
 # ---------------------------------------------------------------- GPU: results through the binding
 @pytest.mark.gpu
 def test_code_some_shards_via_jni_vs_oracle(J):
@@ -303,3 +393,46 @@ def test_clay_perform_coding_via_jni_vs_oracle(J, B, pos):
             assert (o[pos:] == r).all() and (o[:pos] == 0x77).all()
     finally:
         J.call("clayDestroy", clay)
+
+
+@pytest.mark.gpu
+def test_clay_batch_host_buffer_via_jni_vs_oracle(J):
+    """Clay(4,2), e = 1, three stripes of 4 KiB sub-chunks in direct host buffers, through the
+    capacity-checked forwarder: every repaired sub-chunk equals the oracle's performCoding."""
+    clay = handle(J, "clayCreate", 4, 2, J.ints([1]), 1)
+    try:
+        S, B, n, a = 3, 4096, 6, 8
+        iss, isl, oss, osl, _, _ = clay_batch_layout(S, B)
+        inp = rnd(S * iss, 3)
+        out = np.full(S * oss, 0x5A, np.uint8)
+        st = J.call("clayPerformCodingBatchHostBuffer", clay, J.direct(inp), iss, isl, J.direct(out), oss, osl, S, B)
+        assert st == OK, st
+        for s_ in range(S):
+            ins = [None if i % n == 1 else inp[s_ * iss + i * B:s_ * iss + (i + 1) * B].copy() for i in range(n * a)]
+            ref = [np.zeros(B, np.uint8) for _ in range(a)]
+            O.Clay(4, 2, [1]).perform_coding(ins, ref, B)
+            for z in range(a):
+                assert (out[s_ * oss + z * B:s_ * oss + (z + 1) * B] == ref[z]).all(), (s_, z)
+    finally:
+        J.call("clayDestroy", clay)
+
+
+@pytest.mark.gpu
+def test_map_batch_host_buffer_via_jni_vs_oracle(J):
+    mat = np.random.default_rng(4).integers(0, 256, (3, 4), dtype=np.uint8)
+    mp = handle(J, "mapCreate", J.array(mat), 3, 4, J.ints([0, 2, 4, 6]), J.ints([1, 3, 5]))
+    try:
+        S, L, pitch = 5, 1000, 1024
+        inp, out = rnd(S * 8 * pitch, 5), np.zeros(S * 8 * pitch, np.uint8)
+        st = J.call("mapApplyBatchHostBuffer", mp, J.direct(inp), 8 * pitch, pitch, J.direct(out), 8 * pitch, pitch,
+                    S, L)
+        assert st == OK, st
+        for s_ in range(S):
+            base = s_ * 8 * pitch
+            ins = [inp[base + j * pitch:base + j * pitch + L] for j in (0, 2, 4, 6)]
+            ref = [np.zeros(L, np.uint8) for _ in range(3)]
+            O.code_some_shards(mat, ins, ref, 0, L)
+            for r, slot in zip(ref, (1, 3, 5)):
+                assert (out[base + slot * pitch:base + slot * pitch + L] == r).all()
+    finally:
+        J.call("mapDestroy", mp)

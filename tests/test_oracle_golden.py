@@ -130,16 +130,21 @@ def test_big_encode_decode():
     rs = O.ReedSolomon(64, 64)
     allsh = [np.array(d, np.uint8) for d in data] + [np.zeros(200, np.uint8) for _ in range(64)]
     rs.encode_parity(allsh, 0, 200)
-    # a sample of the reference's subsets (all of size <= 2 among [0,10)) keeps this CPU test quick
-    for nmiss in range(3):
+    # runEncodeDecode / tryAllSubsetsMissing (:111-169): numberMissing 0..64, every subset of
+    # that size among shards [0, 10) -- sizes 0..10, 1,024 subsets -- on one set of test
+    # shards that each decode must restore for the next subset
+    test = [s.copy() for s in allsh]
+    n_subsets = 0
+    for nmiss in range(64 + 1):
         for subset in itertools.combinations(range(10), nmiss):
-            test = [s.copy() for s in allsh]
             present = [True] * 128
             for s in subset:
                 test[s][:] = 0
                 present[s] = False
             rs.decode_missing(test, present, 0, 200)
-            assert all((a == b).all() for a, b in zip(allsh, test))
+            assert all((a == b).all() for a, b in zip(allsh, test)), subset
+            n_subsets += 1
+    assert n_subsets == 1024
 
 
 def test_not_enough_shards():

@@ -3,11 +3,15 @@ apply, applied here in numpy, must reproduce the oracle's stage-by-stage
 restatement of the reference on the same (random, non-codeword) inputs.
 This pins the planner independently of the GPU; tests/test_gpu_parity.py then
 pins the kernels against the same oracle."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
 import oracle as O
 from conftest import gf_apply_numpy, shortened_clay_oracle as _shortened_oracle
+
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def test_field_tables_match_reference(ecx, kats):
@@ -133,6 +137,40 @@ def test_clay42_repair_map_pinned_to_survey_a3(ecx):
         if e == 1:
             assert set(mat[mat != 0].tolist()) == A3_E1_COEFFS
             assert set(probed[probed != 0].tolist()) == A3_E1_COEFFS
+
+
+def _probe_oracle_map(k, m, erased, ins):
+    """The oracle's performCoding map for the standard null pattern, read off by unit
+    vectors (byte j of input slot ins[j] is 1, every other byte 0)."""
+    n, nin = k + m, len(ins)
+    c = O.Clay(k, m, list(erased))
+    inputs = [None if (i % n) in erased else np.zeros(nin, np.uint8) for i in range(n * c.alpha)]
+    for j, slot in enumerate(ins):
+        inputs[slot][j] = 1
+    outs = [np.zeros(nin, np.uint8) for _ in range(len(erased) * c.alpha)]
+    c.perform_coding(inputs, outs, nin)
+    return np.stack(outs)
+
+
+@pytest.mark.parametrize("name,erased", [("repair_e1", [1]), ("repair_e4", [4]), ("encode_45", [4, 5])])
+def test_clay42_maps_equal_closed_form(ecx, name, erased):
+    """An independent pin against a shared misreading of ClayCodeErasureDecodingStep.java
+    by the planner and the oracle (both restate its stage sequence): the full Clay(4,2)
+    repair maps of nodes 1 and 4 (8 x 20) and the encode map (16 x 32), derived in closed
+    form from the pair-transform equations, the helper-plane set and the RS(4,2)
+    generator alone (tests/golden/gen_clay42_maps.py, committed as
+    tests/golden/clay42_closed_form.json), equal entry for entry the planner's composed map
+    (ecx_clay_map) and the oracle's, read off by unit vectors."""
+    import json
+    d = json.loads((ROOT / "tests" / "golden" / "clay42_closed_form.json").read_text())[name]
+    want = {(o, i): c for o, i, c in zip(d["out"], d["in"], d["coef"])}
+    mat, ins, outs = ecx.ClayCodeErasureDecodingStep(erased, 4, 2).map().matrix()
+    probed = _probe_oracle_map(4, 2, erased, ins.tolist())
+    for mm in (mat, probed):
+        got = {(int(outs[o]), int(ins[i])): int(mm[o, i]) for o in range(mm.shape[0]) for i in range(mm.shape[1])
+               if mm[o, i]}
+        assert got == want
+    assert d["nnz"] == (144 if name == "encode_45" else 52)
 
 
 def test_clay124_map_shape(ecx):
