@@ -18,19 +18,11 @@
  *   "xcd_misaligned"   single-tile maps with "xcd_group" 0 whose input slots are not 128-B aligned
  *                      (their chunks share boundary cache lines): 1 = use the runs of "xcd_group" 3
  *                      (default), 0 = the identity block order
- *   "wave_groups"      multi-tile maps: one workgroup per group of tiles sharing inputs, one
- *                      wave per tile, 1 KiB chunks: 1 = the group's input union staged once
- *                      through LDS; 2 = each wave loads its own entries (no LDS, no barriers);
- *                      0 = one workgroup per tile (default)
  *   "lds_tables"       0 = all split-table dwords read as scalars (one v_mov per 8-entry table
  *                      and row); 1 = the low dword of each 8-entry table staged per workgroup
  *                      in LDS, for multi-tile maps (default); 2 = for every map
  *   "store_scope"      0 = non-temporal output stores (`nt`, default); 1 = `nt sc0 sc1`
  *                      (system scope: written through, dropped from L2)
- *   "occ_lds"          extra dynamic LDS bytes per k_gf_apply workgroup, which caps the workgroups
- *                      resident per CU at floor(160 KiB / bytes): 0 = no cap (default), -1 = the
- *                      single-tile maps over >= 8 inputs on rings of <= 8 loads at 4 waves per
- *                      SIMD, 1..65536 = that many bytes
  *   "chunk_major"      block order of the one-workgroup-per-tile kernel: 0 = stripe-major
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
  *   "stagger"          unit order of the single-tile kernels (k_gf_apply, k_gf_apply_skew): 0 = none
@@ -63,15 +55,6 @@
  *   "wide_tiles"       multi-tile maps: pairs of 8-row tiles that share inputs in one workgroup
  *                      (16 accumulator rows, each shared input loaded once).  1 = when pairing
  *                      saves >= 1/6 of the input reads (default), 2 = always, 0 = never
- *   "bitslice"         the bit-sliced kernel (k_gf_bits: 32 bytes per lane as 8 bit planes, GF
- *                      multiplies as XORs of the planes of 2^k x) for the full 4 KiB chunks of
- *                      aligned layouts whose slot offsets fit 31 bits: 1 = for multi-tile maps
- *                      that do not run as wide tiles, 2 = for every such map, 0 = never (default;
- *                      measured slower, bound by its scalar branches)
- *   "lds_lut"          per-byte lookup tables in LDS (k_gf_lut) for the full 4 KiB chunks of
- *                      aligned layouts: 1 = log/antilog tables (LOG u16, EXP 1 KiB), 2 = one 256-B
- *                      product row per coefficient (single-tile maps of <= 256 general
- *                      coefficients); 0 = never (default: measured slower, DESIGN.md 4.4)
  *   "clay_rtc"         Clay single-node repair batches (ecx_clay_perform_coding_batch): the
  *                      per-helper-plane kernel generated for the repair and compiled with hiprtc, for
  *                      the whole 4 KiB chunks of 16-B-aligned layouts: 1 = when the composed map spans
@@ -86,12 +69,8 @@
  *                      = a second body for plane groups whose memory-row partner is virtual, bit 3 =
  *                      every load issued at the start, bit 4 = DIAGNOSTIC data-movement-only build
  *                      (coefficients taken as 1, no transposes: the outputs are not the repair;
- *                      refused with ECX_E_ILLEGAL_ARGUMENT unless the environment has ECX_DIAGNOSTIC=1)
- *   "rtc_diag"         the plane-group kernel's DIAGNOSTIC builds, 0 = none (default); bits remove one
- *                      part each to price it (1 row-yc partner loads, 2 LDS exchange + barrier, 4
- *                      lane-row exchange, 8 output stores but one, 16 bit-plane transposes): the
- *                      outputs are not the repair, so any non-zero value is refused with
- *                      ECX_E_ILLEGAL_ARGUMENT unless the environment has ECX_DIAGNOSTIC=1
+ *                      refused with ECX_E_ILLEGAL_ARGUMENT except in the diagnostic library with
+ *                      ECX_DIAGNOSTIC=1 in the environment)
  *   "rtc_waves"        that kernel's __launch_bounds__ minimum waves per SIMD, 2..4 (default 3)
  *   "rtc_group"        Clay single-node repairs of q = 4 codes (Clay(12,4), shortened Clay(10,4)): 1 =
  *                      the plane-group kernel (k_clay_repair_grp: a q x q square of helper planes
@@ -103,15 +82,10 @@
  *                      after every node -- 119 VGPRs and 4 waves per SIMD instead of 154 and 3; 2 =
  *                      every load of a unit issued up front, the accumulators pinned (151 VGPRs;
  *                      default)
- *   "rtc_units"        the plane-group kernel's 512-B slices per workgroup: 1 (default), or 2 with the
- *                      second slice's first two rows loaded while the first slice finishes (software
- *                      pipelining across the exchange barrier; no persistent grid)
  *   "rtc_nt"           non-temporal loads in the generated Clay kernels, bits: plane-group kernel --
  *                      1 the sub-chunks read once (rows ya and yb, the column mates), 2 the row-yc
  *                      own sub-chunks (re-read as partners by the neighbouring plane groups), 4 the
  *                      row-yc partner loads; per-plane kernel -- 8 every load; 0..15, default 5
- *   "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
- *                      a persistent grid of that many workgroups per CU walking the units
  *   "rtc_xcd"          that kernel's block order: 1 = the helper planes of one (stripe, chunk) on one
  *                      XCD (their shared partner loads meet in its L2), 0 = plane-fastest; 2 = the
  *                      same, and for the plane-group kernel all slices and plane groups of one
@@ -141,6 +115,38 @@
  *   "host_zero_copy"   per-call host entry points on the gather path: 1 = the kernel reads and
  *                      writes the pinned staging area over PCIe (no DMA copies; default);
  *                      0 = one H2D and one D2H copy
+ *
+ * Diagnostic library only ("make DIAG=1" builds libecx_diag.so with the same ABI; load it with
+ * ECX_LIB_PATH).  These are the measured-and-rejected kernels and builds DESIGN.md section 4
+ * records; the product library libecx.so does not contain them and ecx_tune refuses their keys
+ * with ECX_E_ILLEGAL_ARGUMENT (ecx_build_diag() tells the two apart):
+ *   [DIAG] "wave_groups"      multi-tile maps: one workgroup per group of tiles sharing inputs, one
+ *                      wave per tile, 1 KiB chunks: 1 = the group's input union staged once
+ *                      through LDS; 2 = each wave loads its own entries (no LDS, no barriers);
+ *                      0 = one workgroup per tile (default)
+ *   [DIAG] "occ_lds"          extra dynamic LDS bytes per k_gf_apply workgroup, which caps the workgroups
+ *                      resident per CU at floor(160 KiB / bytes): 0 = no cap (default), -1 = the
+ *                      single-tile maps over >= 8 inputs on rings of <= 8 loads at 4 waves per
+ *                      SIMD, 1..65536 = that many bytes
+ *   [DIAG] "bitslice"         the bit-sliced kernel (k_gf_bits: 32 bytes per lane as 8 bit planes, GF
+ *                      multiplies as XORs of the planes of 2^k x) for the full 4 KiB chunks of
+ *                      aligned layouts whose slot offsets fit 31 bits: 1 = for multi-tile maps
+ *                      that do not run as wide tiles, 2 = for every such map, 0 = never (default;
+ *                      measured slower, bound by its scalar branches)
+ *   [DIAG] "lds_lut"          per-byte lookup tables in LDS (k_gf_lut) for the full 4 KiB chunks of
+ *                      aligned layouts: 1 = log/antilog tables (LOG u16, EXP 1 KiB), 2 = one 256-B
+ *                      product row per coefficient (single-tile maps of <= 256 general
+ *                      coefficients); 0 = never (default: measured slower, DESIGN.md 4.4)
+ *   [DIAG] "rtc_diag"         the plane-group kernel's DIAGNOSTIC builds, 0 = none (default); bits remove one
+ *                      part each to price it (1 row-yc partner loads, 2 LDS exchange + barrier, 4
+ *                      lane-row exchange, 8 output stores but one, 16 bit-plane transposes): the
+ *                      outputs are not the repair, so any non-zero value is refused with
+ *                      ECX_E_ILLEGAL_ARGUMENT unless the environment has ECX_DIAGNOSTIC=1
+ *   [DIAG] "rtc_units"        the plane-group kernel's 512-B slices per workgroup: 1 (default), or 2 with the
+ *                      second slice's first two rows loaded while the first slice finishes (software
+ *                      pipelining across the exchange barrier; no persistent grid)
+ *   [DIAG] "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
+ *                      a persistent grid of that many workgroups per CU walking the units
  */
 #ifndef ECX_TUNE_H
 #define ECX_TUNE_H
@@ -149,6 +155,8 @@
 extern "C" {
 #endif
 int ecx_tune(const char *key, int value); /* 0, or ECX_E_ILLEGAL_ARGUMENT for an unknown key */
+/* 1 in the diagnostic library (make DIAG=1, libecx_diag.so), 0 in the product library. */
+int ecx_build_diag(void);
 /* Pure-bandwidth probes over nbytes (multiple of 16 KiB) of device memory:
  * kind 0 = read-only stream, kind 1 = copy src -> dst.  Enqueued on `stream`. */
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream);

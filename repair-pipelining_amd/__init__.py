@@ -211,6 +211,14 @@ def tune(key: str, value: int) -> None:
     check(f(key.encode(), int(value)))
 
 
+def is_diag() -> bool:
+    """True for the diagnostic library (make DIAG=1, libecx_diag.so): it also holds the
+    measured-and-rejected kernels, whose ecx_tune keys the product library refuses."""
+    f = lib().ecx_build_diag
+    f.argtypes, f.restype = [], ctypes.c_int
+    return f() == 1
+
+
 def last_kernel() -> str:
     """The kernel instance of this thread's last full-chunk launch, as rocprofv3 names it
     (ecx_last_kernel, include/ecx_tune.h); "" before the first launch."""

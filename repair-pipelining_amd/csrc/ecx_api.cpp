@@ -1104,8 +1104,16 @@ bool diagnostic_builds_allowed() {
     return v && std::strcmp(v, "1") == 0;
 }
 
+// Knobs of the measured-and-rejected kernels and builds: accepted by
+// the diagnostic library only (`make DIAG=1`, libecx_diag.so).
+bool lab_key(const std::string &k) {
+    return k == "bitslice" || k == "lds_lut" || k == "wave_groups" || k == "rtc_units" || k == "rtc_persist" ||
+           k == "rtc_diag" || k == "occ_lds";
+}
+
 // One ecx_tune key, under the tuning lock.
 int set_tune(Tuning &t, const std::string &k, int value) {
+    if (!ECX_DIAG && lab_key(k)) return ECX_E_ILLEGAL_ARGUMENT;
     if (k == "depth") {
         if (value != 0 && value != 2 && value != 4 && value != 8 && value != 10 && value != 12 && value != 16 &&
             value != 20 && value != 24)
@@ -1186,8 +1194,8 @@ int set_tune(Tuning &t, const std::string &k, int value) {
     else if (k == "rtc_lookahead") {
         if (value < 0 || value > 31) return ECX_E_ILLEGAL_ARGUMENT;
         // bit 4 is the DIAGNOSTIC movement-only build, whose outputs are not the repair:
-        // refused unless the process opted in with ECX_DIAGNOSTIC=1
-        if ((value & 16) && !diagnostic_builds_allowed()) return ECX_E_ILLEGAL_ARGUMENT;
+        // refused unless this is the diagnostic library and the process opted in with ECX_DIAGNOSTIC=1
+        if ((value & 16) && !(ECX_DIAG && diagnostic_builds_allowed())) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_lookahead = value;
     }
     else if (k == "rtc_xcd") {
@@ -1282,6 +1290,8 @@ int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_
     });
 }
 
+int ecx_build_diag(void) { return ECX_DIAG ? 1 : 0; }
+
 int ecx_map_layout_choice(const ecx_map *map, int64_t slot_pitch, float *median_ms, int n) {
     if (!map || slot_pitch <= 0 || n < 0) return ECX_E_ILLEGAL_ARGUMENT;
     std::vector<float> ms;
@@ -1366,6 +1376,7 @@ int ecx_map_selftest(const ecx_map *map, uint64_t seed) {
                     bref[(size_t)m.out_slot[o] * blen + i] ^= f.mul(c, bin[(size_t)m.in_slot[j] * blen + i]);
             }
         for (int depth : {2, 4}) {
+            if (!ECX_DIAG) break;  // bit-sliced entries exist in the diagnostic build only
             std::vector<uint8_t> got(bref.size(), 0);
             cm.emulate_bits(cm.padded_plan(depth), bin.data(), got.data(), blen);
             for (int o = 0; o < m.n_out; ++o)

@@ -448,9 +448,9 @@ HostPlan CompiledMap::padded_plan(int depth) const {
             p.atab.push_back(p.entries[e * kEntryDwords + 4 + 5 * r]);      // T0a
             p.atab.push_back(p.entries[e * kEntryDwords + 4 + 5 * r + 2]);  // T1a
         }
-    // Bit-sliced entries: the coefficient of each row, recovered from its table
-    // (T0a byte 1 = c * 1), or 1 for a plain-XOR row.
-    for (size_t e = 0; e < p.entries.size() / kEntryDwords; ++e) {
+    // Bit-sliced entries (k_gf_bits, diagnostic build only): the coefficient of each row,
+    // recovered from its table (T0a byte 1 = c * 1), or 1 for a plain-XOR row.
+    for (size_t e = 0; ECX_DIAG && e < p.entries.size() / kEntryDwords; ++e) {
         const uint32_t *rec = p.entries.data() + e * kEntryDwords;
         uint32_t coef[2] = {0u, 0u};
         for (int r = 0; r < kTileRows; ++r) {
@@ -628,7 +628,7 @@ const DevicePlan &CompiledMap::plan_for_current_device(int depth) {
     upload(&p.atab, h.atab, "hipMalloc(plan atab)");
     upload(&p.wentries, h.wentries, "hipMalloc(plan wide entries)");
     upload(&p.wtiles, h.wtiles, "hipMalloc(plan wide tiles)");
-    upload(&p.bentries, h.bentries, "hipMalloc(plan bit-sliced entries)");
+    if (!h.bentries.empty()) upload(&p.bentries, h.bentries, "hipMalloc(plan bit-sliced entries)");
     return dev_.emplace(std::make_pair(dev, depth), p).first->second;
 }
 

@@ -18,6 +18,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef ECX_DIAG
+#define ECX_DIAG 0  // 1: the diagnostic build (Makefile DIAG=1) with the measured-and-rejected kernels
+#endif
+
 #include <array>
 #include <cstdint>
 #include <map>

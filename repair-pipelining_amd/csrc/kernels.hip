@@ -21,6 +21,7 @@
 
 namespace ecx {
 
+#if ECX_DIAG  // measured and rejected: `make DIAG=1` only
 // Multi-tile maps: one workgroup = one (stripe, 1 KiB chunk, tile GROUP), one
 // wave per tile.  The tiles of a group share inputs (Clay(10,4): 8 tiles read
 // 208 distinct inputs 320 times), so instead of each wave loading its own
@@ -118,6 +119,7 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
         }
     }
 }
+#endif  // ECX_DIAG
 
 // Wide tiles: one 256-thread workgroup = one (stripe, 4 KiB chunk, pair of 8-row
 // tiles A and B).  Each input of the pair's union is loaded once and applied to
@@ -206,6 +208,7 @@ __global__ void __launch_bounds__(kBlockThreads, 4) k_gf_apply_wide(ApplyArgs a)
     }
 }
 
+#if ECX_DIAG  // measured and rejected: `make DIAG=1` only
 // Multi-tile maps, tile groups without staging: one workgroup = one (stripe, 1 KiB
 // chunk, tile GROUP), one wave per tile, each wave loading its own entries directly.
 // The group's tiles share inputs, and each tile's entry list is ordered by the
@@ -235,6 +238,7 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
         a, plan_ptr(a.tiles) + tl * kTileDwords, uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
         uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)), lane16, valid, nullptr);
 }
+#endif  // ECX_DIAG
 
 namespace {
 // pick: -1 = the static rules (skew on 4 MiB-multiple input slot pitches, one-wave
@@ -246,7 +250,9 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                        int64_t nbytes, hipStream_t stream, bool accumulate, int pick) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
     const Tuning &tu = tuning();
-    const bool waves = cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
+    // (the lab kernels -- tile groups, bit-sliced, LDS lookup tables, residency caps -- exist
+    // only in the diagnostic build, `make DIAG=1`; their knobs are refused otherwise)
+    const bool waves = ECX_DIAG && cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
     // Non-temporal policy: 0 never; 1 auto (NT stores, NT loads for single-tile maps); 2 always.
     const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (cm.n_tiles() == 1 ? 2 : 1) : 0);
     const int nts = ntmode == 0 ? 0 : (tu.store_scope ? 2 : 1);
@@ -315,7 +321,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     // (the chunk accounting below is in 4 KiB chunks only for 256-thread shapes)
     const bool bits_ok = aligned && offsets32 && !waves && threads == kBlockThreads && ntmode != 0 &&
                          nbytes >= kChunkBytes;
-    bool bits = bits_ok && !skew &&
+    bool bits = ECX_DIAG && bits_ok && !skew &&
                       (tu.bitslice == 2 || (tu.bitslice == 1 && cm.n_tiles() > 1 && !wide));
     if (bits) {
         depth = tu.depth == 2 ? 2 : 4;
@@ -357,7 +363,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     if (tu.lds_lut == 2)
         for (int o = 0; o < cm.map().n_out; ++o)
             for (int j = 0; j < cm.map().n_in; ++j) lut_pairs += cm.map().at(o, j) > 1;
-    const bool lut = tu.lds_lut && aligned && !waves && nbytes >= kChunkBytes && threads == kBlockThreads &&
+    const bool lut = ECX_DIAG && tu.lds_lut && aligned && !waves && nbytes >= kChunkBytes && threads == kBlockThreads &&
                      (tu.lds_lut == 1 || (cm.n_tiles() == 1 && lut_pairs <= kLutMaxPairs));
     if (lut) {
         planes = bits = wide = false;
@@ -416,6 +422,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
             const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
             a.stripe_begin = s0;
             const dim3 grid((unsigned)(ns * per_stripe));
+#if ECX_DIAG
             if (waves) {
                 const dim3 blk(64 * cm.group_size());
                 if (!safe) note_kernel(tu.wave_groups == 2 ? "k_gf_apply_grp" : "k_gf_apply_lds", false, depth == 8 ? 8 : 4);
@@ -435,6 +442,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                 launch_bits(ntmode == 2, depth, grid, stream, a);
                 continue;
             }
+#endif  // ECX_DIAG
             if (wide) {
                 const dim3 blk(kBlockThreads);
                 const bool ntl = ntmode == 2 || (ntmode == 1 && a.n_wide == 1);  // one pair: no re-reads
@@ -464,8 +472,8 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
             // Residency cap (ecx_tune "occ_lds"): dummy LDS per workgroup.  Auto: the many-stream
             // single-tile maps (>= 8 inputs, rings of <= 8 loads) at 4 waves per SIMD -- 4
             // 256-thread or 16 one-wave workgroups per CU -- instead of the 5 their registers allow.
-            size_t occ = tu.occ_lds > 0 ? (size_t)tu.occ_lds : 0;
-            if (tu.occ_lds < 0 && !safe && a.n_tiles == 1 && cm.map().n_in >= 8 && depth <= 8)
+            size_t occ = ECX_DIAG && tu.occ_lds > 0 ? (size_t)tu.occ_lds : 0;
+            if (ECX_DIAG && tu.occ_lds < 0 && !safe && a.n_tiles == 1 && cm.map().n_in >= 8 && depth <= 8)
                 occ = kLdsPerCu / (kOccWavesPerSimd * kSimdsPerCu / (threads / 64));
             const size_t lds = (s.tlds ? (size_t)plan.max_tile_entries * kAtabDwords * 4 : 0) + occ;
             if (threads == 64) launch_shape_t<64>(s, grid, lds, stream, a);
@@ -473,6 +481,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         }
     };
     int64_t first = 0;  // first full chunk left to the one-chunk kernels
+#if ECX_DIAG
     if (lut) {
         a.chunk_begin = 0;
         a.n_chunks = full;
@@ -480,6 +489,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         launch_lut(tu.lds_lut - 1, ntmode == 2, lut_pairs, nstripes * full * a.n_tiles, stream, a);
         first = full;
     }
+#endif
     if (planes) {
         const int64_t n4k = nbytes / kChunkBytes;
         cm.planes()->launch(in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes, n4k,

@@ -198,11 +198,37 @@ __global__ void __launch_bounds__(256) k_rot(uint8_t *pool, Slots s) {
         for (int r = 0; r < NO; ++r) stnt(base + s.out_slot[r] + k * 4096, acc[k][r]);
 }
 
+// The same with one-wave workgroups over 1 KiB chunks (the one-wave kernels' shape): K
+// consecutive 1 KiB chunks per workgroup, stream i read at chunk (i + t) mod K in phase t.
+template <int NI, int NO, int K>
+__global__ void __launch_bounds__(64) k_rot_wave(uint8_t *pool, Slots s) {
+    const int64_t groups = s.chunks * 4 / K;  // 1 KiB chunks
+    const int64_t stripe = blockIdx.x / groups, g = blockIdx.x % groups;
+    uint8_t *base = pool + stripe * s.stripe_bytes + g * (K * 1024) + threadIdx.x * 16;
+    u32x4 acc[K][NO];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int r = 0; r < NO; ++r) acc[k][r] = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+        u32x4 x[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) x[i] = ldnt(base + s.in_slot[i] + ((i + t) % K) * 1024);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[(i + t) % K][i % NO] ^= x[i];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int r = 0; r < NO; ++r) stnt(base + s.out_slot[r] + k * 1024, acc[k][r]);
+}
+
 static int run_rot(uint8_t *pool, int64_t pool_bytes) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    struct R { const char *name; int ni, no, k; int64_t pitch; Slots s; uint32_t stripes; std::vector<float> ms; };
+    struct R { const char *name; int ni, no, k; int64_t pitch; Slots s; uint32_t stripes; std::vector<float> ms; bool wave = false; };
     std::vector<R> rs;
     auto add = [&](const char *name, int ni, int no, int64_t pitch, std::vector<int> ks) {
         for (int k : ks) {
@@ -219,12 +245,26 @@ static int run_rot(uint8_t *pool, int64_t pool_bytes) {
     };
     for (int64_t p : {4ll << 20, (4ll << 20) + 4096, 1ll << 20, (1ll << 20) + 4096, 8ll << 20})
         add("rs124", 12, 2, p, {1, 2, 4, 8, 12, 16});
+    const size_t n256 = rs.size();
+    for (int64_t p : {4ll << 20, (4ll << 20) + 4096, (1ll << 20) + 4096})
+        add("rs124_wave", 12, 2, p, {1, 2, 4, 8, 12, 16});
+    for (size_t i = n256; i < rs.size(); ++i) {
+        rs[i].wave = true;
+        rs[i].s.chunks = (int)(rs[i].pitch / 1024) / rs[i].k * rs[i].k / 4;  // in 4 KiB units (1 KiB chunks / 4)
+    }
     add("rs173", 17, 3, 200000, {1, 2, 4, 8});
     add("rs173", 17, 3, 262144, {1, 2, 4, 8});
     for (int round = 0; round < 5; ++round)
         for (auto &r : rs) {
-            const dim3 grid(r.stripes * (uint32_t)(r.s.chunks / r.k));
+            const dim3 grid(r.wave ? r.stripes * (uint32_t)(r.s.chunks * 4 / r.k) : r.stripes * (uint32_t)(r.s.chunks / r.k));
             auto launch = [&]() {
+                if (r.wave) {
+#define ROTW(K) \
+    if (r.k == K) hipLaunchKernelGGL((k_rot_wave<12, 2, K>), grid, dim3(64), 0, 0, pool, r.s);
+                    ROTW(1) ROTW(2) ROTW(4) ROTW(8) ROTW(12) ROTW(16)
+#undef ROTW
+                    return;
+                }
 #define ROT(NI, NO, K) \
     if (r.ni == NI && r.k == K) hipLaunchKernelGGL((k_rot<NI, NO, K>), grid, dim3(256), 0, 0, pool, r.s);
                 ROT(12, 2, 1) ROT(12, 2, 2) ROT(12, 2, 4) ROT(12, 2, 8) ROT(12, 2, 12) ROT(12, 2, 16)

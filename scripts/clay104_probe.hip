@@ -11,6 +11,8 @@
 //          (k_clay_repair_grp's shape, without exchanges or partners).
 //   planesK[_wave]  K consecutive helper planes per workgroup, all 13K loads of a lane in
 //          flight at once, 256-thread workgroups over 4 KiB or one wave over 1 KiB.
+//   wave4k_ringD  one wave per helper plane over whole 4 KiB sub-chunks: 52 loads per lane
+//          through a ring of D (8-24) in flight.
 // Each with the identity block order and with a stripe's workgroups on one XCD.  Prints
 // algorithmic GB/s ((832 + 256) x 4 KiB per stripe) as a fraction of 8 TB/s.
 //
@@ -122,6 +124,49 @@ __global__ void __launch_bounds__(THREADS) k_planes(const uint8_t *pool, uint8_t
     }
 }
 
+// One wave per (stripe, helper plane) over WHOLE 4 KiB sub-chunks: lane l owns bytes
+// l*16 + k*1 KiB (k = 0..3) of each of the plane's 13 helper sub-chunks, i.e. 52 loads per
+// lane, issued through a ring of DEPTH in flight (software-pipelined, fully unrolled, so
+// every vmcnt is a constant), folded into 4 slices x 4 outputs.  Round 3's review asked
+// whether more helper loads per lane in flight than the 13 of plane_wave raise the
+// pattern's ceiling.
+template <int DEPTH>
+__global__ void __launch_bounds__(64) k_wave_ring(const uint8_t *pool, uint8_t *out, uint32_t n) {
+    constexpr int NL = 52;
+    const uint32_t u = blockIdx.x;
+    const int64_t s = u / kHelp, p = u % kHelp, z = 192 + p;
+    // wave-uniform plane base in SGPRs + the lane's 16 B: each load is a global load with an
+    // SGPR base and a 32-bit VGPR offset, so the 52 addresses cost no VGPRs
+    const uint64_t b64 = (uint64_t)(pool + s * kStripe + z * kNodes * kSub);
+    const uint8_t *sbase = reinterpret_cast<const uint8_t *>(
+        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b64 >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)b64));
+    uint32_t voff = threadIdx.x * 16;
+    auto ld = [&](int i) -> u32x4 {  // load i: slice i / 13, helper node i % 13, non-temporal
+        const int j = i % 13, k = i / 13;
+        return ldnt(sbase + (j < 3 ? j : j + 1) * kSub + k * 1024 + voff);
+    };
+    u32x4 ring[DEPTH];
+#pragma unroll
+    for (int i = 0; i < DEPTH; ++i) ring[i] = ld(i);
+    u32x4 acc[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[k][r] = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const u32x4 v = ring[i % DEPTH];
+        if (i + DEPTH < NL) ring[i % DEPTH] = ld(i + DEPTH);
+        acc[i / 13][(i % 13) & 3] ^= v;
+        asm volatile("" : "+v"(voff) : "v"(v.x));  // later addresses wait for load i: DEPTH in flight
+    }
+    uint8_t *o = out + s * kOut + threadIdx.x * 16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stnt(o + (p + 64 * r) * kSub + k * 1024, acc[k][r]);
+}
+
 template <typename F>
 float best_ms(F launch) {
     hipEvent_t e0, e1;
@@ -149,8 +194,9 @@ int main() {
     for (int round = 0; round < 2; ++round) {
         const uint32_t np = (uint32_t)(S * kHelp), ng = (uint32_t)(S * 32);
         const char *names[] = {"plane", "plane_xcd", "group", "group_xcd", "plane_readonly", "plane_out_contig",
-                               "plane_read14", "planes2", "planes4", "plane_wave", "planes2_wave"};
-        float ms[11];
+                               "plane_read14", "planes2", "planes4", "plane_wave", "planes2_wave",
+                               "wave4k_ring8", "wave4k_ring13", "wave4k_ring16", "wave4k_ring20", "wave4k_ring24"};
+        float ms[16];
         ms[0] = best_ms([&] { hipLaunchKernelGGL((k_plane<0>), dim3(np), dim3(256), 0, 0, pool, out, np); });
         ms[1] = best_ms([&] { hipLaunchKernelGGL((k_plane<1>), dim3(np), dim3(256), 0, 0, pool, out, np); });
         ms[2] = best_ms([&] { hipLaunchKernelGGL((k_group<0>), dim3(ng), dim3(256), 0, 0, pool, out, ng); });
@@ -162,7 +208,12 @@ int main() {
         ms[8] = best_ms([&] { hipLaunchKernelGGL((k_planes<4, 256>), dim3(np / 4), dim3(256), 0, 0, pool, out, np / 4); });
         ms[9] = best_ms([&] { hipLaunchKernelGGL((k_planes<1, 64>), dim3(np * 4), dim3(64), 0, 0, pool, out, np * 4); });
         ms[10] = best_ms([&] { hipLaunchKernelGGL((k_planes<2, 64>), dim3(np * 2), dim3(64), 0, 0, pool, out, np * 2); });
-        for (int i = 0; i < 11; ++i) {
+        ms[11] = best_ms([&] { hipLaunchKernelGGL((k_wave_ring<8>), dim3(np), dim3(64), 0, 0, pool, out, np); });
+        ms[12] = best_ms([&] { hipLaunchKernelGGL((k_wave_ring<13>), dim3(np), dim3(64), 0, 0, pool, out, np); });
+        ms[13] = best_ms([&] { hipLaunchKernelGGL((k_wave_ring<16>), dim3(np), dim3(64), 0, 0, pool, out, np); });
+        ms[14] = best_ms([&] { hipLaunchKernelGGL((k_wave_ring<20>), dim3(np), dim3(64), 0, 0, pool, out, np); });
+        ms[15] = best_ms([&] { hipLaunchKernelGGL((k_wave_ring<24>), dim3(np), dim3(64), 0, 0, pool, out, np); });
+        for (int i = 0; i < 16; ++i) {
             // read-only: the 832 read sub-chunks only; read14: 896 read + 256 written
             const double b = i == 4 ? (double)S * 832 * kSub : (i == 6 ? (double)S * (896 + 256) * kSub : bytes);
             printf("{\"round\": %d, \"shape\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", round,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session on the MI355X box.  Modes (any of; run in this order): test pmc bench gloo2 workloads refcpu prof
+# One GPU session on the MI355X box.  Modes (any of; run in this order): test diag pmc bench gloo2 workloads refcpu prof
 # Every GPU step has its own time limit; a fault/abort/timeout stops the script.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -16,6 +16,14 @@ if has test; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread \
       > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && stop pytest $rc
+fi
+if has diag; then
+  # the measured-and-rejected kernels, in the diagnostic library (make DIAG=1): the tests marked
+  # `diag` and the lab variants of the mixed tests
+  ECX_LIB_PATH="$ROOT/repair-pipelining_amd/libecx_diag.so" timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf \
+      --timeout 120 --timeout-method thread -k "diag or bitslice or lds_lut or multitile_launch or random_maps or clay_rtc_kernel or two_slice" \
+      > "$OUT/pytest_gpu_diag.log" 2>&1
+  rc=$?; echo "pytest gpu diag rc=$rc"; tail -3 "$OUT/pytest_gpu_diag.log"; [ $rc -ne 0 ] && stop pytest_diag $rc
 fi
 if has pmc; then
   bash "$ROOT/scripts/pmc.sh" || stop pmc $?

@@ -39,6 +39,11 @@ SETS = {
     "default": [{}],
     # the per-layout selection (default) against the static rules alone
     "select": [{}, {"layout_select": 0}],
+    # unit orders without the XCD runs that misaligned layouts get by default (RS(17,3) at 200,000 B)
+    "misaligned": [{}, {"layout_select": 0}, {"xcd_misaligned": 0, "layout_select": 0},
+                   {"stagger": 8, "xcd_misaligned": 0}, {"stagger": 4, "xcd_misaligned": 0},
+                   {"stagger": 16, "xcd_misaligned": 0}, {"stagger": 8, "xcd_misaligned": 0, "block_threads": 64},
+                   {"xcd_group": 3, "xcd_run": 32, "layout_select": 0}, {"xcd_group": 3, "xcd_run": 128, "layout_select": 0}],
 }
 
 

@@ -13,6 +13,21 @@ for p in (ROOT, ROOT / "oracle"):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "diag: needs the diagnostic library (make DIAG=1; ECX_LIB_PATH=.../libecx_diag.so)")
+
+
+def pytest_runtest_setup(item):
+    """Tests of the measured-and-rejected kernels (marked `diag`) run only against the
+    diagnostic library; the product library does not contain those kernels."""
+    if item.get_closest_marker("diag"):
+        import rpamd
+        if not rpamd.load().is_diag():
+            pytest.skip("diagnostic-library kernel (make DIAG=1, ECX_LIB_PATH=.../libecx_diag.so)")
+
+
+def diag_build() -> bool:
+    import rpamd
+    return rpamd.load().is_diag()
 
 
 @pytest.fixture(scope="session")

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(ecx):
     assert headers == ["ecx.h", "ecx_tune.h"]
     missing = [s for h in headers for s in declared_symbols(h) if not hasattr(lib, s)]
     assert not missing, missing
-    assert len(declared_symbols("ecx_tune.h")) == 11
+    assert len(declared_symbols("ecx_tune.h")) == 12
 
 
 def test_binding_table_matches_header(ecx):
@@ -152,8 +152,12 @@ def test_tuning_keys(ecx):
     tune.argtypes, tune.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
     header = (ROOT / "include" / "ecx_tune.h").read_text()
     documented = re.findall(r'^ \*\s+"([a-z_]+)"', header, flags=re.M)
-    defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "wave_groups": 0, "lds_tables": 1, "store_scope": 0, "occ_lds": 0,
-                "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "bitslice": 0, "lds_lut": 0, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_persist": 0, "rtc_units": 1, "rtc_sched": 2, "rtc_nt": 5, "rtc_diag": 0, "xcd_run": 8, "xcd_misaligned": 1,
+    lab = re.findall(r'^ \*\s+\[DIAG\] "([a-z_]+)"', header, flags=re.M)
+    assert sorted(lab) == sorted(["wave_groups", "occ_lds", "bitslice", "lds_lut", "rtc_diag", "rtc_units", "rtc_persist"])
+    for key in lab:  # the product library refuses them; the diagnostic one takes its defaults
+        assert tune(key.encode(), 1 if key == "rtc_units" else 0) == (0 if ecx.is_diag() else -1), key
+    defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0,
+                "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_sched": 2, "rtc_nt": 5, "xcd_run": 8, "xcd_misaligned": 1,
                 "map_planes": 1, "planes_lookahead": 12, "planes_waves": 2,
                 "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512}
     assert sorted(documented) == sorted(defaults)

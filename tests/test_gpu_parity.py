@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from conftest import shortened_clay_oracle
+from conftest import diag_build, shortened_clay_oracle
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -739,10 +739,13 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
                                    (0, 2, 0, 0, 256, 0), (0, 1, 1, 0, 256, 0), (0, 1, 0, 1, 256, 0),
                                    (0, 1, 0, 0, 64, 0), (0, 2, 0, 1, 64, 0), (2, 1, 0, 0, 256, 0),
                                    (0, 1, 0, 0, 256, 2), (0, 1, 0, 0, 256, -1)):
+        if wg and not diag_build():
+            continue  # the tile-group kernels are in the diagnostic library only (make DIAG=1)
         # wd < 0: the generated bit-plane kernel forced (ecx_tune "map_planes" 2; maps of <= 16 rows)
         ecx.tune("map_planes", 2 if wd < 0 else 0)
         wd = max(wd, 0)
-        ecx.tune("wave_groups", wg)
+        if diag_build():
+            ecx.tune("wave_groups", wg)
         ecx.tune("lds_tables", lt)
         ecx.tune("store_scope", sc)
         ecx.tune("chunk_major", cm)
@@ -752,7 +755,8 @@ def test_multitile_launch_shapes_agree(ecx, torch_dev, k, m, v, erased, B):
         step.performCodingBatch(pool, n * a * B, B, o, len(erased) * a * B, B, S, B)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
-    ecx.tune("wave_groups", 0)  # the defaults
+    if diag_build():
+        ecx.tune("wave_groups", 0)  # the defaults
     ecx.tune("lds_tables", 1)
     ecx.tune("store_scope", 0)
     ecx.tune("chunk_major", 0)
@@ -928,8 +932,12 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
                                   (4, 0, 256, 2, 0), (8, 0, 256, 2, 0), (8, 0, 256, 0, 2), (4, 0, 256, 0, 4),
                                   (10, 0, 256, 0, 0), (12, 0, 256, 0, 0), (16, 0, 256, 0, 0), (20, 0, 256, 0, 0),
                                   (24, 0, 256, 0, 0), (20, 2, 256, 0, 0), (4, 0, 256, 0, -2), (2, 0, 256, 0, -2)):
-        # sk < 0: the bit-sliced kernel forced (ecx_tune "bitslice" 2), at ring depth 4 / 2
-        ecx.tune("bitslice", 2 if sk < 0 else 0)
+        # sk < 0: the bit-sliced kernel forced (ecx_tune "bitslice" 2), at ring depth 4 / 2 --
+        # in the diagnostic library only (make DIAG=1)
+        if sk < 0 and not diag_build():
+            continue
+        if diag_build():
+            ecx.tune("bitslice", 2 if sk < 0 else 0)
         sk = max(sk, 0)
         ecx.tune("depth", depth)
         ecx.tune("lds_tables", lt)
@@ -948,7 +956,8 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
     ecx.tune("block_threads", 0)
     ecx.tune("wide_tiles", 1)
     ecx.tune("skew_chunks", 1)
-    ecx.tune("bitslice", 0)
+    if diag_build():
+        ecx.tune("bitslice", 0)
 
 
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
@@ -1252,6 +1261,7 @@ def test_multitile_slot_offset_near_2gib(ecx, torch_dev, stride):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("case", ["clay104", "clay42", "rs124", "dense40x24", "ones"])
 @pytest.mark.parametrize("depth", [2, 4])
 def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
@@ -1298,6 +1308,7 @@ def test_bitslice_kernel_vs_table_product(ecx, torch_dev, case, depth):
             assert bad.size == 0, (case, s, o, bad[:8], got[s, slot][bad[:8]], ref[o][bad[:8]])
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("case", ["clay104", "clay42", "rs124", "dense40x24", "ones", "dense8x30"])
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("acc", [False, True])
@@ -1377,15 +1388,18 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
     modes = [(0, 0, 0, 0, 1), (2, 0, 0, 0, 1), (2, 1, 0, 0, 1)]  # composed; per-plane, both block orders
     if m == 4:
         # the plane-group kernel: both block orders, persistent grid, every schedule bit
-        modes += [(2, 0, 1, 0, 1), (2, 1, 1, 0, 1), (2, 2, 1, 0, 1), (2, 3, 1, 0, 1), (2, 4, 1, 0, 1), (2, 1, 1, 2, 1), (2, 1, 1, 0, 0),
+        modes += [(2, 0, 1, 0, 1), (2, 1, 1, 0, 1), (2, 2, 1, 0, 1), (2, 3, 1, 0, 1), (2, 4, 1, 0, 1), (2, 1, 1, 0, 0),
                   (2, 1, 1, 0, 3), (2, 1, 1, 0, 5), (2, 1, 1, 0, 6), (2, 1, 1, 0, 12)]
+        if diag_build():
+            modes += [(2, 1, 1, 2, 1)]  # the persistent grid: diagnostic library only
     outs = {}
     try:
         for rtc, xcd, grp, persist, la in modes:
             ecx.tune("clay_rtc", rtc)
             ecx.tune("rtc_xcd", xcd)
             ecx.tune("rtc_group", grp)
-            ecx.tune("rtc_persist", persist)
+            if diag_build():
+                ecx.tune("rtc_persist", persist)
             ecx.tune("rtc_lookahead", la)
             ecx.tune("rtc_sched", 2 if la == 1 else 0)  # the default schedule, and rtc_lookahead's for the rest
             o = torch.full((S, a, B), 0x77, dtype=torch.uint8, device="cuda")
@@ -1396,7 +1410,8 @@ def test_clay_rtc_kernel_vs_composed_and_oracle(ecx, torch_dev, k, m, v, e, B, S
         ecx.tune("clay_rtc", 1)
         ecx.tune("rtc_xcd", 2)
         ecx.tune("rtc_group", 1)
-        ecx.tune("rtc_persist", 0)
+        if diag_build():
+            ecx.tune("rtc_persist", 0)
         ecx.tune("rtc_lookahead", 1)
         ecx.tune("rtc_sched", 2)
     ref0 = outs[(0, 0, 0, 0, 1)][0]
@@ -1801,7 +1816,10 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
                                              (2, 3, 2, 0, 1), (2, 4, 3, 0, 1), (2, 0, 2, 0, 1), (1, 2, 4, 1, 1),
                                              (1, 2, 3, 1, 0), (1, 3, 4, 1, 3), (2, 2, 3, 1, 2), (1, 2, 4, 2, 0),
                                              (2, 2, 2, 2, 1)]:
-            ecx.tune("rtc_units", units)
+            if units == 2 and not diag_build():
+                continue  # two-slice units: diagnostic library only (make DIAG=1)
+            if diag_build():
+                ecx.tune("rtc_units", units)
             ecx.tune("rtc_xcd", xcd)
             ecx.tune("rtc_waves", waves)
             ecx.tune("rtc_sched", sched)
@@ -1812,7 +1830,8 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
             assert ecx.last_kernel() == "k_clay_repair_grp"
             outs.append(o.cpu().numpy())
     finally:
-        ecx.tune("rtc_units", 1)
+        if diag_build():
+            ecx.tune("rtc_units", 1)
         ecx.tune("rtc_xcd", 2)
         ecx.tune("rtc_waves", 3)
         ecx.tune("rtc_sched", 2)
@@ -1821,7 +1840,7 @@ def test_clay_grp_two_slice_units_vs_oracle(ecx, torch_dev, e, B, S):
     host = pool[S - 1].cpu().numpy()
     inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
     ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
-    assert all((outs[1][S - 1, z] == ref[z]).all() for z in range(a))
+    assert all((outs[0][S - 1, z] == ref[z]).all() for z in range(a))
 
 
 @pytest.mark.parametrize("e,B,S", [(3, 4096, 5), (11, 4096 + 48, 3)])

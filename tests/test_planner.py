@@ -310,8 +310,11 @@ def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
     step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
     try:
         for grp, persist, nt in ((1, 0, 0), (1, 2, 0), (0, 0, 0), (1, 0, 7), (1, 0, 1), (0, 0, 8), (0, 0, 5), (1, 0, 5)):
+            if persist and not ecx.is_diag():
+                continue  # the persistent grid: diagnostic library only (make DIAG=1)
             ecx.tune("rtc_group", grp)
-            ecx.tune("rtc_persist", persist)
+            if ecx.is_diag():
+                ecx.tune("rtc_persist", persist)
             ecx.tune("rtc_nt", nt)
             assert step.rtcCompileCheck() > 0
             src = step.rtcSource()
@@ -327,7 +330,8 @@ def test_clay_repair_program_and_rtc_compile(ecx, k, m, v, e):
                 assert ("(int)so, 2);" in src) == (nt & 8 > 0)
     finally:
         ecx.tune("rtc_group", 1)
-        ecx.tune("rtc_persist", 0)
+        if ecx.is_diag():
+            ecx.tune("rtc_persist", 0)
         ecx.tune("rtc_nt", 5)
 
 
@@ -377,6 +381,25 @@ def test_map_planes_refuses_wide_maps(ecx):
         gm.planes_source()
 
 
+def test_lab_knobs_refused_by_the_product_library(ecx, monkeypatch):
+    """The product library (libecx.so) does not contain the measured-and-rejected kernels
+    and builds: ecx_tune refuses their keys, at any value, even with
+    ECX_DIAGNOSTIC=1 (which only opens the diagnostic library's output-changing builds)."""
+    if ecx.is_diag():
+        pytest.skip("the diagnostic library accepts these keys")
+    monkeypatch.setenv("ECX_DIAGNOSTIC", "1")
+    for key in ("bitslice", "lds_lut", "wave_groups", "rtc_units", "rtc_persist", "rtc_diag", "occ_lds"):
+        for val in (0, 1, 2):
+            with pytest.raises(ecx.EcxError) as e:
+                ecx.tune(key, val)
+            assert e.value.code == -1, key
+    with pytest.raises(ecx.EcxError):
+        ecx.tune("rtc_lookahead", 17)  # the data-movement-only Clay build
+    with pytest.raises(ecx.EcxError):
+        ecx.tune("skew_trial", 1)  # replaced by layout_select
+
+
+@pytest.mark.diag
 def test_clay_grp_movement_only_build_is_isolated(ecx, monkeypatch):
     """rtc_lookahead bit 4 (16) generates the plane-group kernel's data-movement-only
     diagnostic build (coefficients as 1, no transposes), marked as such; the next
