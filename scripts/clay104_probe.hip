@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -138,8 +139,10 @@ __global__ void __launch_bounds__(64) k_wave_ring(const uint8_t *pool, uint8_t *
     // wave-uniform plane base in SGPRs + the lane's 16 B: each load is a global load with an
     // SGPR base and a 32-bit VGPR offset, so the 52 addresses cost no VGPRs
     const uint64_t b64 = (uint64_t)(pool + s * kStripe + z * kNodes * kSub);
-    const uint8_t *sbase = reinterpret_cast<const uint8_t *>(
-        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b64 >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)b64));
+    // (readfirstlane returns int: take both halves as uint32_t, or the low half sign-extends)
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b64 >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b64);
+    const uint8_t *sbase = reinterpret_cast<const uint8_t *>(((uint64_t)hi << 32) | (uint64_t)lo);
     uint32_t voff = threadIdx.x * 16;
     auto ld = [&](int i) -> u32x4 {  // load i: slice i / 13, helper node i % 13, non-temporal
         const int j = i % 13, k = i / 13;
@@ -178,8 +181,11 @@ float best_ms(F launch) {
         hipEventRecord(e0);
         launch();
         hipEventRecord(e1);
-        hipEventSynchronize(e1);
-        hipEventElapsedTime(&ms, e0, e1);
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess ||
+            hipGetLastError() != hipSuccess) {
+            printf("{\"error\": \"launch or event failed\"}\n");
+            exit(1);
+        }
         if (rep) best = ms < best ? ms : best;
     }
     return best;
