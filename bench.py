@@ -900,9 +900,11 @@ def main():
                 break
             wl.launch()
             torch.cuda.synchronize()
+        wl.launch()  # the kept shape (or the static rules, if the layout is not selected per launch)
+        torch.cuda.synchronize()
+        kernel = ecx.last_kernel()
         choice, med = gm.layout_choice(pitch, with_times=True)
-        launch_shape = {"layout_select": choice, "candidate_median_ms": med,
-                        "kernel": ecx.last_kernel() if choice != -1 else None}
+        launch_shape = {"layout_select": choice, "candidate_median_ms": med, "kernel": kernel}
         if not args.no_verify and not wl.verify():
             raise SystemExit("output differs from the erased originals after the layout selection")
 

@@ -3,7 +3,8 @@
 # (default: all four), from rocprofv3 PMC passes: FETCH_SIZE and WRITE_SIZE in passes
 # of their own (they do not fit one TCC pass on gfx950), then one SQ pass (VALU
 # instructions, wave/busy/wait cycles, GRBM clock).  Every pass runs the bench for one
-# step over its resident pool and writes its launch metadata (--meta: kernel instance,
+# step of 16 launches over its resident pool (the per-layout shape selection's timed first
+# calls of the RS / LRC-encode maps run before it, so the timed launches outnumber them) and writes its launch metadata (--meta: kernel instance,
 # pool, algorithmic bytes, kernel-source hash) next to the counters;
 # scripts/pmc_summary.py turns them into profiles/pmc_traffic.json.
 # A pass that fails stops the script (no retries).
@@ -25,7 +26,7 @@ for W in $WORKLOADS; do
     D="$OUT/pmc_${W}_$i"; mkdir -p "$D"
     timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
         -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 \
-           --stripes-per-step "$POOL" --no-probes --meta "$D/meta.json" > "$D.log" 2>&1
+           --stripes-per-step $((POOL * 16)) --no-probes --meta "$D/meta.json" > "$D.log" 2>&1
     rc=$?; echo "pmc $W pass$i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D.log"; exit $rc; }
     i=$((i + 1))
   done

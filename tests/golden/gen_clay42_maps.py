@@ -38,10 +38,16 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 
-K, M = 4, 2
-N = K + M
-Q, T = M, N // M
-ALPHA = Q ** T
+K, M = 4, 2  # the committed maps; the functions below take any Clay(k, m) with m | k + m
+
+
+class Geo:
+    """ClayCodeUtil's geometry (ClayCodeErasureDecodingStep.java:690-941)."""
+
+    def __init__(self, k, m):
+        self.k, self.m, self.n = k, m, k + m
+        self.q, self.t = m, (k + m) // m
+        self.alpha = self.q ** self.t
 
 
 class GF:
@@ -106,100 +112,109 @@ def lin_scale(gf, c, t):
     return {k: gf.mul(c, v) for k, v in t.items() if gf.mul(c, v)}
 
 
-def zvec(z):
-    v = [0] * T
-    for i in range(T - 1, -1, -1):
-        v[i] = z % Q
-        z //= Q
+def zvec(g, z):
+    v = [0] * g.t
+    for i in range(g.t - 1, -1, -1):
+        v[i] = z % g.q
+        z //= g.q
     return v
 
 
-def zidx(v):
+def zidx(g, v):
     z = 0
     for d in v:
-        z = z * Q + d
+        z = z * g.q + d
     return z
 
 
-def node(x, y):
-    return x + Q * y
+def node(g, x, y):
+    return x + g.q * y
 
 
-def coords(i):
-    return i % Q, i // Q
+def coords(g, i):
+    return i % g.q, i // g.q
 
 
-def C(z, j):
+def C(g, z, j):
     """The coupled (stored) sub-chunk of node j in plane z: an input slot."""
-    return {z * N + j: 1}
+    return {z * g.n + j: 1}
 
 
-def decoupled(gf, z, j):
+def decoupled(gf, g, z, j):
     """U(j, z) from stored sub-chunks: a dot, or the pair transform with its couple."""
-    x, y = coords(j)
-    v = zvec(z)
+    x, y = coords(g, j)
+    v = zvec(g, z)
     if v[y] == x:
-        return C(z, j)
-    partner = node(v[y], y)
+        return C(g, z, j)
+    partner = node(g, v[y], y)
     v2 = list(v)
     v2[y] = x
-    return lin_add(lin_scale(gf, 3, C(z, j)), lin_scale(gf, 2, C(zidx(v2), partner)))
+    return lin_add(lin_scale(gf, 3, C(g, z, j)), lin_scale(gf, 2, C(g, zidx(g, v2), partner)))
 
 
-def solve_plane(gf, rs, U, missing):
-    """RS(4,2) per plane: fill U[j] for the two `missing` nodes from the four known."""
-    known = [j for j in range(N) if j not in missing]
-    assert len(known) == K
+def solve_plane(gf, g, rs, U, missing):
+    """RS(k, m) per plane: fill U[j] for the `missing` nodes from the k known."""
+    known = [j for j in range(g.n) if j not in missing]
+    assert len(known) == g.k
     sub_inv = gf.mat_inv([rs[j] for j in known])
-    data = [lin_add(*[lin_scale(gf, sub_inv[d][c], U[known[c]]) for c in range(K)]) for d in range(K)]
+    data = [lin_add(*[lin_scale(gf, sub_inv[d][c], U[known[c]]) for c in range(g.k)]) for d in range(g.k)]
     for j in missing:
-        U[j] = data[j] if j < K else lin_add(*[lin_scale(gf, rs[j][d], data[d]) for d in range(K)])
+        U[j] = data[j] if j < g.k else lin_add(*[lin_scale(gf, rs[j][d], data[d]) for d in range(g.k)])
     return U
 
 
-def repair_map(gf, rs, e):
-    ex, ey = coords(e)
-    helpers = [z for z in range(ALPHA) if zvec(z)[ey] == ex]
-    column = [node(x, ey) for x in range(Q)]
+def repair_map(gf, g, rs, e):
+    """Single repair of node e: output slot z (|E| = 1) -> linear form over input slots."""
+    ex, ey = coords(g, e)
+    helpers = [z for z in range(g.alpha) if zvec(g, z)[ey] == ex]
+    column = [node(g, x, ey) for x in range(g.q)]
     out = {}
     for z in helpers:
-        U = {j: decoupled(gf, z, j) for j in range(N) if j not in column}
-        solve_plane(gf, rs, U, column)
+        U = {j: decoupled(gf, g, z, j) for j in range(g.n) if j not in column}
+        solve_plane(gf, g, rs, U, column)
         out[z] = U[e]  # a dot in its helper plane: C(e, z) = U(e, z)
         for mate in column:
             if mate == e:
                 continue
-            v = zvec(z)
-            v[ey] = coords(mate)[0]
+            v = zvec(g, z)
+            v[ey] = coords(g, mate)[0]
             # couple of (e, z[ey := x']) is (mate, z): shards (C_e, C_m, U_e, U_m), C_m and U_m known
-            out[zidx(v)] = lin_add(lin_scale(gf, gf.div(3, 2), C(z, mate)), lin_scale(gf, gf.div(1, 2), U[mate]))
-    return out  # output slot z (|E| = 1) -> linear form
+            out[zidx(g, v)] = lin_add(lin_scale(gf, gf.div(3, 2), C(g, z, mate)),
+                                      lin_scale(gf, gf.div(1, 2), U[mate]))
+    return out
 
 
-def encode_map(gf, rs):
-    parity = [node(x, T - 1) for x in range(Q)]  # the parity column {4, 5}
+def encode_map(gf, g, rs):
+    """The parity column (the last node row) from the data nodes, every plane."""
+    parity = [node(g, x, g.t - 1) for x in range(g.q)]
     U = {}
-    for z in range(ALPHA):
-        Uz = {j: decoupled(gf, z, j) for j in range(K)}
+    for z in range(g.alpha):
+        Uz = {j: decoupled(gf, g, z, j) for j in range(g.k)}
         for p in parity:
-            Uz[p] = lin_add(*[lin_scale(gf, rs[p][d], Uz[d]) for d in range(K)])
+            Uz[p] = lin_add(*[lin_scale(gf, rs[p][d], Uz[d]) for d in range(g.k)])
         U[z] = Uz
+    pinv = gf.mat_inv([[3, 2], [2, 3]])
     out = {}
-    for z in range(ALPHA):
-        v = zvec(z)
+    for z in range(g.alpha):
+        v = zvec(g, z)
         for jj, p in enumerate(parity):
-            x, y = coords(p)
+            x, y = coords(g, p)
             if v[y] == x:
                 out[z * len(parity) + jj] = U[z][p]
             else:
-                partner = node(v[y], y)
+                partner = node(g, v[y], y)
                 v2 = list(v)
                 v2[y] = x
                 # [C_p, C_p'] = P^-1 [U_p, U_p'] with P = [[3, 2], [2, 3]] (its own inverse)
-                pinv = gf.mat_inv([[3, 2], [2, 3]])
                 out[z * len(parity) + jj] = lin_add(lin_scale(gf, pinv[0][0], U[z][p]),
-                                                    lin_scale(gf, pinv[0][1], U[zidx(v2)][partner]))
+                                                    lin_scale(gf, pinv[0][1], U[zidx(g, v2)][partner]))
     return out
+
+
+def field_and_code(k, m):
+    kats = json.loads((HERE / "reference_kats.json").read_text())
+    gf = GF(kats["galois"]["log_table"], kats["galois"]["exp_table"])
+    return gf, Geo(k, m), gf.rs_matrix(k, m)
 
 
 def triples(m):
@@ -214,15 +229,14 @@ def triples(m):
 
 def main():
     kats = json.loads((HERE / "reference_kats.json").read_text())
-    gf = GF(kats["galois"]["log_table"], kats["galois"]["exp_table"])
-    rs = gf.rs_matrix(K, M)
+    gf, g, rs = field_and_code(K, M)
     assert rs[K:] == kats["rs_parity_rows"]["4,2"], rs[K:]
     assert gf.rs_matrix(2, 2)[2:] == [[3, 2], [2, 3]]
     doc = {
         "source": "closed-form Clay(4,2) maps (tests/golden/gen_clay42_maps.py); no reference stage sequence run",
-        "repair_e1": triples(repair_map(gf, rs, 1)),
-        "repair_e4": triples(repair_map(gf, rs, 4)),
-        "encode_45": triples(encode_map(gf, rs)),
+        "repair_e1": triples(repair_map(gf, g, rs, 1)),
+        "repair_e4": triples(repair_map(gf, g, rs, 4)),
+        "encode_45": triples(encode_map(gf, g, rs)),
     }
     (HERE / "clay42_closed_form.json").write_text(json.dumps(doc) + "\n")
     print("wrote", HERE / "clay42_closed_form.json", {k: v["nnz"] for k, v in doc.items() if k != "source"})

@@ -173,6 +173,34 @@ def test_clay42_maps_equal_closed_form(ecx, name, erased):
     assert d["nnz"] == (144 if name == "encode_45" else 52)
 
 
+@pytest.mark.parametrize("k,m,v,e", [(12, 4, 0, 5), (12, 4, 0, 14), (10, 4, 2, 3), (10, 4, 2, 13)])
+def test_clay_q4_repair_maps_equal_closed_form(ecx, k, m, v, e):
+    """The same independent pin for the q = 4 codes of BASELINE config 4: the Clay(12,4)
+    single repair (256 x 960) and the shortened Clay(10,4) one -- the Clay(12,4) repair with
+    the two virtual data nodes' columns dropped (they read zeros) and real node
+    r >= 10 standing for Clay(12,4) node r + 2 -- derived in closed form by
+    tests/golden/gen_clay42_maps.py's equations equal the planner's composed map."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import gen_clay42_maps as cf
+    kk = k + v
+    gf, g, rs = cf.field_and_code(kk, m)
+    real_to_full = (lambda r: r if r < k else r + v)
+    want_full = cf.repair_map(gf, g, rs, real_to_full(e))
+    full_to_real = {real_to_full(r): r for r in range(k + m)}
+    n_real = k + m
+    want = {}
+    for o, form in want_full.items():
+        for slot, c in form.items():
+            z, node = divmod(slot, g.n)
+            if node in full_to_real:  # a virtual node's column multiplies zeros
+                want[(o, z * n_real + full_to_real[node])] = c
+    mat, ins, outs = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v).map().matrix()
+    nz = np.nonzero(mat)
+    got = {(int(outs[o]), int(ins[i])): int(mat[o, i]) for o, i in zip(*nz)}
+    assert got == want
+
+
 def test_clay124_map_shape(ecx):
     inf = ecx.ClayCodeErasureDecodingStep([5], 12, 4).map().info()
     assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (256, 960, 5568)
