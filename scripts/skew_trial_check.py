@@ -1,4 +1,8 @@
-"""skew_trial (include/ecx_tune.h) against the kernels it chooses between: RS(12,4)
+"""(Round 3 tool, kept for the provenance of profiles/r03_shape_trial_check.jsonl: the
+skew_trial knob it drives was replaced in round 4 by the per-layout selection, ecx_tune
+"layout_select", so it no longer runs; scripts/layout_sweep.py --set select is its successor.)
+
+skew_trial (include/ecx_tune.h) against the kernels it chooses between: RS(12,4)
 2-erasure decode in place at several shard pitches, each timed with the one-chunk
 launch in 256-thread and in one-wave workgroups (skew_chunks 0, block_threads 256 / 64),
 the skewed launch (skew_chunks 4), the static rules (skew_trial 0, the default) and the
