@@ -225,6 +225,7 @@ struct Registry {
     std::list<const T *> idle;  // front = most recently released
     std::map<const T *, typename std::list<const T *>::iterator> idle_pos;
     std::map<const T *, int> refs;
+    std::map<const T *, std::unique_ptr<T>> priv;  // private objects (registry full): freed by destroy
 
     template <typename Make>
     T *get(const Key &key, Make make) {
@@ -241,7 +242,11 @@ struct Registry {
             return obj;
         }
         std::unique_ptr<T> obj(make());  // may throw (invalid geometry): nothing registered
-        if (reg.size() >= kCodecRegistryMax) return obj.release();
+        if (reg.size() >= kCodecRegistryMax) {
+            T *p = obj.get();
+            priv.emplace(p, std::move(obj));
+            return p;
+        }
         obj->shared = true;
         T *p = obj.get();
         reg.emplace(key, std::move(obj));
@@ -250,16 +255,20 @@ struct Registry {
         return p;
     }
 
-    // Drops one reference; frees a private object, parks a shared one as idle.
+    // Drops one reference; frees a private object, parks a shared one as idle.  A pointer
+    // the registry does not hold a live reference for (a second destroy) is ignored, never
+    // dereferenced.
     void release(T *obj) {
         if (!obj) return;
-        if (!obj->shared) {
-            delete obj;
-            return;
-        }
         std::vector<std::unique_ptr<T>> evicted;  // destroyed outside the lock (hipFree syncs)
         {
             std::lock_guard<std::mutex> lk(mu);
+            auto pv = priv.find(obj);
+            if (pv != priv.end()) {
+                evicted.push_back(std::move(pv->second));
+                priv.erase(pv);
+                return;
+            }
             auto r = refs.find(obj);
             if (r == refs.end() || r->second <= 0) return;  // not a live reference: ignore
             if (--r->second > 0) return;

@@ -211,6 +211,8 @@ def test_codec_registry_refcounts_and_bounds_idle(ecx):
     assert counts()[:2] == [live0 + 1, idle0]        # one reference left
     destroy(b)
     assert counts()[:2] == [live0, idle0 + 1]        # parked idle, not freed
+    destroy(b)                                        # a second destroy holds no reference: ignored
+    assert counts()[:2] == [live0, idle0 + 1]
     assert rs(29, 3) == a and counts()[:2] == [live0 + 1, idle0]  # revived: same object
     destroy(a)
     # many distinct codecs created and released: the idle cache stays bounded
