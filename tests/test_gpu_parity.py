@@ -960,6 +960,44 @@ def test_random_maps_on_device(ecx, torch_dev, seed):
         ecx.tune("bitslice", 0)
 
 
+def test_codec_eviction_frees_and_recreates_device_plans(ecx, torch_dev):
+    """Reference-counted codecs on the device: 80 distinct RS(k, 2) codecs, each created,
+    used for a device batch encode and destroyed, push the first ones out of the 64-codec
+    idle cache (their device plans freed); re-creating and using them again rebuilds the
+    plans, and every encode equals the oracle's."""
+    import ctypes
+    torch = torch_dev
+    stats = ecx.lib().ecx_codec_stats
+    stats.argtypes, stats.restype = [ctypes.POINTER(ctypes.c_int)] * 4, ctypes.c_int
+
+    def idle():
+        v = ctypes.c_int()
+        stats(None, ctypes.byref(v), None, None)
+        return v.value
+
+    L, S = 256, 3
+
+    def encode_and_check(k):
+        rs = ecx.ReedSolomon.create(k, 2)
+        pool = torch.zeros((S, k + 2, L), dtype=torch.uint8, device="cuda")
+        data = torch.randint(0, 256, (S, k, L), dtype=torch.uint8, device="cuda")
+        pool[:, :k] = data
+        rs.encodeParityBatch(pool, (k + 2) * L, L, S, 0, L)
+        torch.cuda.synchronize()
+        host = pool.cpu().numpy()
+        for s_ in (0, S - 1):
+            shards = [host[s_, i].copy() for i in range(k)] + [np.zeros(L, np.uint8) for _ in range(2)]
+            O.ReedSolomon(k, 2).encode_parity(shards, 0, L)
+            assert all((host[s_, k + p] == shards[k + p]).all() for p in range(2)), (k, s_)
+        del rs  # ecx_rs_destroy: the last reference
+
+    for k in range(100, 180):
+        encode_and_check(k)
+    assert idle() == 64
+    for k in (100, 101, 179):  # 100, 101 were evicted (device plans freed); 179 is idle
+        encode_and_check(k)
+
+
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
 def test_rs_batch_codec_entry_points(ecx, torch_dev, k, m):
     """ecx_rs_encode_parity_batch / ecx_rs_decode_missing_batch: encodeParity and
