@@ -17,7 +17,11 @@
  *     GF(256) map, and the results are copied back.  There is no CPU
  *     arithmetic fallback: without a usable device they return ECX_E_DEVICE.
  *   - "Batch" entry points take DEVICE pointers (HBM-resident stripes) and a
- *     hipStream_t passed as void*; they only enqueue work.
+ *     hipStream_t passed as void*; they only enqueue work.  For the many-stream
+ *     RS / LRC-encode maps on batches of >= 256 MiB of input, the first calls of a
+ *     new layout time the candidate launch shapes with events on that stream (read
+ *     later without blocking) and keep the fastest; every shape writes the same bytes
+ *     (ecx_tune.h "layout_select").
  *   - Byte order / layout: a shard or sub-chunk is `byte_count` contiguous
  *     bytes.  Clay stripes are plane-major as in the reference
  *     (ClayCodeErasureDecodingStep.java:84-97): input slot z*n + node,
