@@ -40,6 +40,16 @@ SETS = {
     # the per-layout selection (default) against the static rules alone
     "select": [{}, {"layout_select": 0}],
     # unit orders without the XCD runs that misaligned layouts get by default (RS(17,3) at 200,000 B)
+    # ring depth / accumulator rows under the stagger, one-wave and 4 KiB workgroups (4 MiB pitch)
+    "depth": [{}, {"layout_select": 0},
+              {"block_threads": 64, "stagger": 2, "depth": 4}, {"block_threads": 64, "stagger": 2},
+              {"block_threads": 64, "stagger": 4, "depth": 4},
+              {"block_threads": 256, "skew_chunks": 0, "small_tiles": 1, "depth": 12, "stagger": 2},
+              {"block_threads": 256, "skew_chunks": 0, "small_tiles": 1, "depth": 8, "stagger": 2},
+              {"block_threads": 256, "skew_chunks": 0, "small_tiles": 1, "depth": 12},
+              {"block_threads": 256, "skew_chunks": 0, "depth": 12, "stagger": 2},
+              {"block_threads": 256, "skew_chunks": 0, "depth": 16, "stagger": 2},
+              {"skew_chunks": 4, "stagger": 2}, {"skew_chunks": 2, "stagger": 2}, {"skew_chunks": 2}],
     "misaligned": [{}, {"layout_select": 0}, {"xcd_misaligned": 0, "layout_select": 0},
                    {"stagger": 8, "xcd_misaligned": 0}, {"stagger": 4, "xcd_misaligned": 0},
                    {"stagger": 16, "xcd_misaligned": 0}, {"stagger": 8, "xcd_misaligned": 0, "block_threads": 64},
@@ -104,13 +114,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cases", default="rs124,rs173")
+    ap.add_argument("--pitches", default=None, help="comma-separated shard+pad byte pairs as L:pad (default: all)")
     args = ap.parse_args()
     import torch
     ecx = rpamd.load()
     buf = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")
     ecx.fill_random(buf, buf.numel(), 7)
     for kind in args.cases.split(","):
-        for L, pad in (RS124 if kind == "rs124" else RS173):
+        cases = RS124 if kind == "rs124" else RS173
+        if args.pitches:
+            cases = [tuple(int(x) for x in c.split(":")) for c in args.pitches.split(",")]
+        for L, pad in cases:
             run_case(ecx, torch, buf, kind, L, pad, SETS[args.set], args.rounds, args.reps)
 
 
