@@ -45,8 +45,8 @@
  *                      and one chunk per workgroup otherwise; 0 = never
  *   "layout_select"    single-tile maps over >= 8 inputs with <= 4 rows (the many-stream RS maps), with the
  *                      knobs "skew_chunks", "block_threads" and "stagger" on auto, on batches of >= 256 MiB of
- *                      input: 1 = the launch shape is chosen per batch layout (map, strides, byte and
- *                      stripe count, device) by timing the caller's own first launches -- the static
+ *                      input: 1 = the launch shape is chosen per batch layout (map, strides, size classes
+ *                      (log2) of the shard and of the batch, device; up to 64 layouts per map) by timing the caller's own first launches -- the static
  *                      rules' shape, 4 KiB and one-wave workgroups, skewed chunks, staggered stripes,
  *                      3 timings each, events read without blocking on later calls -- and the fastest
  *                      median is kept (default; every candidate computes the same bytes, nothing extra

@@ -667,6 +667,7 @@ MapPlanes *CompiledMap::planes() {
 
 namespace {
 constexpr float kLayoutMargin = 0.98f;  // another shape replaces the static rules' only if 2 % faster
+constexpr size_t kMaxLayouts = 64;      // layouts selected per map; past that, new ones use the static rules
 
 float median_of(std::vector<float> v) {
     std::sort(v.begin(), v.end());
@@ -676,9 +677,10 @@ float median_of(std::vector<float> v) {
 
 int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, bool *time) {
     std::lock_guard<std::mutex> lk(mu_);
+    *time = false;
+    if (!layout_sel_.count(key) && layout_sel_.size() >= kMaxLayouts) return 0;  // bounded: the static rules
     LayoutSel &s = layout_sel_[key];
     if ((int)s.ms.size() != n_cand) s.ms.assign(n_cand, {});
-    *time = false;
     if (s.chosen >= 0) return s.chosen;
     for (auto it = s.pending.begin(); it != s.pending.end();) {
         const hipError_t q = hipEventQuery(it->e1);

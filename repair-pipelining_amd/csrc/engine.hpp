@@ -155,7 +155,8 @@ public:
     // the candidate to run for this call of the batch layout `key`.  Finished timing probes
     // are harvested first (non-blocking); once every one of the n_cand candidates has
     // `samples` timings the fastest median is kept (candidate 0 -- the static rules --
-    // unless another is faster by kLayoutMargin).  While exploring, the least-sampled
+    // unless another is faster by kLayoutMargin).  At most kMaxLayouts layouts are selected per
+    // map (later ones get candidate 0, untimed).  While exploring, the least-sampled
     // candidate is returned with *time set: the caller brackets that launch with two
     // events on its stream and hands them to add_layout_probe.
     int next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, bool *time);

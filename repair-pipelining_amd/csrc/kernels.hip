@@ -522,7 +522,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 // whose stripes collide) queue on one bank (scripts/addr_probe.hip), and
 // no static rule predicts which shape -- 4 KiB or one-wave workgroups, skewed chunks,
 // staggered stripes -- is fastest at a given pitch (scripts/layout_sweep.py).  So for a
-// new layout (map, strides, byte count, stripe count, device) the first calls run the
+// new layout (map, strides, size classes of the shard and the batch, device) the first calls run the
 // candidates in turn, each launch bracketed by two events on the caller's stream; the
 // events are read without blocking on later calls, and once every candidate has
 // kLayoutSamples timings the fastest median is kept for that layout.  Every candidate
@@ -564,8 +564,12 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     }
     int dev = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
+    // A layout is its strides, the size class of the shard (log2 of the byte count) and of the
+    // batch (log2 of its input bytes), the mode and the device: callers whose batch sizes vary
+    // from call to call share one selection instead of exploring anew at every size.
+    auto log2i = [](int64_t v) { return (int64_t)(63 - __builtin_clzll((unsigned long long)std::max<int64_t>(v, 1))); };
     const std::array<int64_t, 8> key{in_slot_stride, in_stripe_stride, out_slot_stride, out_stripe_stride,
-                                     nbytes, nstripes, (int64_t)accumulate, (int64_t)dev};
+                                     log2i(nbytes), log2i(nstripes * in_bytes), (int64_t)accumulate, (int64_t)dev};
     bool time = false;
     const int cand = cm.next_layout_pick(key, kLayoutNCand, kLayoutSamples, &time);
     hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -1807,6 +1807,16 @@ def test_layout_select_is_measured_and_exact(ecx, torch_dev, pitch):
     choice, ms = dmap.layout_choice(pitch, with_times=True)
     assert choice != -1, ms
     assert all(t > 0 for t in ms[:7]), ms
+    # a batch of another stripe count in the same size class reuses the choice: no exploring
+    dmap.apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S, L)
+    torch.cuda.synchronize()
+    kept = ecx.last_kernel()
+    for _ in range(3):
+        pool[:, 0:2, :L] = 0
+        dmap.apply_batch(pool, 16 * pitch, pitch, pool, 16 * pitch, pitch, S - 1, L)
+        torch.cuda.synchronize()
+        assert ecx.last_kernel() == kept
+        assert bool(torch.equal(pool[:S - 1, 0:2, :L], orig[:S - 1]))
     assert any(k.startswith("k_gf_apply_skew") for k in kernels) and any(", 64, " in k for k in kernels), kernels
     static_ms = ms[0]
     assert min(ms[:7]) <= static_ms
