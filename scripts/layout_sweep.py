@@ -25,6 +25,7 @@ TOTAL = 16 << 30
 RS124 = [(4 << 20, 0), (4 << 20, 4096), (1 << 20, 0), (1 << 20, 4096), (3 << 20, 0), (8 << 20, 0), (4 << 20, 65536),
          (1 << 19, 0)]
 RS173 = [(200000, 0), (262144, 0)]
+CLAY42 = [(32768, 0), (65536, 0), (262144, 0), (1 << 20, 0), (4 << 20, 0), (16384, 0)]
 DEFAULTS = {"depth": 0, "block_threads": 0, "small_tiles": 2, "skew_chunks": 1, "xcd_group": 0, "xcd_run": 8,
             "xcd_misaligned": 1, "stagger": 0, "chunk_major": 0, "layout_select": 1}
 SETS = {
@@ -50,6 +51,10 @@ SETS = {
               {"block_threads": 256, "skew_chunks": 0, "depth": 12, "stagger": 2},
               {"block_threads": 256, "skew_chunks": 0, "depth": 16, "stagger": 2},
               {"skew_chunks": 4, "stagger": 2}, {"skew_chunks": 2, "stagger": 2}, {"skew_chunks": 2}],
+    # the 8-row Clay(4,2) repair map across sub-chunk sizes
+    "clay": [{}, {"block_threads": 64}, {"skew_chunks": 2}, {"stagger": 2}, {"stagger": 8},
+             {"block_threads": 64, "stagger": 2}, {"block_threads": 64, "stagger": 8}, {"chunk_major": 1},
+             {"xcd_group": 3, "xcd_run": 32}],
     "misaligned": [{}, {"layout_select": 0}, {"xcd_misaligned": 0, "layout_select": 0},
                    {"stagger": 8, "xcd_misaligned": 0}, {"stagger": 4, "xcd_misaligned": 0},
                    {"stagger": 16, "xcd_misaligned": 0}, {"stagger": 8, "xcd_misaligned": 0, "block_threads": 64},
@@ -64,6 +69,14 @@ def run_case(ecx, torch, buf, kind, L, pad, knobs, rounds, reps):
         mat, ins, outs = ecx.ReedSolomon.create(12, 4).decode_map([False, False] + [True] * 14).matrix()
         out_view = lambda: buf[:S * n * p].view(S, n, p)[:, :2, :L]  # noqa: E731
         moved = (12 + 2) * L * S
+    elif kind == "clay42":  # Clay(4,2) repair of node 1 (8 x 20), B-byte sub-chunks: [S][48][B] -> [S][8][B]
+        n, S = 48, min(1 << 15, (TOTAL * 6 // 7) // (48 * p))
+        mat, ins, outs = ecx.ClayCodeErasureDecodingStep([1], 4, 2).map().matrix()
+        obase = S * n * p
+        gm0 = ecx.GfMap.from_matrix(mat, in_slot=[int(i) for i in ins], out_slot=[int(o) for o in outs])
+        out_view = lambda: buf[obase:obase + S * 8 * p].view(S, 8, p)[:, :, :L]  # noqa: E731
+        moved = 28 * L * S
+        del gm0
     else:
         n, S = 20, min(8192, TOTAL // (20 * p))
         mat, ins, outs = ecx.ReedSolomon.create(17, 3).encode_map().matrix()
@@ -76,7 +89,11 @@ def run_case(ecx, torch, buf, kind, L, pad, knobs, rounds, reps):
     for _ in range(rounds):
         for i, kn in enumerate(knobs):
             gm = maps[i]
-            launch = lambda: gm.apply_batch(buf, n * p, p, buf, n * p, p, S, L)  # noqa: E731
+            if kind == "clay42":
+                ob = buf[S * n * p:]
+                launch = lambda: gm.apply_batch(buf, n * p, p, ob, 8 * p, p, S, L)  # noqa: E731
+            else:
+                launch = lambda: gm.apply_batch(buf, n * p, p, buf, n * p, p, S, L)  # noqa: E731
             for k, v in kn.items():
                 ecx.tune(k, v)
             try:
@@ -121,7 +138,7 @@ def main():
     buf = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")
     ecx.fill_random(buf, buf.numel(), 7)
     for kind in args.cases.split(","):
-        cases = RS124 if kind == "rs124" else RS173
+        cases = {"rs124": RS124, "rs173": RS173, "clay42": CLAY42}[kind]
         if args.pitches:
             cases = [tuple(int(x) for x in c.split(":")) for c in args.pitches.split(",")]
         for L, pad in cases:
