@@ -1164,6 +1164,49 @@ def test_skew_chunks_agree(ecx, torch_dev, nbytes):
         ecx.tune("skew_chunks", 1)
 
 
+@pytest.mark.parametrize("S", [7, 16])
+def test_stagger_unit_orders_agree(ecx, torch_dev, S):
+    """The stagger unit order (ecx_tune "stagger" G: G stripes interleaved, stripe j of a
+    group starting at chunk j*C/G, stripes past the last whole group stripe-major) is a
+    bijection of the (stripe, chunk) units for every G, under 4 KiB and one-wave workgroups
+    and skewed chunks, with a ragged tail chunk and a stripe count that leaves a partial
+    group: every setting writes the bytes of the stripe-major launch, and those equal the
+    oracle's decodeMissing on a stripe, in overwrite and in accumulate mode."""
+    torch = torch_dev
+    L = 9 * 4096 + 1000
+    pitch = (L + 512 + 15) // 16 * 16  # 16-B aligned slots: the full chunks run the fast kernels
+    rs = ecx.ReedSolomon.create(12, 4)
+    dmap = rs.decode_map([False, False] + [True] * 14)
+    src = torch.empty((S, 16, pitch), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(src, src.numel(), 71)
+    outs = {}
+    try:
+        for G in (0, 2, 3, 4, 8, 64):
+            for bt, skew in ((256, 0), (64, 0), (256, 4), (256, 2)):
+                ecx.tune("stagger", G)
+                ecx.tune("block_threads", bt)
+                ecx.tune("skew_chunks", skew)
+                for acc in (False, True):
+                    o = torch.full((S, 2, pitch), 0x5A if acc else 0, dtype=torch.uint8, device="cuda")
+                    if acc:
+                        dmap.accumulate_batch(src, 16 * pitch, pitch, o, 2 * pitch, pitch, S, L)
+                    else:
+                        dmap.apply_batch(src, 16 * pitch, pitch, o, 2 * pitch, pitch, S, L)
+                    torch.cuda.synchronize()
+                    outs[(G, bt, skew, acc)] = o
+    finally:
+        ecx.tune("stagger", 0)
+        ecx.tune("block_threads", 0)
+        ecx.tune("skew_chunks", 1)
+    for (G, bt, skew, acc), o in outs.items():
+        assert bool(torch.equal(o, outs[(0, 256, 0, acc)])), (G, bt, skew, acc)
+    host = src[S - 1].cpu().numpy()
+    shards = [np.zeros(L, np.uint8) if i < 2 else host[i, :L].copy() for i in range(16)]
+    O.ReedSolomon(12, 4).decode_missing(shards, [i >= 2 for i in range(16)], 0, L)
+    got = outs[(0, 256, 0, False)][S - 1].cpu().numpy()
+    assert (got[0, :L] == shards[0]).all() and (got[1, :L] == shards[1]).all()
+
+
 def test_every_product_on_device(ecx, torch_dev):
     """Every GF(256) product c*x through the device kernel's split tables: a 256 x 1
     map whose row c has coefficient c (0 and 1 included), over an input holding every
