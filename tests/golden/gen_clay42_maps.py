@@ -30,6 +30,12 @@ C_e = (3/2) C_m + (1/2) U_m.
 Encode (erasing the parity column {4, 5}): U of the data nodes from the pair transform, U of
 the parity nodes = RS(4,2) parity rows times them, C of the parity nodes = P^-1 (U_p, U_p').
 
+Any m-node erasure (solve_map): the erased sub-chunks are the unique solution of every
+plane's RS parity checks on the decoupled symbols -- the code's definition as a linear
+system, solved by Gaussian elimination, with no decoding order at all.  The tests compare it
+with the planner's multi-node maps (doDecodeMulti's composition) of Clay(4,2), (6,3), (8,4),
+(12,4) and the shortened (10,4).
+
 Slots are the reference's: input z*n + node (ClayCodeErasureDecodingStep.java:84-97),
 output z*|E| + j.  Maps are stored as {"out": [...], "in": [...], "coef": [...]} triples.
 """
@@ -208,6 +214,57 @@ def encode_map(gf, g, rs):
                 # [C_p, C_p'] = P^-1 [U_p, U_p'] with P = [[3, 2], [2, 3]] (its own inverse)
                 out[z * len(parity) + jj] = lin_add(lin_scale(gf, pinv[0][0], U[z][p]),
                                                     lin_scale(gf, pinv[0][1], U[zidx(g, v2)][partner]))
+    return out
+
+
+def solve_map(gf, g, rs, erased):
+    """Any m-node erasure, from the code's definition alone: the unknowns are the erased
+    nodes' stored sub-chunks C(e, z), every plane's decoupled symbols must satisfy the
+    RS(k, m) parity checks U_p = sum_d G[p][d] U_d (m equations per plane, m * alpha in
+    all -- as many as unknowns), and Gaussian elimination over GF(2^8) expresses each
+    unknown in the known sub-chunks.  No decoding order, helper choice or stage sequence
+    is involved, and with |E| = m the result is unique (k * alpha known symbols carry
+    the whole codeword), so every correct decoder composes to exactly this map.
+    Output slot z * |E| + j for the j-th erased node in ascending order; the result is
+    {output slot: {input slot: coefficient}} like repair_map's."""
+    import numpy as np
+    erased = sorted(erased)
+    assert len(erased) == g.m
+    unk = {z * g.n + e: j * g.alpha + z for j, e in enumerate(erased) for z in range(g.alpha)}
+    known = sorted(s for s in range(g.alpha * g.n) if s not in unk)
+    col_of = dict(unk)
+    col_of.update({s: len(unk) + i for i, s in enumerate(known)})
+    mul = np.zeros((256, 256), np.uint8)
+    for a in range(1, 256):
+        for b in range(1, 256):
+            mul[a, b] = gf.mul(a, b)
+    inv = np.zeros(256, np.uint8)
+    inv[1:] = [gf.inv(a) for a in range(1, 256)]
+    W = np.zeros((g.m * g.alpha, len(col_of)), np.uint8)  # [A | B]: A x = B y over GF(2^8)
+    r = 0
+    for z in range(g.alpha):
+        U = [decoupled(gf, g, z, j) for j in range(g.n)]
+        for p in range(g.k, g.n):
+            # U_p + sum_d G[p][d] U_d = 0; a known term moves across unchanged (characteristic 2)
+            for slot, c in lin_add(U[p], *[lin_scale(gf, rs[p][d], U[d]) for d in range(g.k)]).items():
+                W[r, col_of[slot]] ^= c
+            r += 1
+    n = len(unk)
+    for col in range(n):
+        piv = col + int(np.flatnonzero(W[col:, col])[0])
+        W[[col, piv]] = W[[piv, col]]
+        W[col] = mul[inv[W[col, col]], W[col]]
+        h = W[:, col].copy()
+        h[col] = 0
+        rows = np.flatnonzero(h)
+        cols = np.flatnonzero(W[col])
+        W[np.ix_(rows, cols)] ^= mul[h[rows][:, None], W[col, cols][None, :]]
+    assert (W[:, :n] == np.eye(n, dtype=np.uint8)).all()
+    out = {}
+    for j in range(len(erased)):
+        for z in range(g.alpha):
+            row = W[j * g.alpha + z, n:]
+            out[z * len(erased) + j] = {known[i]: int(row[i]) for i in np.flatnonzero(row)}
     return out
 
 

@@ -201,6 +201,40 @@ def test_clay_q4_repair_maps_equal_closed_form(ecx, k, m, v, e):
     assert got == want
 
 
+@pytest.mark.parametrize("k,m,v,erased", [(4, 2, 0, E) for E in ([0, 3], [1, 5], [0, 1], [2, 3], [4, 5], [0, 5])] +
+                         [(6, 3, 0, [0, 4, 8]), (6, 3, 0, [1, 2, 3]), (8, 4, 0, [0, 5, 10, 11]),
+                          (12, 4, 0, [0, 5, 10, 15]), (10, 4, 2, [0, 5, 11, 13]), (10, 4, 2, [10, 11, 12, 13])])
+def test_clay_multi_erasure_maps_equal_parity_check_solution(ecx, k, m, v, erased):
+    """Multi-node repair (doDecodeMulti's composition in the planner and the oracle)
+    against the code's definition alone: gen_clay42_maps.solve_map solves every plane's RS
+    parity checks on the pair-transformed symbols for the m erased nodes' sub-chunks by
+    Gaussian elimination -- no decoding order, helper choice or stage sequence.  With
+    |E| = m the linear map is unique, so the planner's composed map must equal it entry
+    for entry, and so must the oracle's (read off by unit vectors, k + m <= 12).
+    Shortened codes: the Clay(k + v, m) solution with the virtual nodes' columns dropped."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import gen_clay42_maps as cf
+    gf, g, rs = cf.field_and_code(k + v, m)
+    real_to_full = (lambda r: r if r < k else r + v)
+    full_to_real = {real_to_full(r): r for r in range(k + m)}
+    want = {}
+    for o, form in cf.solve_map(gf, g, rs, [real_to_full(e) for e in erased]).items():
+        for slot, c in form.items():
+            z, node = divmod(slot, g.n)
+            if node in full_to_real:  # a virtual node's column multiplies zeros
+                want[(o, z * (k + m) + full_to_real[node])] = c
+    kw = {"virtualUnits": v} if v else {}
+    mat, ins, outs = ecx.ClayCodeErasureDecodingStep(erased, k, m, **kw).map().matrix()
+    mats = [mat]
+    if v == 0 and k + m <= 12:
+        mats.append(_probe_oracle_map(k, m, erased, ins.tolist()))
+    for mm in mats:
+        nz = np.nonzero(mm)
+        got = {(int(outs[o]), int(ins[i])): int(mm[o, i]) for o, i in zip(*nz)}
+        assert got == want
+
+
 def test_clay124_map_shape(ecx):
     inf = ecx.ClayCodeErasureDecodingStep([5], 12, 4).map().info()
     assert (inf["n_out"], inf["n_in"], inf["nnz"]) == (256, 960, 5568)
