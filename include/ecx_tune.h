@@ -48,7 +48,7 @@
  *                      input: 1 = the launch shape is chosen per batch layout (map, strides, size classes
  *                      (log2) of the shard and of the batch, device; up to 64 layouts per map) by timing the caller's own first launches -- the static
  *                      rules' shape, 4 KiB and one-wave workgroups, skewed chunks, staggered stripes,
- *                      3 timings each, events read without blocking on later calls -- and the fastest
+ *                      5 timings each, events read without blocking on later calls -- and the fastest
  *                      median is kept (default; every candidate computes the same bytes, nothing extra
  *                      is launched); 0 = the static rules only (skew on 4 MiB-multiple pitches, one
  *                      wave for <= 2-row maps over >= 8 inputs)

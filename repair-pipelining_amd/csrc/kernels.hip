@@ -247,7 +247,8 @@ namespace {
 // chunks, and stagger the unit order (apply.hpp unit_of) -- the per-layout candidates
 void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                        uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
-                       int64_t nbytes, hipStream_t stream, bool accumulate, int pick) {
+                       int64_t nbytes, hipStream_t stream, bool accumulate, int pick,
+                       hipEvent_t probe_start = nullptr) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
     const Tuning &tu = tuning();
     // (the lab kernels -- tile groups, bit-sliced, LDS lookup tables, residency caps -- exist
@@ -481,6 +482,9 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         }
     };
     int64_t first = 0;  // first full chunk left to the one-chunk kernels
+    // a layout probe's start: after the host-side work (plan upload on first use), so the
+    // probe times the kernels alone; a failed record only drops that probe
+    if (probe_start && hipEventRecord(probe_start, stream) != hipSuccess) (void)hipGetLastError();
 #if ECX_DIAG
     if (lut) {
         a.chunk_begin = 0;
@@ -530,7 +534,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
 // exploration costs only the slower candidates' launches.  Batches under kLayoutMinBytes of
 // input, streams being captured and forced shapes use the static rules.
 constexpr int64_t kLayoutMinBytes = (int64_t)256 << 20;
-constexpr int kLayoutSamples = 3;
+constexpr int kLayoutSamples = 5;  // median of 5: 3 left a 2-5 % spread between fresh maps (scripts/select_check.py)
 // candidate 0 = the static rules, then shape + 8 * stagger (launch_apply_core's pick)
 constexpr int kLayoutCand[] = {-1, 0, 1, 2, 2 + 8 * 2, 2 + 8 * 8, 0 + 8 * 4};
 constexpr int kLayoutNCand = (int)(sizeof(kLayoutCand) / sizeof(kLayoutCand[0]));
@@ -574,8 +578,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     const int cand = cm.next_layout_pick(key, kLayoutNCand, kLayoutSamples, &time);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (time) {
-        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
-            hipEventRecord(e0, stream) != hipSuccess) {
+        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
             (void)hipGetLastError();
             if (e0) (void)hipEventDestroy(e0);
             if (e1) (void)hipEventDestroy(e1);
@@ -585,7 +588,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     }
     try {
         launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
-                          nbytes, stream, accumulate, kLayoutCand[cand]);
+                          nbytes, stream, accumulate, kLayoutCand[cand], time ? e0 : nullptr);
     } catch (...) {
         if (time) {
             (void)hipEventDestroy(e0);
