@@ -363,8 +363,10 @@ template <int T>
 void launch_shape_t(const Shape &s, dim3 grid, size_t lds, hipStream_t stream, const ApplyArgs &a);
 
 // k_gf_apply_skew (apply_skew.hip): single-tile maps, K = 2 or 4 chunks per workgroup
-// with rotated chunk order; grid = stripes x chunk groups (ApplyArgs::n_chunks groups).
-void launch_skew(int k, int rows, int depth, bool ntl, dim3 grid, hipStream_t stream, const ApplyArgs &a);
+// with rotated chunk order; grid = stripes x chunk groups (ApplyArgs::n_chunks groups) x
+// (4 KiB / (threads x 16)) columns.
+void launch_skew(int k, int rows, int depth, bool ntl, int threads, dim3 grid, hipStream_t stream,
+                 const ApplyArgs &a);
 
 // k_gf_bits (apply_bits.hip): the bit-sliced kernel, 128-lane workgroups over 4 KiB
 // chunks, ring depth 2 or 4; grid = stripes x chunks x tiles, as k_gf_apply.

@@ -8,7 +8,10 @@
 // collide (0.63 of HBM against 0.77 with a 4 KiB pad).  Here a
 // workgroup owns chunks c..c+K-1 of its stripe and walks its K x n entry sequence as
 // K phases: in phase t entry e reads chunk (e + t) mod K, so consecutive loads in
-// the ring alternate between K byte offsets.  Entry e accumulates into the
+// the ring alternate between K byte offsets.  THREADS = 64 (one wave, diagnostic build
+// only): each 4 KiB chunk is split into four 1 KiB columns, one per workgroup, so a
+// workgroup's K loads of a slot still sit 4 KiB apart (the spacing that separates
+// colliding streams, profiles/r04_addr_pitch.jsonl) with the one-wave shape's footprint.  Entry e accumulates into the
 // accumulators of chunk (e + t) mod K; with the entry count and DEPTH multiples of
 // K that is physical accumulator set e mod K once the sets are rotated by one at
 // every phase change (K rotations restore the identity before the stores).
@@ -16,14 +19,18 @@
 
 namespace ecx {
 
-template <bool NTL, int DEPTH, int ROWS, int K>
-__global__ void __launch_bounds__(kBlockThreads, ROWS * K <= 8 ? 5 : 4) k_gf_apply_skew(ApplyArgs a) {
+template <bool NTL, int DEPTH, int ROWS, int K, int THREADS>
+__global__ void __launch_bounds__(THREADS, ROWS * K <= 8 ? 5 : 4) k_gf_apply_skew(ApplyArgs a) {
     static_assert(DEPTH % K == 0, "the ring must hold whole rotations");
+    constexpr uint32_t kSub = kChunkBytes / (THREADS * 16);  // workgroups per 4 KiB chunk
+    static_assert(kSub * THREADS * 16 == kChunkBytes, "a chunk is whole workgroup columns");
+    const uint32_t col = blockIdx.x % kSub;
     int64_t s, g;  // stripe, chunk group
-    unit_of(blockIdx.x, (uint32_t)a.n_chunks, gridDim.x / (uint32_t)a.n_chunks, 0, (uint32_t)a.stagger, s, g);
+    unit_of(blockIdx.x / kSub, (uint32_t)a.n_chunks, gridDim.x / kSub / (uint32_t)a.n_chunks, 0, (uint32_t)a.stagger, s,
+            g);
     s += a.stripe_begin;
     g += a.chunk_begin;
-    const int64_t cbase = g * (int64_t)(K * kChunkBytes);
+    const int64_t cbase = g * (int64_t)(K * kChunkBytes) + col * (THREADS * 16);
     const uint32_t lane16 = threadIdx.x * 16;
     cu32 *tile = plan_ptr(a.tiles);
     const uint8_t *ib = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase))) +
@@ -90,17 +97,24 @@ __global__ void __launch_bounds__(kBlockThreads, ROWS * K <= 8 ? 5 : 4) k_gf_app
         }
 }
 
-void launch_skew(int k, int rows, int depth, bool ntl, dim3 grid, hipStream_t stream, const ApplyArgs &a) {
-    const dim3 blk(kBlockThreads);
-#define ECX_SKEW(NTL, D, R, KK)                                                                 \
-    if (ntl == NTL && depth == D && rows == R && k == KK) {                                     \
-        note_kernel("k_gf_apply_skew", NTL, D, R, KK);                                          \
-        hipLaunchKernelGGL((k_gf_apply_skew<NTL, D, R, KK>), grid, blk, 0, stream, a);          \
+void launch_skew(int k, int rows, int depth, bool ntl, int threads, dim3 grid, hipStream_t stream,
+                 const ApplyArgs &a) {
+#define ECX_SKEW(NTL, D, R, KK, T)                                                              \
+    if (ntl == NTL && depth == D && rows == R && k == KK && threads == T) {                     \
+        note_kernel("k_gf_apply_skew", NTL, D, R, KK, T);                                       \
+        hipLaunchKernelGGL((k_gf_apply_skew<NTL, D, R, KK, T>), grid, dim3(T), 0, stream, a);   \
         return;                                                                                 \
     }
-    ECX_SKEW(true, 4, 2, 2) ECX_SKEW(true, 8, 2, 2) ECX_SKEW(true, 4, 2, 4) ECX_SKEW(true, 8, 2, 4)
-    ECX_SKEW(true, 4, 4, 2) ECX_SKEW(true, 8, 4, 2) ECX_SKEW(true, 4, 4, 4) ECX_SKEW(true, 8, 4, 4)
-    ECX_SKEW(true, 4, 8, 2)  // 8 rows x 2 chunks: depth 4 only (depth 8 spills)
+    ECX_SKEW(true, 4, 2, 2, 256) ECX_SKEW(true, 8, 2, 2, 256) ECX_SKEW(true, 4, 2, 4, 256) ECX_SKEW(true, 8, 2, 4, 256)
+    ECX_SKEW(true, 4, 4, 2, 256) ECX_SKEW(true, 8, 4, 2, 256) ECX_SKEW(true, 4, 4, 4, 256) ECX_SKEW(true, 8, 4, 4, 256)
+    ECX_SKEW(true, 4, 8, 2, 256)  // 8 rows x 2 chunks: depth 4 only (depth 8 spills)
+#if ECX_DIAG
+    // one-wave columns: measured and kept off -- 0.67-0.73 of HBM on the colliding RS pitches,
+    // below the selected shapes, and 7-11 % below the one-chunk kernel elsewhere
+    // (profiles/r04_layout_skewcheck.jsonl)
+    ECX_SKEW(true, 4, 2, 2, 64) ECX_SKEW(true, 8, 2, 2, 64) ECX_SKEW(true, 4, 2, 4, 64) ECX_SKEW(true, 8, 2, 4, 64)
+    ECX_SKEW(true, 4, 4, 2, 64) ECX_SKEW(true, 8, 4, 2, 64) ECX_SKEW(true, 4, 4, 4, 64) ECX_SKEW(true, 8, 4, 4, 64)
+#endif
 #undef ECX_SKEW
     throw Error(ECX_E_ILLEGAL_ARGUMENT, "no k_gf_apply_skew instance for this shape");
 }

@@ -244,7 +244,8 @@ namespace {
 // pick: -1 = the static rules (skew on 4 MiB-multiple input slot pitches, one-wave
 // workgroups for narrow maps otherwise); else shape + 8 * stagger with shape 0 = 256-thread
 // workgroups over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB
-// chunks, and stagger the unit order (apply.hpp unit_of) -- the per-layout candidates
+// chunks, 3 = skewed chunks on one-wave workgroups (1 KiB columns, diagnostic build), and
+// stagger the unit order (apply.hpp unit_of) -- the per-layout candidates
 void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                        uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                        int64_t nbytes, hipStream_t stream, bool accumulate, int pick,
@@ -266,10 +267,12 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     // workgroups: 0-4 % faster than one wave once the byte-safe tail took 16-B accesses
     // (profiles/r03_rs_km.jsonl, r03_rs173_pitch.jsonl, r03_rs173_ab.jsonl).
     const int shape = pick < 0 ? -1 : pick & 7;
-    const bool skew_pitch = pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4 : shape == 1;
+    const bool skew_pitch =
+        pick < 0 ? in_slot_stride % ((int64_t)4 << 20) == 0 && cm.map().n_in >= 4 : (shape == 1 || shape == 3);
     const bool one_wave = tu.block_threads == 64 ||
                           (tu.block_threads == 0 && cm.n_tiles() == 1 && tu.bitslice != 2 && !tu.lds_lut &&
-                           (pick < 0 ? cm.max_tile_rows() <= 2 && cm.map().n_in >= 8 && !skew_pitch : shape == 2));
+                           (pick < 0 ? cm.max_tile_rows() <= 2 && cm.map().n_in >= 8 && !skew_pitch
+                                     : (shape == 2 || shape == 3)));
     int threads = one_wave && nts == 1 ? 64 : kBlockThreads;
     int rows = kTileRows;
     // Small-row kernel variants: forced (1), or auto (2) for maps of <= 2 rows over <= 4
@@ -310,8 +313,11 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     int skew = tu.skew_chunks == 1 ? (skew_auto ? 4 : 0) : tu.skew_chunks;
     const int skew_rows = cm.max_tile_rows() <= 2 ? 2 : (cm.max_tile_rows() <= 4 ? 4 : kTileRows);
     if (skew == 4 && skew_rows == kTileRows) skew = 2;  // 8 rows x 4 chunks would not fit the VGPRs
-    if (!(skew && cm.n_tiles() == 1 && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1 && aligned &&
-          nbytes >= skew * kChunkBytes))
+    // (one-wave workgroups take the skewed order over 1 KiB columns of <= 4-row maps in the
+    // diagnostic build only: measured slower than the selected shapes)
+    if (!(skew && cm.n_tiles() == 1 && !waves &&
+          (threads == kBlockThreads || (ECX_DIAG && threads == 64 && skew_rows <= 4)) &&
+          ntmode == 2 && nts == 1 && aligned && nbytes >= skew * kChunkBytes))
         skew = 0;
     if (skew) depth = depth == 4 || skew_rows == kTileRows ? 4 : 8;
     // Bit-sliced kernel (k_gf_bits, apply_bits.hip) for the full 4 KiB chunks: forced (2)
@@ -501,17 +507,18 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         first = n4k * kChunkBytes / chunk;
     }
     if (skew) {
-        const int64_t groups = full / skew;
+        const int64_t cols = kChunkBytes / chunk;  // workgroups per 4 KiB chunk (4 for one wave)
+        const int64_t groups = full / (skew * cols);
         a.chunk_begin = 0;
         a.n_chunks = groups;
         const int64_t max_blocks = (int64_t)1 << 30;
-        const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / groups);
+        const int64_t stripes_per_launch = std::max<int64_t>(1, max_blocks / (groups * cols));
         for (int64_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
             const int64_t ns = std::min(stripes_per_launch, nstripes - s0);
             a.stripe_begin = s0;
-            launch_skew(skew, skew_rows, depth, true, dim3((unsigned)(ns * groups)), stream, a);
+            launch_skew(skew, skew_rows, depth, true, threads, dim3((unsigned)(ns * groups * cols)), stream, a);
         }
-        first = groups * skew;
+        first = groups * skew * cols;  // in units of `chunk`
     }
     run(false, first, full - first);
     run(true, full, tail_chunks);

@@ -57,7 +57,9 @@ SETS = {
                  {"depth": 2, "skew_chunks": 0, "block_threads": 256}, {"depth": 12, "layout_select": 0}],
     # the skewed-chunk kernel on colliding and non-colliding pitches: what the rotation repairs
     "skewcheck": [{}, {"skew_chunks": 4, "block_threads": 256}, {"skew_chunks": 2, "block_threads": 256},
-                  {"skew_chunks": 0, "block_threads": 256}, {"skew_chunks": 0, "block_threads": 64}],
+                  {"skew_chunks": 0, "block_threads": 256}, {"skew_chunks": 0, "block_threads": 64},
+                  {"skew_chunks": 4, "block_threads": 64}, {"skew_chunks": 2, "block_threads": 64},
+                  {"skew_chunks": 4, "block_threads": 64, "depth": 4}, {"skew_chunks": 4, "block_threads": 64, "stagger": 2}],
     # the 8-row Clay(4,2) repair map across sub-chunk sizes
     "clay": [{}, {"block_threads": 64}, {"skew_chunks": 2}, {"stagger": 2}, {"stagger": 8},
              {"block_threads": 64, "stagger": 2}, {"block_threads": 64, "stagger": 8}, {"chunk_major": 1},

@@ -1126,9 +1126,10 @@ def test_small_tiles_auto_picks_lrc_repair(ecx, torch_dev):
 @pytest.mark.parametrize("nbytes", [8192 * 3 + 4096, 4096 * 9 + 100, 65536])
 def test_skew_chunks_agree(ecx, torch_dev, nbytes):
     """k_gf_apply_skew (ecx_tune "skew_chunks" 2 / 4: several chunks per workgroup,
-    rotated chunk order) gives the bytes of the one-chunk kernel for 2-, 4- and 8-row
-    single-tile maps, with chunk counts that leave a remainder for the one-chunk kernel
-    and a ragged tail, in place (RS) and with accumulation (partial sums)."""
+    rotated chunk order; on 256-thread workgroups, and in the diagnostic build on one-wave
+    workgroups, whose 1 KiB columns take the same 4 KiB-spaced rotation) gives the bytes of the one-chunk kernel for 2-,
+    4- and 8-row single-tile maps, with chunk counts that leave a remainder for the
+    one-chunk kernel and a ragged tail, in place (RS) and with accumulation (partial sums)."""
     torch = torch_dev
     S = 3
     rs = ecx.ReedSolomon.create(12, 4)
@@ -1146,22 +1147,27 @@ def test_skew_chunks_agree(ecx, torch_dev, nbytes):
             nin = int(mp.matrix()[1].max()) + 1
             nout = int(mp.matrix()[2].max()) + 1
             outs = []
-            for skew in (0, 2, 4, 1):
-                ecx.tune("skew_chunks", skew)
-                for acc in (False, True):
-                    o = torch.zeros((S, nout, pitch), dtype=torch.uint8, device="cuda")
-                    if acc:
-                        o.fill_(0x5A)
-                        mp.accumulate_batch(src, 48 * pitch, pitch, o, nout * pitch, pitch, S, nbytes)
-                    else:
-                        mp.apply_batch(src, 48 * pitch, pitch, o, nout * pitch, pitch, S, nbytes)
-                    torch.cuda.synchronize()
-                    outs.append((skew, acc, o))
-            for skew, acc, o in outs:
-                ref = [x for s2, a2, x in outs if s2 == 0 and a2 == acc][0]
-                assert torch.equal(o, ref), (mp.info(), skew, acc, nin)
+            for bt in (0, 256, 64):
+                ecx.tune("block_threads", bt)
+                for skew in (0, 2, 4, 1):
+                    ecx.tune("skew_chunks", skew)
+                    for acc in (False, True):
+                        o = torch.zeros((S, nout, pitch), dtype=torch.uint8, device="cuda")
+                        if acc:
+                            o.fill_(0x5A)
+                            mp.accumulate_batch(src, 48 * pitch, pitch, o, nout * pitch, pitch, S, nbytes)
+                        else:
+                            mp.apply_batch(src, 48 * pitch, pitch, o, nout * pitch, pitch, S, nbytes)
+                        torch.cuda.synchronize()
+                        outs.append((bt, skew, acc, o, ecx.last_kernel()))
+            for bt, skew, acc, o, kern in outs:
+                ref = [x for b2, s2, a2, x, _ in outs if b2 == 0 and s2 == 0 and a2 == acc][0]
+                assert torch.equal(o, ref), (mp.info(), bt, skew, acc, nin, kern)
+            if diag_build() and nbytes == 65536 and mp.info()["n_out"] <= 4:  # one-wave skew: diagnostic build
+                assert any(k.startswith("k_gf_apply_skew") and k.endswith(", 64>") for *_, k in outs), outs
     finally:
         ecx.tune("skew_chunks", 1)
+        ecx.tune("block_threads", 0)
 
 
 @pytest.mark.parametrize("S", [7, 16])
@@ -1182,7 +1188,7 @@ def test_stagger_unit_orders_agree(ecx, torch_dev, S):
     outs = {}
     try:
         for G in (0, 2, 3, 4, 8, 64):
-            for bt, skew in ((256, 0), (64, 0), (256, 4), (256, 2)):
+            for bt, skew in ((256, 0), (64, 0), (256, 4), (256, 2), (64, 4), (64, 2)):
                 ecx.tune("stagger", G)
                 ecx.tune("block_threads", bt)
                 ecx.tune("skew_chunks", skew)
