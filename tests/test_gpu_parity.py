@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from conftest import diag_build, shortened_clay_oracle
+from conftest import diag_build, gf_apply_numpy, shortened_clay_oracle
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -1168,6 +1168,70 @@ def test_skew_chunks_agree(ecx, torch_dev, nbytes):
     finally:
         ecx.tune("skew_chunks", 1)
         ecx.tune("block_threads", 0)
+
+
+@pytest.mark.parametrize("nbytes", [200000, 2 * 4096 + 16, 4096 + 4080, 1024 + 48, 64, 4000])
+def test_partial_last_chunk_in_main_launch(ecx, torch_dev, nbytes):
+    """A shard whose byte count is a multiple of 16 but not of the chunk (RS(17,3) on the
+    published 200,000-B shards) runs its partial last chunk in the main k_gf_apply launch
+    as a workgroup over the shard's last chunk-sized window that stores only the partial
+    chunk (kernels.hip launch_apply_core); shards shorter than one chunk and layouts whose
+    outputs are inputs of the same launch keep the byte-safe launch.  RS(17,3) encode in place
+    (3 rows), a 2-row decode to a separate buffer in 256-thread and one-wave workgroups,
+    overwrite and accumulate, and an in-place map whose output slot is also an input slot:
+    every result equals the oracle's, and no byte outside the shards changes."""
+    torch = torch_dev
+    S = 5
+    pitch = nbytes + 4096 + 48  # guard bytes after every slot (and 16-B aligned slots)
+    rs = ecx.ReedSolomon.create(17, 3)
+    pool = torch.empty((S, 20, pitch), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 5)
+    before = pool.clone()
+    rs.encode_map().apply_batch(pool, 20 * pitch, pitch, pool, 20 * pitch, pitch, S, nbytes)
+    torch.cuda.synchronize()
+    host, ref_host = pool.cpu().numpy(), before.cpu().numpy()
+    for s in (0, S - 1):
+        shards = [ref_host[s, i, :nbytes].copy() for i in range(20)]
+        O.ReedSolomon(17, 3).encode_parity(shards, 0, nbytes)
+        for i in range(20):
+            assert (host[s, i, :nbytes] == shards[i]).all(), (s, i)
+    assert (host[:, :, nbytes:] == ref_host[:, :, nbytes:]).all()  # nothing past the shards
+    # 2-row decode to a separate buffer, both workgroup sizes, overwrite and accumulate
+    r12 = ecx.ReedSolomon.create(12, 4)
+    mat, ins, outs = r12.decode_map([False, False] + [True] * 14).matrix()
+    dmap = r12.decode_map([False, False] + [True] * 14)
+    src = pool[:, :16]
+    try:
+        for bt in (0, 256, 64):
+            ecx.tune("block_threads", bt)
+            for acc in (False, True):
+                o = torch.full((S, 2, pitch), 0x3C if acc else 0, dtype=torch.uint8, device="cuda")
+                if acc:
+                    dmap.accumulate_batch(pool, 20 * pitch, pitch, o, 2 * pitch, pitch, S, nbytes)
+                else:
+                    dmap.apply_batch(pool, 20 * pitch, pitch, o, 2 * pitch, pitch, S, nbytes)
+                torch.cuda.synchronize()
+                oh = o.cpu().numpy()
+                for s in (0, S - 1):
+                    want = gf_apply_numpy(mat, [host[s, int(j), :nbytes] for j in ins])
+                    for r in range(2):
+                        w = want[r] ^ np.uint8(0x3C) if acc else want[r]
+                        assert (oh[s, int(outs[r]), :nbytes] == w).all(), (bt, acc, s, r)
+                assert (oh[:, :, nbytes:] == (0x3C if acc else 0)).all(), (bt, acc)
+    finally:
+        ecx.tune("block_threads", 0)
+    del src
+    # in place, an output slot that is also an input slot (slot 0 <- slot 0 + 2 * slot 1):
+    # every output byte must come from the inputs as they were before the launch
+    gm = ecx.GfMap.from_matrix(np.array([[1, 2]], np.uint8), in_slot=[0, 1], out_slot=[0])
+    buf = pool[:, :2].contiguous()
+    b0 = buf.cpu().numpy()
+    gm.apply_batch(buf, 2 * pitch, pitch, buf, 2 * pitch, pitch, S, nbytes)
+    torch.cuda.synchronize()
+    b1 = buf.cpu().numpy()
+    want = gf_apply_numpy(np.array([[1, 2]], np.uint8), [b0[:, 0, :nbytes].reshape(-1), b0[:, 1, :nbytes].reshape(-1)])[0]
+    assert (b1[:, 0, :nbytes].reshape(-1) == want).all()
+    assert (b1[:, 1] == b0[:, 1]).all() and (b1[:, 0, nbytes:] == b0[:, 0, nbytes:]).all()
 
 
 @pytest.mark.parametrize("S", [7, 16])
