@@ -230,7 +230,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 
 template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS, int ROWS>
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint64_t in_base, uint64_t out_base,
-                                           uint32_t lane16, int valid, uint2 *lds_tab) {
+                                           uint32_t lane16, int valid, uint2 *lds_tab, bool store_lane = true) {
     const uint8_t *ib = reinterpret_cast<const uint8_t *>(in_base) + lane16;
     const uint32_t zoff = lane16;
     const int ebeg = (int)tile[0];
@@ -313,7 +313,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
             u32x4 v = acc[o];
             if (a.accumulate) v ^= SAFE ? load_partial(p, valid) : load16(p);  // wave-uniform branch
             if (SAFE) store_partial(p, v, valid);
-            else st16<NTS>(p, v);
+            else if (store_lane) st16<NTS>(p, v);
         }
     }
 }
@@ -323,11 +323,13 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
 // TLDS: dynamic LDS holds the tile's low table dwords (launch_apply sizes it to the
 // longest padded tile).
 // ROWS < kTileRows: every tile of the map has at most ROWS rows (Shape::rows).
-template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS, int ROWS>
-__global__ void __launch_bounds__(THREADS, ROWS < kTileRows ? (DEPTH >= 12 ? 5 : 6)
-                                                            : (DEPTH == 2 ? 8 : (DEPTH == 4 ? 6 : (DEPTH <= 8 ? 5 : (DEPTH <= 12 ? 4 : 3)))))
-    k_gf_apply(ApplyArgs a) {
-    extern __shared__ uint2 lds_tab[];
+// TAIL (k_gf_apply_tail): the launch also covers a shard's partial last chunk (ApplyArgs::tail_chunk,
+// its byte count a multiple of 16).  That workgroup covers the last THREADS x 16 bytes of the
+// shard instead, and only the lanes on the partial chunk store -- a scalar base shift, no
+// per-lane address change -- so the chunk needs no byte-safe launch of its own.  A kernel of its
+// own: the branch alone, never taken, cost the other instances 0.1-1.2 % (profiles/r04_tail_ab.jsonl).
+template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS, int ROWS, bool TAIL>
+__device__ __forceinline__ void apply_unit(const ApplyArgs &a, uint2 *lds_tab) {
     const uint32_t w = logical_block(a.xcd_group, (uint32_t)a.n_tiles, (uint32_t)a.xcd_run);
     const uint32_t tl = w % (uint32_t)a.n_tiles;
     const uint32_t rest = w / (uint32_t)a.n_tiles;
@@ -337,16 +339,38 @@ __global__ void __launch_bounds__(THREADS, ROWS < kTileRows ? (DEPTH >= 12 ? 5 :
     unit_of(rest, (uint32_t)a.n_chunks, nst, a.chunk_major, (uint32_t)a.stagger, s, c);
     s += a.stripe_begin;
     c += a.chunk_begin;
-    const int64_t cbase = c * (THREADS * 16);
+    int64_t cbase = c * (THREADS * 16);
     int valid = 16;
+    bool store_lane = true;
     if (SAFE) {
         const int64_t v = a.nbytes - cbase - (int64_t)threadIdx.x * 16;
         valid = v <= 0 ? 0 : (v >= 16 ? 16 : (int)v);
     }
+    if constexpr (TAIL) {
+        if (c == a.tail_chunk) {
+            cbase = a.nbytes - THREADS * 16;
+            store_lane = threadIdx.x * 16 >= (uint32_t)(THREADS * 16 - a.tail_bytes);
+        }
+    }
     apply_tile<SAFE, NTL, NTS, DEPTH, TLDS, THREADS, ROWS>(a, plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords,
                                             uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase)),
                                             uniform64((uint64_t)(a.out + s * a.out_stripe_stride + cbase)),
-                                            threadIdx.x * 16, valid, lds_tab);
+                                            threadIdx.x * 16, valid, lds_tab, store_lane);
+}
+
+#define ECX_APPLY_BOUNDS(ROWS, DEPTH) \
+    (ROWS < kTileRows ? (DEPTH >= 12 ? 5 : 6) : (DEPTH == 2 ? 8 : (DEPTH == 4 ? 6 : (DEPTH <= 8 ? 5 : (DEPTH <= 12 ? 4 : 3)))))
+
+template <bool SAFE, bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS, int ROWS>
+__global__ void __launch_bounds__(THREADS, ECX_APPLY_BOUNDS(ROWS, DEPTH)) k_gf_apply(ApplyArgs a) {
+    extern __shared__ uint2 lds_tab[];
+    apply_unit<SAFE, NTL, NTS, DEPTH, TLDS, THREADS, ROWS, false>(a, lds_tab);
+}
+
+// Single-tile maps with NT loads and stores, SGPR tables, 8 accumulator rows, depth 4 or 8.
+template <int DEPTH, int THREADS>
+__global__ void __launch_bounds__(THREADS, ECX_APPLY_BOUNDS(kTileRows, DEPTH)) k_gf_apply_tail(ApplyArgs a) {
+    apply_unit<false, true, 1, DEPTH, false, THREADS, kTileRows, true>(a, nullptr);
 }
 
 // Run-time launch shape of k_gf_apply, mapped onto a template instance by
@@ -357,6 +381,7 @@ struct Shape {
     bool tlds;
     int threads;
     int rows;  // kTileRows, or 2 / 4 for maps whose tiles all have at most that many rows
+    bool tail = false;  // k_gf_apply_tail: ApplyArgs::tail_chunk is in the launch
 };
 
 template <int T>

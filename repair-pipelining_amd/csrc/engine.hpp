@@ -217,6 +217,10 @@ struct ApplyArgs {
     int lane_zero;        // always 0 (keeps k_gf_apply's LDS table base in a VGPR)
     int chunk_major;      // k_gf_apply block order: 0 = stripe by stripe, 1 = chunk c of every stripe, then c + 1
     int stagger;          // k_gf_apply / _skew unit order: > 1 = groups of that many stripes interleaved (unit_of)
+    // k_gf_apply (not byte-safe): the chunk index holding a shard's partial last chunk when it
+    // runs in the same launch as the full chunks (-1: none), and its byte count (a multiple of 16)
+    int64_t tail_chunk;
+    int tail_bytes;
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).

@@ -241,6 +241,27 @@ __global__ void __launch_bounds__(64 * kWaveGroup, DEPTH == 4 ? 6 : 5) k_gf_appl
 #endif  // ECX_DIAG
 
 namespace {
+// May a partial last chunk run in the main launch (apply.hpp: that workgroup re-reads the end of
+// the previous chunk)?  Only if no output byte of the launch is an input byte of it: disjoint
+// buffers, or one buffer laid out as [stripe][slot][bytes] whose output slots are not inputs.
+bool outputs_never_read(const LinearMap &m, const uint8_t *in, int64_t iss, int64_t isl, const uint8_t *out,
+                        int64_t oss, int64_t osl, int64_t nstripes, int64_t nbytes) {
+    if (iss < 0 || isl < 0 || oss < 0 || osl < 0) return false;
+    int max_in = 0, max_out = 0;
+    for (int v : m.in_slot) max_in = std::max(max_in, v);
+    for (int v : m.out_slot) max_out = std::max(max_out, v);
+    const uintptr_t in_lo = (uintptr_t)in, out_lo = (uintptr_t)out;
+    const uintptr_t in_hi = in_lo + (uintptr_t)((nstripes - 1) * iss + (int64_t)max_in * isl + nbytes);
+    const uintptr_t out_hi = out_lo + (uintptr_t)((nstripes - 1) * oss + (int64_t)max_out * osl + nbytes);
+    if (in_hi <= out_lo || out_hi <= in_lo) return true;
+    const int max_slot = std::max(max_in, max_out);
+    if (in != out || iss != oss || isl != osl || isl < nbytes || iss < (int64_t)(max_slot + 1) * isl) return false;
+    for (int o : m.out_slot)
+        for (int i : m.in_slot)
+            if (o == i) return false;
+    return true;
+}
+
 // pick: -1 = the static rules (skew on 4 MiB-multiple input slot pitches, one-wave
 // workgroups for narrow maps otherwise); else shape + 8 * stagger with shape 0 = 256-thread
 // workgroups over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB
@@ -417,7 +438,10 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                       : (tu.xcd_group == 0 && tu.xcd_misaligned && misaligned128 ? 3 : 0);
     a.xcd_run = tu.xcd_run;
     a.accumulate = accumulate ? 1 : 0;
+    a.tail_chunk = -1;
+    a.tail_bytes = 0;
 
+    bool tail_launch = false;  // the next non-safe run covers the partial last chunk (k_gf_apply_tail)
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;
         a.chunk_begin = chunk_begin;
@@ -476,6 +500,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                      (tu.lds_tables == 2 || (tu.lds_tables == 1 && a.n_tiles > 1));
             s.threads = threads;
             s.rows = rows;
+            s.tail = tail_launch && !safe;
             // Residency cap (ecx_tune "occ_lds"): dummy LDS per workgroup.  Auto: the many-stream
             // single-tile maps (>= 8 inputs, rings of <= 8 loads) at 4 waves per SIMD -- 4
             // 256-thread or 16 one-wave workgroups per CU -- instead of the 5 their registers allow.
@@ -520,8 +545,29 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         }
         first = groups * skew * cols;  // in units of `chunk`
     }
-    run(false, first, full - first);
-    run(true, full, tail_chunks);
+    // A partial last chunk whose byte count is a multiple of 16 (RS(17,3) on the published
+    // 200,000-B shards: 48 full 4 KiB chunks and 3,392 B) runs in the same k_gf_apply launch
+    // as the full chunks, as a workgroup over the shard's last chunk-sized window whose lanes
+    // store only the partial chunk (apply.hpp); otherwise the byte-safe kernel takes it in a
+    // launch of its own.
+    const int64_t tail_len = nbytes - full * chunk;
+    const bool fuse_tail = aligned && full >= 1 && tail_len > 0 && tail_len % 16 == 0 && (depth == 4 || depth == 8) &&
+                           cm.n_tiles() == 1 && rows == kTileRows && ntmode == 2 && nts == 1 && tu.lds_tables != 2 &&
+                           !waves && !wide && !bits && !lut && outputs_never_read(cm.map(), in, in_stripe_stride, in_slot_stride, out,
+                                                      out_stripe_stride, out_slot_stride, nstripes, nbytes);
+    if (fuse_tail) {
+        a.tail_chunk = full;
+        a.tail_bytes = (int)tail_len;
+        // (a launch of the partial chunk alone is not the launch's kernel of record)
+        const std::string noted = first == full ? last_kernel() : std::string();
+        tail_launch = true;
+        run(false, first, full + 1 - first);
+        tail_launch = false;
+        if (first == full) set_last_kernel(noted);
+    } else {
+        run(false, first, full - first);
+        run(true, full, tail_chunks);
+    }
     check_hip(hipGetLastError(), "k_gf_apply launch");
 }
 }  // namespace
