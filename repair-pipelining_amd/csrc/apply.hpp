@@ -367,10 +367,11 @@ __global__ void __launch_bounds__(THREADS, ECX_APPLY_BOUNDS(ROWS, DEPTH)) k_gf_a
     apply_unit<SAFE, NTL, NTS, DEPTH, TLDS, THREADS, ROWS, false>(a, lds_tab);
 }
 
-// Single-tile maps with NT loads and stores, SGPR tables, 8 accumulator rows, depth 4 or 8.
-template <int DEPTH, int THREADS>
-__global__ void __launch_bounds__(THREADS, ECX_APPLY_BOUNDS(kTileRows, DEPTH)) k_gf_apply_tail(ApplyArgs a) {
-    apply_unit<false, true, 1, DEPTH, false, THREADS, kTileRows, true>(a, nullptr);
+// Instances (apply_launch.inc): single-tile maps with NT loads and stores, SGPR tables and 8
+// accumulator rows, depth 4 or 8; the parameters name the shape as k_gf_apply's do.
+template <bool NTL, int NTS, int DEPTH, bool TLDS, int THREADS, int ROWS>
+__global__ void __launch_bounds__(THREADS, ECX_APPLY_BOUNDS(ROWS, DEPTH)) k_gf_apply_tail(ApplyArgs a) {
+    apply_unit<false, NTL, NTS, DEPTH, TLDS, THREADS, ROWS, true>(a, nullptr);
 }
 
 // Run-time launch shape of k_gf_apply, mapped onto a template instance by
