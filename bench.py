@@ -36,6 +36,9 @@ contract (same launch, timing and JSON line; the default is the headline):
            encodeParity in place on 200,000-B shards, 4,096 resident stripes per GPU;
            value in its own convention, MB/s of input data (10^6 B,
            ReedSolomonBenchmark.java:116-121), with vs_baseline = value / 525.7 MB/s
+  rs173check the same benchmark's other half (ReedSolomonBenchmark.java:73-87,126-149): RS(17,3)
+           isParityCorrect over the encoded pool, read-only, one verdict byte per stripe; MB/s of
+           data bytes checked (no published figure)
 Every workload carries a cpu_baseline (rank 0, after the timed region, at any N): the
 oracle's restatement of the reference path for that workload on this host's cores.
 """
@@ -72,6 +75,8 @@ WORKLOADS = {
     "lrcenc": ("GiB/s local-parity encode (device-resident), LRC(12,4) 64 KiB blocks, 1/2/4/8 GPU", 1 << 15, 1 << 18),
     "rs173": ("MB/s RS(17,3) encodeParity (device-resident), 200,000-B shards, input data bytes / 10^6 "
               "(ReedSolomonBenchmark convention), 1/2/4/8 GPU", 4096, 1 << 15),
+    "rs173check": ("MB/s RS(17,3) isParityCorrect (device-resident), 200,000-B shards, data bytes checked / 10^6 "
+                   "(ReedSolomonBenchmark convention), 1/2/4/8 GPU", 4096, 1 << 15),
 }
 # the one published reference number for a workload: vs_baseline = value / it
 PUBLISHED = {"rs173": 525.7}  # MB/s, RS(17,3) encodeParity, InputOutputByteTableCodingLoop (rs/README.md:53)
@@ -94,6 +99,9 @@ def parse():
                     help="reference (default): BASELINE.md section 4 / ReedSolomonBenchmark.java:104-124, 2 warm-ups + "
                          "the mean of 10 x 2 s measurements per thread count (~50 s on rank 0 after the timed region); "
                          "bounded: one sample of cpu-seconds/2 on one thread and one of cpu-seconds on all")
+    ap.add_argument("--e2e-seconds", type=float, default=2.0,
+                    help="end-to-end leg (pinned host -> H2D -> kernel -> D2H) after the timed region, on every "
+                         "rank at once: > 0 = its length in seconds; 0 = skip")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-probes", action="store_true", help="skip the in-run memory ceiling probes")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -315,6 +323,48 @@ def pmc_traffic(workload: str, pool: int, kernel: str):
         return None, "unreadable PMC profile: %s" % e
 
 
+E2E_HOST_BYTES = 3 << 30  # pinned host input per rank for the end-to-end leg (at least one stripe)
+
+
+def e2e_rate(ecx, torch, wl, seconds: float):
+    """End-to-end rate of this workload's map on this rank's GPU with the data starting and
+    ending in host memory, as the reference's path does (sub-chunks arrive and leave on
+    sockets, ClayCoordinator.kt:372-395, ClayCodeNode.kt:330-347): pinned host stripes ->
+    pipelined H2D -> the same kernel -> D2H (ecx_*_batch_host, host_pipe.cpp), repeated for
+    >= `seconds`.  The host input holds the first stripes of the GPU run's own (valid) pool;
+    the host outputs are compared with the device run's.  GiBps counts the workload's
+    algorithmic bytes per stripe (as `value`); h2d/d2h_GBps the bytes that crossed PCIe."""
+    import numpy as np
+    if not wl.host_ok:
+        return None
+    sb, ob = wl.host_stripe_bytes(), wl.host_out_bytes()
+    n = max(1, min(wl.P, E2E_HOST_BYTES // sb))
+    hin = ecx.HostBuffer(n * sb)
+    hout = ecx.HostBuffer(n * ob) if ob else None
+    hin.array.reshape(n, sb)[:] = wl.pool[:n].reshape(n, sb).cpu().numpy()
+    ha, ho = hin.array, (hout.array if hout else None)
+    wl.host_call(ha, ho, n)  # warm-up: plans, pipe buffers
+    ok = wl.host_expect(ha, ho if ho is not None else np.empty(0, np.uint8), n)
+    calls, t0 = 0, time.perf_counter()
+    while True:
+        wl.host_call(ha, ho, n)
+        calls += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    h2d, d2h = wl.pcie_bytes()
+    units = calls * n
+    out = {"GiBps": round(units * wl.unit_bytes / el / 2**30, 3),
+           "h2d_GBps": round(units * h2d / el / 1e9, 2), "d2h_GBps": round(units * d2h / el / 1e9, 2),
+           "stripes_per_call": n, "calls": calls, "seconds": round(el, 3), "verified": ok,
+           "path": "pinned host -> H2D -> kernel -> D2H, pipelined (ecx host batch, host_pipe.cpp)"}
+    if wl.metric_unit != "GiB/s":
+        out["value"] = round(units * (wl.metric_bytes or wl.unit_bytes) / el / wl.metric_scale, 1)
+        out["unit"] = wl.metric_unit
+    del hin, hout
+    return out
+
+
 def memory_probes(ecx, torch, region, reads: int, writes: int, reps: int = 5):
     """In-run memory ceilings on this GPU: NT read stream, NT copy
     kernel, hipMemcpyDtoD (torch copy_), each the best of `reps` over 8 GiB regions of
@@ -379,6 +429,35 @@ class Workload:
         cpu_spec() describes."""
         raise NotImplementedError
 
+    # ---- end-to-end (PCIe-inclusive) leg: the same map over pinned host stripes (ecx host batches)
+    host_ok = True        # False: the workload has no host-memory form (the device check)
+
+    def host_stripe_bytes(self) -> int:
+        """Bytes of one stripe in the host input layout (the device pool's layout)."""
+        return self.pool[0].numel()
+
+    def host_out_bytes(self) -> int:
+        """Bytes of one stripe's output in the host output buffer; 0 = written in place."""
+        return self.out[0].numel()
+
+    def host_call(self, hin, hout, n):
+        raise NotImplementedError
+
+    def host_expect(self, hin, hout, n) -> bool:
+        """The host outputs of the first n stripes equal the device run's."""
+        import numpy as np
+        got = (hin if self.host_out_bytes() == 0 else hout)[:n * max(self.host_out_bytes(), 1)]
+        if self.host_out_bytes() == 0:
+            return bool(np.array_equal(got.reshape(n, -1), self.pool[:n].reshape(n, -1).cpu().numpy()))
+        return bool(np.array_equal(got.reshape(n, -1), self.out[:n].reshape(n, -1).cpu().numpy()))
+
+    def pcie_bytes(self):
+        """(H2D, D2H) bytes per stripe: only the map's used input / output slots cross PCIe."""
+        return self.reads * self.sub_bytes(), self.writes * self.sub_bytes()
+
+    def sub_bytes(self) -> int:
+        return self.write_bytes // max(1, self.writes)
+
     def cpu_spec(self) -> dict:
         """How cpu_baseline runs the oracle on this workload: op / data / parity / erased
         for orc_bench_run, make(rng) -> distinct host units [slots][bytes], and per oracle
@@ -406,6 +485,10 @@ class Clay42(Workload):
 
     def launch(self):
         self.step.performCodingBatch(self.pool, STRIPE_BYTES, B, self.out, ALPHA * B, B, self.P, B)
+
+    def host_call(self, hin, hout, n):
+        e = len(self.erased_list)
+        self.step.performCodingBatchHost(hin, STRIPE_BYTES, B, hout, e * ALPHA * B, B, n, B)
 
     def verify(self):
         return bool(self.torch.equal(self.out, self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.erased, :]))
@@ -505,6 +588,10 @@ class Clay104(Workload):
         n, a, b = self.n, self.alpha, self.b
         self.step.performCodingBatch(self.pool, n * a * b, b, self.out, a * b, b, self.P, b)
 
+    def host_call(self, hin, hout, n_):
+        n, a, b = self.n, self.alpha, self.b
+        self.step.performCodingBatchHost(hin, n * a * b, b, hout, a * b, b, n_, b)
+
     def verify(self):
         orig = self.pool.view(self.P, self.alpha, self.n, self.b)[:, :, self.erased, :]
         return bool(self.torch.equal(self.out, orig))
@@ -577,6 +664,16 @@ class RS124(Workload):
     def selected_map(self):
         return self.dmap, self.pitch
 
+    def host_out_bytes(self):
+        return 0
+
+    def host_call(self, hin, hout, n):
+        p = self.pitch
+        self.dmap.apply_batch_host(hin, 16 * p, p, hin, 16 * p, p, n, self.L)
+
+    def sub_bytes(self):
+        return self.L
+
     def verify(self):
         return bool(self.torch.equal(self.pool[:, 0:2, :self.L], self.orig))
 
@@ -633,6 +730,12 @@ class RS173(Workload):
     def selected_map(self):
         return self.rs.encode_map(), self.L
 
+    def host_out_bytes(self):
+        return 0
+
+    def host_call(self, hin, hout, n):
+        self.rs.encode_map().apply_batch_host(hin, 20 * self.L, self.L, hin, 20 * self.L, self.L, n, self.L)
+
     def verify(self):
         """The parity the GPU wrote equals the oracle's on two stripes, and re-encoding
         leaves every stripe unchanged (isParityCorrect over the whole pool)."""
@@ -670,6 +773,85 @@ class RS173(Workload):
                         "200,000-B shards"}
 
 
+class RS173Check(RS173):
+    """ReedSolomonBenchmark's "Check" half (ReedSolomonBenchmark.java:73-87,126-149): RS(17,3)
+    isParityCorrect (ReedSolomon.java:129-178) over the encoded pool of 200,000-B shards,
+    read-only (k_gf_check: the syndromes OR-folded in registers, one verdict byte per stripe).
+    The roofline prices the 20 shards read per stripe; nothing is written but the verdicts."""
+    reads, writes = 20, 0
+    unit_bytes = 20 * 200 * 1000        # 17 data + 3 parity shards read
+    write_bytes = 0
+    metric_bytes = 17 * 200 * 1000      # bytesChecked += BUFFER_SIZE * DATA_COUNT (:139)
+    data_desc = "synthetic (device splitmix64 data shards, GPU encodeParity; the timed launch is the check itself)"
+
+    def __init__(self, ecx, torch, dev, P, seed):
+        super().__init__(ecx, torch, dev, P, seed)
+        RS173.launch(self)  # valid parity everywhere, as the benchmark's encode pass leaves it
+        self.verdict = torch.zeros(P, dtype=torch.uint8, device=dev)
+        self.description = ("RS(17,3) isParityCorrect (read-only, one verdict per stripe), 200,000-B shards back to "
+                             "back (the published shape)")
+
+    def launch(self):
+        self.rs.isParityCorrectBatch(self.pool, 20 * self.L, self.L, self.P, 0, self.L, self.verdict)
+
+    def selected_map(self):
+        return None
+
+    host_ok = False  # the check's host form is the per-call isParityCorrect (ecx_rs_is_parity_correct)
+
+    def verify(self):
+        """Every stripe passes; a flipped byte in a data shard (stripe 1, byte 0), in a parity
+        shard (stripe P-2, the 3,392-B partial last chunk) fails exactly that stripe; both are
+        restored afterwards; the verdicts equal the oracle's isParityCorrect on those stripes."""
+        import oracle as O
+        self.launch()
+        self.torch.cuda.synchronize()
+        if not bool((self.verdict == 1).all()):
+            return False
+        bad = [(1, 0, 0), (self.P - 2, 18, self.L - 100)]
+        for s_, sh, b in bad:
+            self.pool[s_, sh, b] ^= 0x40
+        self.launch()
+        self.torch.cuda.synchronize()
+        got = self.verdict.cpu().numpy()
+        want = [0 if s_ in (1, self.P - 2) else 1 for s_ in range(self.P)]
+        ok = got.tolist() == want
+        for s_, _, _ in bad:
+            shards = [x.copy() for x in self.pool[s_].cpu().numpy()]
+            ok = ok and not O.ReedSolomon(self.k, self.m).is_parity_correct(shards, 0, self.L)
+        for s_, sh, b in bad:
+            self.pool[s_, sh, b] ^= 0x40
+        self.launch()
+        self.torch.cuda.synchronize()
+        return ok and bool((self.verdict == 1).all())
+
+    def sample(self):
+        s_ = self.P // 2
+        return self.pool[s_].cpu().numpy(), self.verdict[s_:s_ + 1].cpu().numpy()
+
+    def oracle_check(self, stripe, got):
+        import oracle as O
+        shards = [stripe[i].copy() for i in range(20)]
+        return bool(O.ReedSolomon(self.k, self.m).is_parity_correct(shards, 0, self.L)) == bool(got[0])
+
+    def cpu_spec(self):
+        import numpy as np
+        import oracle as O
+
+        def make(rng):  # valid stripes: the check must pass (the benchmark throws otherwise)
+            out = []
+            for _ in range(8):
+                st = rng.integers(0, 256, (20, self.L), dtype=np.uint8)
+                shards = [st[i] for i in range(20)]
+                O.ReedSolomon(self.k, self.m).encode_parity(shards, 0, self.L)
+                out.append(st)
+            return out
+        return {"op": O.BENCH_RS_CHECK, "data": self.k, "parity": self.m, "erased": [], "make": make,
+                "arena_slot": np.arange(20), "present": np.ones(20, np.int64), "data_kind": "valid-stripe",
+                "what": "RS(17,3) isParityCorrect with a temp buffer (ReedSolomon.java:159-178, "
+                        "InputOutputByteTableCodingLoop.checkSomeShards), 200,000-B shards"}
+
+
 class LRCEncode(Workload):
     """Config 3, encode half (LRCErasureCodeExample.kt:30-60): each local group of 3 data
     blocks gets its XOR parity (RS(3,1) encodeParity, parity row [1, 1, 1]), written in place
@@ -699,6 +881,13 @@ class LRCEncode(Workload):
 
     def selected_map(self):
         return self.emap, self.b
+
+    def host_out_bytes(self):
+        return 0
+
+    def host_call(self, hin, hout, n):
+        b = self.b
+        self.emap.apply_batch_host(hin, 16 * b, b, hin, 16 * b, b, n, b)
 
     def verify(self):
         """Re-encoding leaves every stripe unchanged, and two stripes' parities equal the oracle's."""
@@ -769,6 +958,10 @@ class LRC(Workload):
     def launch(self):
         b = self.b
         self.rmap.apply_batch(self.pool, 16 * b, b, self.out, b, b, self.P, b)
+
+    def host_call(self, hin, hout, n):
+        b = self.b
+        self.rmap.apply_batch_host(hin, 16 * b, b, hout, b, b, n, b)
 
     def verify(self):
         return bool(self.torch.equal(self.out[:, 0], self.pool[:, 2]))
@@ -874,6 +1067,8 @@ def main():
         wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed)
     elif args.workload == "rs173":
         wl = RS173(ecx, torch, dev, P, seed)
+    elif args.workload == "rs173check":
+        wl = RS173Check(ecx, torch, dev, P, seed)
     elif args.workload == "lrcenc":
         wl = LRCEncode(ecx, torch, dev, P, seed)
     else:
@@ -955,6 +1150,23 @@ def main():
         per_rank = [float(x.item()) for x in g]
     per_rank_gibs = [stripes_per_step * args.steps * metric_bytes / e / wl.metric_scale for e in per_rank]
 
+    # the end-to-end leg: every rank at once (they share the host's PCIe and memory), after the
+    # timed region; the line carries rank 0's figures and the whole-job sum
+    e2e = None
+    if args.e2e_seconds > 0:
+        if grouped:
+            dist.barrier()
+        mine = e2e_rate(ecx, torch, wl, args.e2e_seconds)
+        if mine is not None:
+            rates = [mine["GiBps"]]
+            if grouped:
+                g = [torch.zeros(1, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+                     for _ in range(world)]
+                dist.all_gather(g, torch.tensor([mine["GiBps"]], dtype=torch.float64, device=g[0].device))
+                rates = [float(x.item()) for x in g]
+            e2e = dict(mine, rank0_GiBps=mine["GiBps"], GiBps=round(sum(rates), 3),
+                       per_rank_GiBps=[round(r, 3) for r in rates])
+
     sample = units = None
     if rank == 0 and args.cpu_seconds > 0:
         sample = wl.sample()  # one pool unit for the oracle check
@@ -1015,6 +1227,7 @@ def main():
             "per_rank_%s" % ("GiBps" if wl.metric_unit == "GiB/s" else "MBps"): {"min": round(min(per_rank_gibs), 3), "max": round(max(per_rank_gibs), 3),
                                "ranks": [round(v, 3) for v in per_rank_gibs]},
             "cpu_baseline": cpu,
+            "e2e": e2e,
             "verified": verified,
         }
         print(json.dumps(line), flush=True)

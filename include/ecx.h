@@ -143,6 +143,14 @@ int ecx_map_apply_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe
  * parity shards k..n-1 are overwritten for bytes [offset, offset + byte_count). */
 int ecx_rs_encode_parity_batch(ecx_rs *rs, uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
                                int64_t nstripes, int64_t offset, int64_t byte_count, void *stream);
+/* ReedSolomon.isParityCorrect (ReedSolomon.java:129-178; the "Check" half of
+ * ReedSolomonBenchmark.java:73-87,126-149) over nstripes device-resident stripes (same layout
+ * as ecx_rs_encode_parity_batch), read-only: verdict[s] (a device byte array of nstripes) is
+ * set to 1 when every parity shard of stripe s equals the parity of its data over bytes
+ * [offset, offset + byte_count), else 0.  Nothing is written to the shards. */
+int ecx_rs_is_parity_correct_batch(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
+                                   int64_t nstripes, int64_t offset, int64_t byte_count, uint8_t *verdict,
+                                   void *stream);
 /* ReedSolomon.decodeMissing (ReedSolomon.java:189-286) over nstripes device-resident
  * stripes, in place (same layout): every shard with shard_present[i] == 0 is rebuilt,
  * data from the first k present shards (ascending index), parity from all data -- the
@@ -249,6 +257,22 @@ int ecx_map_apply_batch_host(const ecx_map *map, const uint8_t *in, int64_t in_s
 int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
                                        int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
                                        int64_t out_sub_stride, int64_t nstripes, int64_t buf_size);
+/* The same over several GPUs of this process (one host thread, stream set and
+ * buffer ring per GPU).  Device j of `devices` (ndev entries, HIP ordinals; repeats allowed)
+ * takes the contiguous stripe range [j*S/ndev, (j+1)*S/ndev) (the remainder spread over the
+ * first ranges, as shard_stripes), on a worker thread of its own; the call returns when every
+ * worker has finished.  An out-of-range device id or ndev <= 0 is refused
+ * (ECX_E_ILLEGAL_ARGUMENT) before anything is copied; on a failure every device is drained and
+ * the first failing device's status is returned.  The calling thread's current device is
+ * unchanged. */
+int ecx_map_apply_batch_host_devices(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
+                                     int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride,
+                                     int64_t out_slot_stride, int64_t nstripes, int64_t byte_count,
+                                     const int *devices, int ndev);
+int ecx_clay_perform_coding_batch_host_devices(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
+                                               int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
+                                               int64_t out_sub_stride, int64_t nstripes, int64_t buf_size,
+                                               const int *devices, int ndev);
 /* Page-locked host memory for the calls above (e.g. backing direct ByteBuffers). */
 int ecx_host_alloc(int64_t nbytes, void **out);
 int ecx_host_free(void *ptr);

@@ -1,5 +1,7 @@
 package com.backblaze.erasure.ecx;
 
+import java.nio.ByteBuffer;
+
 /**
  * Status codes of libecx.so (include/ecx.h:40-50) mapped back onto the exceptions the
  * reference throws for the same conditions, with the library's thread-local message.
@@ -58,6 +60,26 @@ public final class Ecx {
             f[i] = (byte) (present[i] ? 1 : 0);
         }
         return f;
+    }
+
+    /**
+     * A direct ByteBuffer of exactly {@code nbytes} over page-locked host memory
+     * (ecx_host_alloc), for the host-batch calls to run at the PCIe rate.  Its capacity is the
+     * allocation's size, so the capacity-checked host-batch natives bound every access to it.
+     * Release it with {@link #freePinned}.
+     */
+    public static ByteBuffer allocatePinned(long nbytes) {
+        if (nbytes < 0) {
+            throw new IllegalArgumentException("negative size");
+        }
+        long[] p = new long[1];
+        check(EcxNative.hostAlloc(nbytes, p));
+        return EcxNative.wrapAddress(p[0], nbytes);
+    }
+
+    /** Frees a buffer from {@link #allocatePinned}; the buffer must not be used afterwards. */
+    public static void freePinned(ByteBuffer buffer) {
+        check(EcxNative.hostFree(EcxNative.directAddress(buffer)));
     }
 
     /** Creates the codec handle of ReedSolomon.create(k, m) (ReedSolomon.java:34-61). */

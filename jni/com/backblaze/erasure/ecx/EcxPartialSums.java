@@ -8,7 +8,7 @@ package com.backblaze.erasure.ecx;
  * ClayCodeNode.kt:182-186 and :225-228 (Clay chain).
  */
 public final class EcxPartialSums {
-    private final long rs;
+    private long rs;  // 0 once closed
     private final int dataShards;
 
     /** The codec of ReedSolomon.create(dataShards, parityShards). */
@@ -20,7 +20,7 @@ public final class EcxPartialSums {
     /** ReedSolomon.encodeParitySingle: output ^= parityRows[outputIndex][inputIndex] * shard. */
     public void encodeParitySingle(byte[] shard, byte[] output, int inputIndex, int outputIndex, int offset,
                                    int byteCount) {
-        Ecx.check(EcxNative.rsEncodeParitySingle(rs, shard, output, inputIndex, outputIndex, offset, byteCount));
+        Ecx.check(EcxNative.rsEncodeParitySingle(handle(), shard, output, inputIndex, outputIndex, offset, byteCount));
     }
 
     /**
@@ -49,12 +49,28 @@ public final class EcxPartialSums {
                 }
             }
         }
-        Ecx.check(EcxNative.rsDecodeMissingSingle(rs, shard, shardIndex, index, Ecx.flags(shardPresent), outputs,
+        Ecx.check(EcxNative.rsDecodeMissingSingle(handle(), shard, shardIndex, index, Ecx.flags(shardPresent), outputs,
                 null, outputs.length, offset, byteCount, isFirst ? 1 : 0));
     }
 
-    /** Releases the native codec. */
-    public void close() {
-        EcxNative.rsDestroy(rs);
+    private long handle() {
+        if (rs == 0) {
+            throw new IllegalStateException("EcxPartialSums is closed");
+        }
+        return rs;
+    }
+
+    /**
+     * Releases this wrapper's reference to the native codec.  Idempotent: the codec is
+     * shared by every wrapper of the same (k, m) (ecx_rs_create), so a second release would
+     * drop another wrapper's reference; later calls on this wrapper throw IllegalStateException.
+     */
+    public synchronized void close() {
+        if (rs == 0) {
+            return;
+        }
+        long h = rs;
+        rs = 0;
+        EcxNative.rsDestroy(h);
     }
 }

@@ -16,7 +16,7 @@ import java.nio.ByteBuffer;
  * affect only caller-visible side effects (DESIGN.md section 5).
  */
 public class EcxClayCodeErasureDecodingStep {
-    private final long clay;
+    private long clay;  // 0 once closed
     private final int numErased;
 
     public EcxClayCodeErasureDecodingStep(int[] erasedIndexes, int numDataUnits, int numParityUnits) {
@@ -29,7 +29,7 @@ public class EcxClayCodeErasureDecodingStep {
     /** Sub-packetization alpha (ClayCodeUtil, ClayCodeErasureDecodingStep.java:690-695). */
     public int subPacketSize() {
         int[] q = new int[1], t = new int[1], alpha = new int[1];
-        Ecx.check(EcxNative.clayGeometry(clay, q, t, alpha));
+        Ecx.check(EcxNative.clayGeometry(handle(), q, t, alpha));
         return alpha[0];
     }
 
@@ -65,7 +65,7 @@ public class EcxClayCodeErasureDecodingStep {
             outArrays[i] = out[i].array();
             outPos[i] = out[i].arrayOffset() + out[i].position();
         }
-        Ecx.check(EcxNative.clayPerformCoding(clay, inArrays, inPos, outArrays, outPos, bufSize));
+        Ecx.check(EcxNative.clayPerformCoding(handle(), inArrays, inPos, outArrays, outPos, bufSize));
         for (ByteBuffer b : in) {
             if (b != null) {
                 b.position(b.position() + bufSize);
@@ -81,7 +81,7 @@ public class EcxClayCodeErasureDecodingStep {
      */
     public void performCodingBatch(long in, long inStripeStride, long inSubStride, long out, long outStripeStride,
                                    long outSubStride, long nstripes, long bufSize, long stream) {
-        Ecx.check(EcxNative.clayPerformCodingBatch(clay, in, inStripeStride, inSubStride, out, outStripeStride,
+        Ecx.check(EcxNative.clayPerformCodingBatch(handle(), in, inStripeStride, inSubStride, out, outStripeStride,
                 outSubStride, nstripes, bufSize, stream));
     }
 
@@ -106,14 +106,41 @@ public class EcxClayCodeErasureDecodingStep {
             checkExtent(in, "input", inStripeStride, inSubStride, slots[0], nstripes, bufSize);
             checkExtent(out, "output", outStripeStride, outSubStride, slots[1], nstripes, bufSize);
         }
-        Ecx.check(EcxNative.clayPerformCodingBatchHostBuffer(clay, in, inStripeStride, inSubStride, out,
+        Ecx.check(EcxNative.clayPerformCodingBatchHostBuffer(handle(), in, inStripeStride, inSubStride, out,
                 outStripeStride, outSubStride, nstripes, bufSize));
+    }
+
+    /**
+     * performCodingBatchHost split over several GPUs of this process (SURVEY.md 8(e)): device
+     * j of {@code devices} repairs the contiguous stripe range j of devices.length (the
+     * remainder on the first ranges) with a host thread, streams and buffer ring of its own;
+     * returns when every device has finished.  Same buffer contract and checks as
+     * performCodingBatchHost; an unknown device id throws IllegalArgumentException before
+     * anything is copied.
+     */
+    public void performCodingBatchHostDevices(ByteBuffer in, long inStripeStride, long inSubStride, ByteBuffer out,
+                                              long outStripeStride, long outSubStride, long nstripes, long bufSize,
+                                              int[] devices) {
+        if (devices == null || devices.length == 0) {
+            throw new IllegalArgumentException("no devices");
+        }
+        if (nstripes < 0 || bufSize < 0 || inStripeStride < 0 || inSubStride < 0 || outStripeStride < 0
+                || outSubStride < 0) {
+            throw new IllegalArgumentException("negative batch count, size or stride");
+        }
+        if (numErased > 0 && nstripes > 0 && bufSize > 0) {
+            int[] slots = maxSlots();
+            checkExtent(in, "input", inStripeStride, inSubStride, slots[0], nstripes, bufSize);
+            checkExtent(out, "output", outStripeStride, outSubStride, slots[1], nstripes, bufSize);
+        }
+        Ecx.check(EcxNative.clayPerformCodingBatchHostDevicesBuffer(handle(), in, inStripeStride, inSubStride, out,
+                outStripeStride, outSubStride, nstripes, bufSize, devices, devices.length));
     }
 
     /** Highest input and output sub-chunk slot of the repair (ecx_map_slot_extent). */
     private int[] maxSlots() {
         long[] m = new long[1];
-        Ecx.check(EcxNative.clayMap(clay, m));
+        Ecx.check(EcxNative.clayMap(handle(), m));
         int[] in = new int[1], out = new int[1];
         Ecx.check(EcxNative.mapSlotExtent(m[0], in, out));
         return new int[] {in[0], out[0]};
@@ -144,8 +171,24 @@ public class EcxClayCodeErasureDecodingStep {
         return numErased;
     }
 
-    /** Releases the native decoding step. */
-    public void close() {
-        EcxNative.clayDestroy(clay);
+    private long handle() {
+        if (clay == 0) {
+            throw new IllegalStateException("EcxClayCodeErasureDecodingStep is closed");
+        }
+        return clay;
+    }
+
+    /**
+     * Releases this step's reference to the native decoding step.  Idempotent: equal steps
+     * share one reference-counted native object (ecx_clay_create), so a second release would
+     * drop another step's reference; later calls on this step throw IllegalStateException.
+     */
+    public synchronized void close() {
+        if (clay == 0) {
+            return;
+        }
+        long h = clay;
+        clay = 0;
+        EcxNative.clayDestroy(h);
     }
 }

@@ -151,6 +151,8 @@ RULES = {
                                                   L("outputs", "cl_a", "buf_size", nulls=True)]),
     "ecx_lrc_map": ((), [A("block_present", "16")]),
     "ecx_lrc_decode_batch": ((), [A("block_present", "16")]),
+    "ecx_map_apply_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
+    "ecx_clay_perform_coding_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
 }
 
 
@@ -168,17 +170,37 @@ BUFFER_VARIANTS = {
                                            "        if (st == ECX_OK) st = ecx_map_slot_extent(cm, &max_in, &max_out);\n"
                                            "    }", "cl_ne > 0"),
 }
+# the multi-GPU forms take the same buffers, extents and conditions
+BUFFER_VARIANTS["ecx_map_apply_batch_host_devices"] = BUFFER_VARIANTS["ecx_map_apply_batch_host"]
+BUFFER_VARIANTS["ecx_clay_perform_coding_batch_host_devices"] = BUFFER_VARIANTS["ecx_clay_perform_coding_batch_host"]
+
+
+def host_address_native(name):
+    """Host-batch exports whose buffers are raw host addresses (longs): their natives are
+    package-private, so Java callers outside com.backblaze.erasure.ecx reach them only
+    through the capacity-checked <camel>Buffer forwarders (ClayCoordinator.kt:378-390)."""
+    return "_batch_host" in name
 
 
 def buffer_variant(ret, name, params):
     """The <camel>Buffer forwarder of a host-batch export (BUFFER_VARIANTS)."""
     query, extent, when = BUFFER_VARIANTS[name]
     names = [p for _, p in params]
-    handle, length = names[0], names[-1]
-    jparams, cparams, args, bufs = [], ["JNIEnv *env", "jclass cls"], [], []
+    handle = names[0]
+    length = next(p for p in reversed(names) if p in ("byte_count", "buf_size"))
+    jparams, cparams, args, bufs, ints = [], ["JNIEnv *env", "jclass cls"], [], [], []
     for i, (t, p) in enumerate(params):
         kind = classify(name, t, p)[0]
-        if kind == "addr":
+        if kind == "int":
+            jparams.append("int %s" % camel("ecx_" + p))
+            cparams.append("jint %s" % p)
+            args.append("(int)%s" % p)
+        elif kind == "ints":  # copied out of the Java array (no critical region), length-checked
+            jparams.append("int[] %s" % camel("ecx_" + p))
+            cparams.append("jintArray %s" % p)
+            ints.append((p, names[i + 1]))
+            args.append("%s_c" % p)
+        elif kind == "addr":
             jparams.append("ByteBuffer %s" % camel("ecx_" + p))
             cparams.append("jobject %s" % p)
             bufs.append((p, names[i + 1], names[i + 2]))
@@ -200,7 +222,16 @@ def buffer_variant(ret, name, params):
     for p, ss, sl in bufs:
         body.append("    if (%s) st = direct_check(env, %s, %s, %s, %s, nstripes, %s, &%s_p);"
                     % (cond, p, ss, sl, "max_in" if p == "in" else "max_out", length, p))
+    for p, cnt in ints:
+        body.append("    int *%s_c = NULL;" % p)
+        body.append("    if (st == ECX_OK && %s < 0) st = ECX_E_ILLEGAL_ARGUMENT;" % cnt)
+        body.append("    if (st == ECX_OK) st = array_check(env, %s, %s, 0, ECX_E_ILLEGAL_ARGUMENT);" % (p, cnt))
+        body.append("    if (st == ECX_OK && !(%s_c = (int *)malloc(sizeof(int) * ((size_t)%s + 1)))) st = ECX_E_NOMEM;"
+                    % (p, cnt))
+        body.append("    if (st == ECX_OK) (*env)->GetIntArrayRegion(env, %s, 0, %s, (jint *)%s_c);" % (p, cnt, p))
     body.append("    if (st == ECX_OK) st = %s(%s);" % (name, ", ".join(args)))
+    for p, _ in ints:
+        body.append("    free(%s_c);" % p)
     body.append("    return st;")
     jname = camel(name) + "Buffer"
     c = ("\n/* %s over direct ByteBuffers, extent-checked from their capacity */\n"
@@ -389,7 +420,8 @@ static int direct_check(JNIEnv *env, jobject buf, int64_t stripe_stride, int64_t
     return need > (int64_t)cap ? ECX_E_INDEX : ECX_OK;
 }
 
-/* Address of a direct ByteBuffer (host-batch calls take addresses). */
+/* Address of a direct ByteBuffer (package-private on the Java side: host-batch callers use
+ * the capacity-checked ByteBuffer forwarders). */
 JNIEXPORT jlong JNICALL Java_%(J)s_directAddress(JNIEnv *env, jclass cls, jobject buffer) {
     (void)cls;
     return (jlong)(intptr_t)(*env)->GetDirectBufferAddress(env, buffer);
@@ -419,11 +451,13 @@ public final class EcxNative {
     private EcxNative() {
     }
 
-    /** Address of a direct ByteBuffer (for the host-batch entry points). */
-    public static native long directAddress(ByteBuffer buffer);
+    /** Address of a direct ByteBuffer.  Package-private: outside this package host batches
+     *  go through the capacity-checked ByteBuffer forwarders. */
+    static native long directAddress(ByteBuffer buffer);
 
-    /** A direct ByteBuffer over host memory (e.g. pinned memory from hostAlloc). */
-    public static native ByteBuffer wrapAddress(long address, long nbytes);
+    /** A direct ByteBuffer over host memory.  Package-private (a caller-chosen capacity would
+     *  defeat the forwarders' extent checks): use {@link Ecx#allocatePinned}. */
+    static native ByteBuffer wrapAddress(long address, long nbytes);
 """)
     for ret, name, params in exports():
         jname = camel(name)
@@ -437,7 +471,10 @@ public final class EcxNative {
                 cparams.append("jintArray %s_positions" % p)
         jret = {"constchar*": "String", "int": "int", "void": "void"}[ret]
         cret = {"constchar*": "jstring", "int": "jint", "void": "void"}[ret]
-        java.append("\n    public static native %s %s(%s);\n" % (jret, jname, ", ".join(jparams)))
+        vis = "" if host_address_native(name) else "public "
+        if vis == "":
+            java.append("\n    /** Raw host addresses: package-private (use %sBuffer). */" % jname)
+        java.append("\n    %sstatic native %s %s(%s);\n" % (vis, jret, jname, ", ".join(jparams)))
         body = []
         pre, pin, unpin, post, args = [], [], [], [], []
         pnames = {p: kind for (kind, _, _), t, p in kinds}

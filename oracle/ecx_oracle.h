@@ -108,7 +108,7 @@ int orc_clay_get_inputs(int data_units, int parity_units, int block_size, uint8_
 /* orc_bench.c -- timing harness (bench.py cpu_baseline): `threads` workers, each with its
  * own Clay step object, repair `erased` on their own `per_thread` stripes for `seconds`.
  * stripes: [threads*per_thread][n*alpha] sub-chunk pointers (NULL = absent). */
-enum { ORC_BENCH_CLAY = 0, ORC_BENCH_RS_DECODE = 1, ORC_BENCH_RS_ENCODE = 2 };
+enum { ORC_BENCH_CLAY = 0, ORC_BENCH_RS_DECODE = 1, ORC_BENCH_RS_ENCODE = 2, ORC_BENCH_RS_CHECK = 3 };
 /* Generic form: `op` on units of `slots` pointers ([threads*per_thread][slots]): Clay
  * (data, parity, erased) repair of n*alpha sub-chunk pointers, or RS(data, parity)
  * decodeMissing (erased = the missing shards) / encodeParity over n shard pointers of

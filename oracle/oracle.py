@@ -349,7 +349,7 @@ def shortened_clay_perform_coding(k, m, v, erased_real, inputs_real, B):
     return outs
 
 
-BENCH_CLAY, BENCH_RS_DECODE, BENCH_RS_ENCODE = 0, 1, 2
+BENCH_CLAY, BENCH_RS_DECODE, BENCH_RS_ENCODE, BENCH_RS_CHECK = 0, 1, 2, 3
 
 
 def bench_run(op, data, parity, erased, buf_size, addrs, threads, seconds):

@@ -13,6 +13,9 @@
  *                        RS(3,1) is the LRC local-group repair (LRCErasureCodeExample.kt:100-131)
  *   ORC_BENCH_RS_ENCODE  ReedSolomon.encodeParity (ReedSolomon.java:94-108), the operation
  *                        ReedSolomonBenchmark.java times
+ *   ORC_BENCH_RS_CHECK   ReedSolomon.isParityCorrect with a temp buffer (ReedSolomon.java:159-178),
+ *                        the "Check" half of ReedSolomonBenchmark.java:73-87,126-149; a stripe
+ *                        whose parity is wrong fails the run, as the benchmark throws
  * Nothing here is used by the product (libecx.so).
  */
 #define _POSIX_C_SOURCE 200809L
@@ -47,6 +50,7 @@ typedef struct {
     uint8_t *present; /* RS decode: shard flags */
     uint8_t **outs;   /* Clay: |E| * alpha repaired sub-chunks */
     uint8_t *out_mem;
+    uint8_t *temp;    /* RS check: the benchmark's tempBuffer (one shard) */
 } op_state;
 
 static int op_init(worker_t *w, op_state *s) {
@@ -67,6 +71,7 @@ static int op_init(worker_t *w, op_state *s) {
     if (!s->present) return ORC_E_NOMEM;
     memset(s->present, 1, (size_t)(w->k + w->m));
     for (int i = 0; i < w->n_erased; i++) s->present[w->erased[i]] = 0;
+    if (w->op == ORC_BENCH_RS_CHECK && !(s->temp = (uint8_t *)malloc((size_t)w->buf))) return ORC_E_NOMEM;
     return 0;
 }
 
@@ -75,6 +80,10 @@ static int op_run(worker_t *w, op_state *s, uint8_t *const *unit) {
     case ORC_BENCH_CLAY: return orc_clay_perform_coding(s->clay, unit, s->outs, w->buf);
     case ORC_BENCH_RS_DECODE: return orc_rs_decode_missing(s->rs, unit, s->present, w->k + w->m, w->buf, 0, w->buf);
     case ORC_BENCH_RS_ENCODE: return orc_rs_encode_parity(s->rs, unit, w->k + w->m, w->buf, 0, w->buf);
+    case ORC_BENCH_RS_CHECK: {
+        const int ok = orc_rs_is_parity_correct(s->rs, unit, w->k + w->m, w->buf, 0, w->buf, s->temp, w->buf);
+        return ok == 1 ? 0 : (ok < 0 ? ok : ORC_E_ILLEGAL_ARGUMENT); /* "parity not correct" */
+    }
     default: return ORC_E_ILLEGAL_ARGUMENT;
     }
 }
@@ -83,6 +92,7 @@ static void op_free(op_state *s) {
     free(s->outs);
     free(s->out_mem);
     free(s->present);
+    free(s->temp);
     if (s->clay) orc_clay_free(s->clay);
     if (s->rs) orc_rs_free(s->rs);
 }
@@ -111,7 +121,8 @@ int orc_bench_run(int op, int data, int parity, const int *erased, int n_erased,
                   uint8_t *const *units, int slots, int per_thread, int threads, double seconds, long long *reps,
                   double *elapsed) {
     if (threads < 1 || per_thread < 1 || buf_size < 1 || slots < 1 || n_erased < 0) return ORC_E_ILLEGAL_ARGUMENT;
-    if (op != ORC_BENCH_CLAY && op != ORC_BENCH_RS_DECODE && op != ORC_BENCH_RS_ENCODE) return ORC_E_ILLEGAL_ARGUMENT;
+    if (op != ORC_BENCH_CLAY && op != ORC_BENCH_RS_DECODE && op != ORC_BENCH_RS_ENCODE && op != ORC_BENCH_RS_CHECK)
+        return ORC_E_ILLEGAL_ARGUMENT;
     (void)orc_mul_table(); /* the GF tables, built before the threads start */
     worker_t *w = (worker_t *)calloc((size_t)threads, sizeof(worker_t));
     pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));

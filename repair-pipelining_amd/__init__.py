@@ -477,6 +477,19 @@ class GfMap:
                                              _host_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
                                              byte_count))
 
+    def apply_batch_host_devices(self, inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride,
+                                 out_slot_stride, nstripes, byte_count, devices):
+        """apply_batch_host split over several GPUs (ecx_map_apply_batch_host_devices): device j
+        of ``devices`` takes the contiguous stripe range shard_stripes(nstripes, len(devices), j)
+        on a worker thread of its own; synchronous."""
+        self._check(inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
+                    byte_count)
+        devs = np.ascontiguousarray(list(devices), np.int32)
+        check(lib().ecx_map_apply_batch_host_devices(self._h, _host_ptr(inp), in_stripe_stride, in_slot_stride,
+                                                     _host_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
+                                                     byte_count, devs.ctypes.data if len(devs) else None,
+                                                     len(devs)))
+
 
 # ---------------------------------------------------------------- ReedSolomon.java
 class ReedSolomon:
@@ -555,6 +568,18 @@ class ReedSolomon:
                       "shards")
         check(lib().ecx_rs_encode_parity_batch(self._h, _dev_ptr(shards), stripe_stride, shard_stride, nstripes,
                                                offset, byteCount, _stream(stream)))
+
+    def isParityCorrectBatch(self, shards, stripe_stride, shard_stride, nstripes, firstByte, byteCount, verdict,
+                             stream=None) -> None:
+        """isParityCorrect over nstripes device-resident stripes, read-only
+        (ecx_rs_is_parity_correct_batch): the device uint8 array ``verdict`` (nstripes bytes)
+        receives 1 for each stripe whose parity is correct over [firstByte, firstByte +
+        byteCount), else 0.  Enqueued on ``stream``; read verdict after synchronising."""
+        _check_layout(shards, stripe_stride, shard_stride, self.getTotalShardCount() - 1, nstripes,
+                      firstByte + byteCount, "shards")
+        _check_layout(verdict, 1, 0, 0, nstripes, 1, "verdict")
+        check(lib().ecx_rs_is_parity_correct_batch(self._h, _dev_ptr(shards), stripe_stride, shard_stride, nstripes,
+                                                   firstByte, byteCount, _dev_ptr(verdict), _stream(stream)))
 
     def decodeMissingBatch(self, shards, shardPresent, stripe_stride, shard_stride, nstripes, offset, byteCount,
                            stream=None):
@@ -740,6 +765,19 @@ class ClayCodeErasureDecodingStep:
         check(lib().ecx_clay_perform_coding_batch_host(self._h, _host_ptr(inp), in_stripe_stride, in_sub_stride,
                                                        _host_ptr(out), out_stripe_stride, out_sub_stride, nstripes,
                                                        bufSize))
+
+    def performCodingBatchHostDevices(self, inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride,
+                                      out_sub_stride, nstripes, bufSize, devices) -> None:
+        """performCodingBatchHost split over several GPUs of this process
+        (ecx_clay_perform_coding_batch_host_devices): contiguous stripe ranges, one worker
+        thread and pipe per device entry."""
+        self._check_batch(inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
+                          bufSize)
+        devs = np.ascontiguousarray(list(devices), np.int32)
+        check(lib().ecx_clay_perform_coding_batch_host_devices(self._h, _host_ptr(inp), in_stripe_stride,
+                                                               in_sub_stride, _host_ptr(out), out_stripe_stride,
+                                                               out_sub_stride, nstripes, bufSize,
+                                                               devs.ctypes.data if len(devs) else None, len(devs)))
 
 
 class JavaRandom:

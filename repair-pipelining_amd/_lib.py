@@ -105,6 +105,7 @@ SIGNATURES = {
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_rs_decode_map": (I, [P, P, ctypes.POINTER(P)]),
     "ecx_rs_encode_parity_batch": (I, [P, P, I64, I64, I64, I64, I64, P]),
+    "ecx_rs_is_parity_correct_batch": (I, [P, P, I64, I64, I64, I64, I64, P, P]),
     "ecx_rs_decode_missing_batch": (I, [P, P, P, I64, I64, I64, I64, I64, P]),
     "ecx_rs_decode_partial_batch": (I, [P, P, I, P, I64, P, I64, I64, I64, I64, I, P]),
     "ecx_rs_encode_partial_batch": (I, [P, I, P, I64, P, I64, I64, I64, I64, I, P]),
@@ -123,6 +124,8 @@ SIGNATURES = {
     "ecx_lrc_decode_batch": (I, [P, I64, I64, P, I64, I64, P]),
     "ecx_map_apply_batch_host": (I, [P, P, I64, I64, P, I64, I64, I64, I64]),
     "ecx_clay_perform_coding_batch_host": (I, [P, P, I64, I64, P, I64, I64, I64, I64]),
+    "ecx_map_apply_batch_host_devices": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P, I]),
+    "ecx_clay_perform_coding_batch_host_devices": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P, I]),
     "ecx_host_alloc": (I, [I64, ctypes.POINTER(P)]),
     "ecx_host_free": (I, [P]),
     "ecx_host_register": (I, [P, I64]),

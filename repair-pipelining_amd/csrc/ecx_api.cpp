@@ -192,6 +192,27 @@ ecx_map *rs_decode_map(ecx_rs *rs, const std::vector<bool> &present) {
     return slot.get();
 }
 
+// isParityCorrect's map (ReedSolomon.java:129-178): row p = parityRows[p] over the data
+// shards plus 1 x parity shard p, i.e. the syndrome, all zero exactly when the parity is right.
+ecx_map *rs_check_map(ecx_rs *rs) {
+    const RsCode &c = rs->code;
+    std::lock_guard<std::mutex> lk(rs->mu);
+    if (!rs->check) {
+        LinearMap lm;
+        lm.n_out = c.m();
+        lm.n_in = c.n();
+        lm.a.assign((size_t)c.m() * c.n(), 0);
+        for (int p = 0; p < c.m(); ++p) {
+            std::memcpy(&lm.a[(size_t)p * c.n()], c.parity_row(p), (size_t)c.k());
+            lm.a[(size_t)p * c.n() + c.k() + p] = 1;
+            lm.out_slot.push_back(p);
+        }
+        for (int j = 0; j < c.n(); ++j) lm.in_slot.push_back(j);
+        rs->check = std::make_unique<ecx_map>(lm.pruned());
+    }
+    return rs->check.get();
+}
+
 ecx_map *clay_standard_map(ecx_clay *c) {
     const int n = c->pl.n_real(), a = c->pl.alpha();
     std::vector<bool> present((size_t)n * a, true);
@@ -564,26 +585,21 @@ int ecx_rs_is_parity_correct(ecx_rs *rs, uint8_t *const *shards, int shard_count
         check_buffers(rs->code, shards, shard_count, shard_length, first_byte, byte_count);
         if (temp_buffer && (long long)temp_length < (long long)first_byte + byte_count)
             throw Error(ECX_E_ILLEGAL_ARGUMENT, "tempBuffer is not big enough");
-        const RsCode &c = rs->code;
-        ecx_map *m;
-        {
-            std::lock_guard<std::mutex> lk(rs->mu);
-            if (!rs->check) {
-                LinearMap lm;
-                lm.n_out = c.m();
-                lm.n_in = c.n();
-                lm.a.assign((size_t)c.m() * c.n(), 0);
-                for (int p = 0; p < c.m(); ++p) {
-                    std::memcpy(&lm.a[(size_t)p * c.n()], c.parity_row(p), (size_t)c.k());
-                    lm.a[(size_t)p * c.n() + c.k() + p] = 1;
-                    lm.out_slot.push_back(p);
-                }
-                for (int j = 0; j < c.n(); ++j) lm.in_slot.push_back(j);
-                rs->check = std::make_unique<ecx_map>(lm.pruned());
-            }
-            m = rs->check.get();
-        }
-        return run_host_all_zero(m->cm, shards, first_byte, byte_count) ? 1 : 0;
+        return run_host_all_zero(rs_check_map(rs)->cm, shards, first_byte, byte_count) ? 1 : 0;
+    });
+}
+
+int ecx_rs_is_parity_correct_batch(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
+                                   int64_t nstripes, int64_t offset, int64_t byte_count, uint8_t *verdict,
+                                   void *stream) {
+    return guarded(__func__, [&]() -> int {
+        if (!rs) throw Error(ECX_E_NULL, "null codec");
+        if (nstripes < 0 || offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (nstripes == 0) return ECX_OK;
+        if (!base || !verdict) throw Error(ECX_E_NULL, "null device pointer");
+        launch_check(rs_check_map(rs)->cm, base + offset, stripe_stride, shard_stride, verdict, nstripes, byte_count,
+                     (hipStream_t)stream);
+        return ECX_OK;
     });
 }
 
@@ -1068,6 +1084,37 @@ int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_
         ecx_map *m = clay_standard_map(clay);
         run_host_batch(m->cm, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
                        buf_size);
+        return ECX_OK;
+    });
+}
+
+int ecx_map_apply_batch_host_devices(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
+                                     int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride,
+                                     int64_t out_slot_stride, int64_t nstripes, int64_t byte_count,
+                                     const int *devices, int ndev) {
+    return guarded(__func__, [&]() -> int {
+        if (!map) throw Error(ECX_E_NULL, "null map");
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null host pointer");
+        run_host_batch_devices(const_cast<ecx_map *>(map)->cm, in, in_stripe_stride, in_slot_stride, out,
+                               out_stripe_stride, out_slot_stride, nstripes, byte_count, devices, ndev);
+        return ECX_OK;
+    });
+}
+
+int ecx_clay_perform_coding_batch_host_devices(ecx_clay *clay, const uint8_t *in, int64_t in_stripe_stride,
+                                               int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
+                                               int64_t out_sub_stride, int64_t nstripes, int64_t buf_size,
+                                               const int *devices, int ndev) {
+    return guarded(__func__, [&]() -> int {
+        if (!clay) throw Error(ECX_E_NULL, "null decoding step");
+        if (!devices) throw Error(ECX_E_NULL, "null device list");
+        if (ndev <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "empty device list");
+        if (clay->pl.erased().empty()) return ECX_OK;
+        if (nstripes < 0 || buf_size < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!in || !out) throw Error(ECX_E_NULL, "null host pointer");
+        run_host_batch_devices(clay_standard_map(clay)->cm, in, in_stripe_stride, in_sub_stride, out,
+                               out_stripe_stride, out_sub_stride, nstripes, buf_size, devices, ndev);
         return ECX_OK;
     });
 }

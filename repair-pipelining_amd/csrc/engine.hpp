@@ -354,6 +354,11 @@ int layout_candidate_code(int cand);
 void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride, uint8_t *out,
                   int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes,
                   hipStream_t stream, bool accumulate = false);
+// isParityCorrect over device-resident stripes (apply_check.hip k_gf_check): `cm` is a check
+// map (one syndrome row per parity shard); verdict[s] = 1 when every syndrome byte of stripe s
+// over [0, nbytes) is zero, else 0.  Read-only on the stripes.
+void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                  uint8_t *verdict, int64_t nstripes, int64_t nbytes, hipStream_t stream);
 void launch_fill_random(uint8_t *dst, int64_t nbytes, uint64_t seed, hipStream_t stream);
 void launch_count_mismatch(const uint8_t *a, int64_t a_stride, const uint8_t *b, int64_t b_stride, int64_t nrows,
                            int64_t row_bytes, uint64_t *d_count, hipStream_t stream);
@@ -407,5 +412,13 @@ bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t of
 void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                     uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                     int64_t nbytes);
+
+// run_host_batch over several devices (host_pipe.cpp): device j of `devices` takes the
+// contiguous stripe range j of ndev (remainder on the first), on a worker thread of its own
+// with that device's pipe.  Refuses bad device ids before any copy; joins every worker, then
+// throws the first failing device's error.
+void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                            uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                            int64_t nbytes, const int *devices, int ndev);
 
 }  // namespace ecx

@@ -16,6 +16,7 @@
 // that are also consecutive in host memory are merged into one strided (2D)
 // copy per chunk.
 #include <algorithm>
+#include <thread>
 
 #include "engine.hpp"
 
@@ -160,6 +161,55 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
         p.drain();
         throw;
     }
+}
+
+void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                            uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                            int64_t nbytes, const int *devices, int ndev) {
+    if (!devices) throw Error(ECX_E_NULL, "null device list");
+    if (ndev <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "empty device list");
+    int count = 0;
+    check_hip(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    for (int j = 0; j < ndev; ++j)
+        if (devices[j] < 0 || devices[j] >= count)
+            throw Error(ECX_E_ILLEGAL_ARGUMENT, "device " + std::to_string(devices[j]) + " of " +
+                                                    std::to_string(count) + " visible");
+    if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
+    struct Result {
+        int code = ECX_OK;
+        std::string what;
+    };
+    std::vector<Result> res((size_t)ndev);
+    // Device j's range: contiguous, the remainder on the first ranges (shard_stripes, __init__.py).
+    const int64_t base = nstripes / ndev, extra = nstripes % ndev;
+    auto work = [&](int j) {
+        const int64_t lo = j * base + std::min<int64_t>(j, extra), n = base + (j < extra ? 1 : 0);
+        if (n <= 0) return;
+        try {
+            check_hip(hipSetDevice(devices[j]), "hipSetDevice (host batch worker)");
+            run_host_batch(cm, in + lo * in_stripe_stride, in_stripe_stride, in_slot_stride,
+                           out + lo * out_stripe_stride, out_stripe_stride, out_slot_stride, n, nbytes);
+        } catch (const Error &e) {
+            res[(size_t)j] = {e.code, e.what()};
+        } catch (const std::bad_alloc &) {
+            res[(size_t)j] = {ECX_E_NOMEM, "out of memory"};
+        } catch (const std::exception &e) {
+            res[(size_t)j] = {ECX_E_ILLEGAL_ARGUMENT, e.what()};
+        }
+    };
+    // one worker thread per device entry; the caller's thread (and its current device) only waits
+    std::vector<std::thread> th;
+    th.reserve((size_t)ndev);
+    try {
+        for (int j = 0; j < ndev; ++j) th.emplace_back(work, j);
+    } catch (...) {
+        for (std::thread &t : th) t.join();
+        throw Error(ECX_E_NOMEM, "cannot start a host-batch worker thread");
+    }
+    for (std::thread &t : th) t.join();
+    for (int j = 0; j < ndev; ++j)
+        if (res[(size_t)j].code != ECX_OK)
+            throw Error(res[(size_t)j].code, "device " + std::to_string(devices[j]) + ": " + res[(size_t)j].what);
 }
 
 }  // namespace ecx

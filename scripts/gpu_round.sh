@@ -43,7 +43,7 @@ if has gloo2; then
   rc=$?; echo "bench gloo2 rc=$rc"; tail -2 "$OUT/bench_gloo2.log"; [ $rc -ne 0 ] && stop gloo2 $rc
 fi
 if has workloads; then
-  for W in clay104 rs124 lrc clay42x2 rs173 lrcenc; do
+  for W in clay104 rs124 lrc clay42x2 rs173 lrcenc rs173check; do
     timeout -k 10 300 python bench.py --workload $W --steps 3 --warmup 1 > "$OUT/bench_$W.log" 2>&1
     rc=$?; echo "bench $W rc=$rc"; tail -1 "$OUT/bench_$W.log"; [ $rc -ne 0 ] && stop "bench $W" $rc
   done
@@ -56,7 +56,7 @@ fi
 if has prof; then
   export TMPDIR=/tmp
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0) > "$OUT/prof.log" 2>&1
+      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --e2e-seconds 0) > "$OUT/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/prof.log"; [ $rc -ne 0 ] && stop prof $rc
   find "$OUT/prof" -name '*stats*'
 fi

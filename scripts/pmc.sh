@@ -14,18 +14,18 @@ OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-WORKLOADS="${*:-clay42 clay104 rs124 lrc clay42x2 rs173 lrcenc}"
+WORKLOADS="${*:-clay42 clay104 rs124 lrc clay42x2 rs173 lrcenc rs173check}"
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
 for W in $WORKLOADS; do
   case $W in
-    clay42|clay42x2) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; rs173) POOL=4096 ;; lrcenc) POOL=32768 ;; lrc) POOL=32768 ;;
+    clay42|clay42x2) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; rs173|rs173check) POOL=4096 ;; lrcenc) POOL=32768 ;; lrc) POOL=32768 ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
   i=0
   for C in FETCH_SIZE WRITE_SIZE "$SQ"; do
     D="$OUT/pmc_${W}_$i"; mkdir -p "$D"
     timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
-        -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 \
+        -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 --e2e-seconds 0 \
            --stripes-per-step $((POOL * 16)) --no-probes --meta "$D/meta.json" > "$D.log" 2>&1
     rc=$?; echo "pmc $W pass$i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D.log"; exit $rc; }
     i=$((i + 1))

@@ -230,3 +230,43 @@ def test_codec_registry_refcounts_and_bounds_idle(ecx):
     lib.ecx_clay_destroy(h1)
     lib.ecx_clay_destroy(h2)
     assert counts()[2] == cl_live - 1
+
+
+def test_host_batch_devices_argument_checks(ecx):
+    """The multi-GPU host batches refuse an empty or null device list before touching a
+    device (ECX_E_ILLEGAL_ARGUMENT / ECX_E_NULL); without a device, a valid list reaches the
+    device query and fails loudly (ECX_E_DEVICE), never a CPU path."""
+    import numpy as np
+    if _has_device(ecx):
+        pytest.skip("a device is present (the GPU tests cover the calls)")
+    lib = ecx.lib()
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    hin, hout = np.zeros((2, 48, 64), np.uint8), np.zeros((2, 8, 64), np.uint8)
+    args = (step._h, hin.ctypes.data, 48 * 64, 64, hout.ctypes.data, 8 * 64, 64, 2, 64)
+    assert lib.ecx_clay_perform_coding_batch_host_devices(*args, None, 1) == -6
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert lib.ecx_clay_perform_coding_batch_host_devices(*args, devs, 0) == -1
+    assert lib.ecx_clay_perform_coding_batch_host_devices(*args, devs, -3) == -1
+    assert lib.ecx_clay_perform_coding_batch_host_devices(*args, devs, 2) == -10
+    m = step.map()
+    margs = (m._h, hin.ctypes.data, 48 * 64, 64, hout.ctypes.data, 8 * 64, 64, 2, 64)
+    assert lib.ecx_map_apply_batch_host_devices(*margs, None, 1) == -6
+    assert lib.ecx_map_apply_batch_host_devices(*margs, devs, 0) == -1
+    assert lib.ecx_map_apply_batch_host_devices(*margs, devs, 2) == -10
+    assert (hout == 0).all()
+
+
+def test_is_parity_correct_batch_argument_checks(ecx):
+    """ecx_rs_is_parity_correct_batch: negative counts are IllegalArgumentException, a null
+    codec or pointer NullPointerException; an empty batch is a no-op; no CPU path."""
+    lib = ecx.lib()
+    rs = ecx.ReedSolomon.create(17, 3)
+    assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, -1, 0, 64, 16, None) == -1
+    assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, 1, -1, 64, 16, None) == -1
+    assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, 1, 0, -64, 16, None) == -1
+    assert lib.ecx_rs_is_parity_correct_batch(None, 16, 20 * 64, 64, 1, 0, 64, 16, None) == -6
+    assert lib.ecx_rs_is_parity_correct_batch(rs._h, None, 20 * 64, 64, 1, 0, 64, 16, None) == -6
+    assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, 1, 0, 64, None, None) == -6
+    assert lib.ecx_rs_is_parity_correct_batch(rs._h, None, 20 * 64, 64, 0, 0, 64, None, None) == 0
+    if not _has_device(ecx):
+        assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, 1, 0, 64, 16, None) == -10

@@ -699,6 +699,128 @@ def test_rs_host_batch_in_place_unaligned(ecx, small_host_chunks):
     assert (pool[:, (0, 5, 13), L:] == 0x5A).all()  # bytes past the shard untouched
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_clay_host_batch_devices_vs_oracle(ecx, small_host_chunks, devices):
+    """performCodingBatchHostDevices (ecx_clay_perform_coding_batch_host_devices): a ragged
+    stripe count split into contiguous ranges over the device list -- here device 0 several
+    times, each entry a worker thread of its own -- equals the oracle on every stripe."""
+    k, m, B, S, e = 4, 2, 4096, 7, 2
+    rng = np.random.default_rng(77)
+    pool = rng.integers(0, 256, (S, 48, B), dtype=np.uint8)
+    out = np.full((S, 8, B), 0xCD, np.uint8)
+    ecx.ClayCodeErasureDecodingStep([e], k, m).performCodingBatchHostDevices(pool, 48 * B, B, out, 8 * B, B, S, B,
+                                                                              devices)
+    for s in range(S):
+        inputs = [None if (i % 6) == e else pool[s, i].copy() for i in range(48)]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(k, m, [e]).perform_coding(inputs, ref, B)
+        assert all((out[s, z] == ref[z]).all() for z in range(8)), s
+
+
+def test_map_host_batch_devices_and_refusals(ecx, small_host_chunks):
+    """ecx_map_apply_batch_host_devices over [0, 0] with a ragged count equals the one-device
+    host batch; an unknown device id, an empty list or a null list is refused before anything
+    is copied (the output stays untouched)."""
+    k, m, L, S = 12, 4, 5000, 5
+    rs = ecx.ReedSolomon.create(k, m)
+    rng = np.random.default_rng(78)
+    pool = np.zeros((S, 16, L), np.uint8)
+    pool[:, :k] = rng.integers(0, 256, (S, k, L), dtype=np.uint8)
+    one = pool.copy()
+    emap = rs.encode_map()
+    emap.apply_batch_host(one, 16 * L, L, one, 16 * L, L, S, L)
+    emap.apply_batch_host_devices(pool, 16 * L, L, pool, 16 * L, L, S, L, [0, 0])
+    assert (pool == one).all()
+    ref = [one[S - 1, i].copy() for i in range(16)]
+    ref[k:] = [np.zeros(L, np.uint8) for _ in range(m)]
+    O.ReedSolomon(k, m).encode_parity(ref, 0, L)
+    assert all((ref[i] == pool[S - 1, i]).all() for i in range(16))
+    fresh = np.zeros((S, 16, L), np.uint8)
+    fresh[:, :k] = pool[:, :k]
+    for bad in ([ecx.device_count()], [0, -1], []):
+        with pytest.raises(ecx.EcxError) as ei:
+            emap.apply_batch_host_devices(fresh, 16 * L, L, fresh, 16 * L, L, S, L, bad)
+        assert ei.value.code == -1, bad
+        assert (fresh[:, k:] == 0).all()
+
+
+@pytest.mark.parametrize("k,m,L,off,S", [(17, 3, 200000, 0, 6), (4, 2, 104449, 0, 5), (4, 2, 4096 * 3, 16, 4),
+                                         (10, 10, 8192 + 48, 0, 3), (5, 5, 1001, 3, 4), (17, 3, 4096, 0, 3),
+                                         (2, 1, 16, 0, 2)])
+def test_is_parity_correct_batch_vs_oracle(ecx, torch_dev, k, m, L, off, S):
+    """isParityCorrectBatch (k_gf_check, read-only): valid stripes pass; one flipped byte --
+    in a data shard at byte 0, in a parity shard inside the partial last chunk, at the last
+    byte -- fails exactly that stripe, as the oracle's isParityCorrect says; the shards are
+    not written; firstByte / byteCount windows follow ReedSolomon.java:129-178 (a flip
+    outside the window passes).  Shapes: the published RS(17,3) 200,000 B (fused partial
+    chunk), RS(4,2) on the LP-block shard size (ragged: byte-safe tail), an unaligned base
+    (offset 3), RS(10,10) (two 8-row tiles), a shard of one chunk and one of 16 B."""
+    torch = torch_dev
+    n = k + m
+    pitch = off + L + 32
+    rng = np.random.default_rng(k * 1000 + L)
+    host = np.zeros((S, n, pitch), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (S, k, pitch), dtype=np.uint8)
+    rs = ecx.ReedSolomon.create(k, m)
+    for s in range(S):
+        sh = [host[s, i] for i in range(n)]
+        O.ReedSolomon(k, m).encode_parity(sh, off, L)
+    pool = torch.from_numpy(host).cuda()
+    verdict = torch.full((S,), 7, dtype=torch.uint8, device="cuda")
+    rs.isParityCorrectBatch(pool, n * pitch, pitch, S, off, L, verdict)
+    torch.cuda.synchronize()
+    assert verdict.cpu().tolist() == [1] * S
+    flips = {0: (0, off), S - 1: (n - 1, off + L - 1)}
+    if S > 2:
+        flips[1] = (k, off + L - max(1, (L % 4096) // 2))  # a parity shard, in the partial last chunk
+    for s, (i, b) in flips.items():
+        host[s, i, b] ^= 0x81
+    pool = torch.from_numpy(host).cuda()
+    before = pool.clone()
+    rs.isParityCorrectBatch(pool, n * pitch, pitch, S, off, L, verdict)
+    torch.cuda.synchronize()
+    want = [0 if s in flips else 1 for s in range(S)]
+    assert verdict.cpu().tolist() == want
+    assert torch.equal(pool, before)  # read-only
+    for s in range(S):
+        sh = [host[s, i].copy() for i in range(n)]
+        assert O.ReedSolomon(k, m).is_parity_correct(sh, off, L) == bool(want[s])
+    # the window: a check that ends before the last flipped byte passes that stripe
+    if L > 1:
+        rs.isParityCorrectBatch(pool, n * pitch, pitch, S, off, L - 1, verdict)
+        torch.cuda.synchronize()
+        assert verdict.cpu().tolist()[S - 1] == 1
+    # empty: no stripes, or zero bytes (every verdict 1)
+    rs.isParityCorrectBatch(pool, n * pitch, pitch, 0, off, L, verdict)
+    rs.isParityCorrectBatch(pool, n * pitch, pitch, S, off, 0, verdict)
+    torch.cuda.synchronize()
+    assert verdict.cpu().tolist() == [1] * S
+
+
+def test_is_parity_correct_batch_at_benchmark_scale(ecx, torch_dev):
+    """ReedSolomonBenchmark's buffer sets at scale (4,096 RS(17,3) stripes of 200,000 B, 16 GB):
+    GPU encode then GPU check -- every verdict 1 -- then one byte flipped per 512th stripe fails
+    exactly those (the size-independent property at BASELINE size)."""
+    torch = torch_dev
+    S, L = 4096, 200000
+    pool = torch.empty((S, 20, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 99)
+    rs = ecx.ReedSolomon.create(17, 3)
+    rs.encodeParityBatch(pool, 20 * L, L, S, 0, L)
+    verdict = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    rs.isParityCorrectBatch(pool, 20 * L, L, S, 0, L, verdict)
+    torch.cuda.synchronize()
+    assert bool((verdict == 1).all())
+    bad = list(range(0, S, 512))
+    for j, s in enumerate(bad):
+        pool[s, j % 20, (j * 7919) % L] ^= 1
+    rs.isParityCorrectBatch(pool, 20 * L, L, S, 0, L, verdict)
+    torch.cuda.synchronize()
+    v = verdict.cpu().numpy()
+    assert sorted(np.nonzero(v == 0)[0].tolist()) == bad
+    del pool
+
+
 def test_lrc_host_batch_matches_device_batch(ecx, torch_dev):
     """The same map over the same stripes: host and device batch paths agree byte for byte."""
     torch = torch_dev

@@ -66,7 +66,7 @@ def test_one_forwarder_per_export_with_matching_arguments():
 
 def test_java_natives_match_forwarders():
     fw = forwarders()
-    natives = re.findall(r"public static native [\w\[\]]+ (\w+)\(([^)]*)\);", JAVA_SRC)
+    natives = re.findall(r"(?:public )?static native [\w\[\]]+ (\w+)\(([^)]*)\);", JAVA_SRC)
     assert len(natives) == len(fw)
     for jname, params in natives:
         key = "Java_%s_%s" % (gen_jni.JCLASS, jname)
@@ -78,12 +78,14 @@ def test_java_natives_match_forwarders():
 def test_java_classes_use_existing_natives():
     """EcxCodingLoop / EcxPartialSums / EcxClayCodeErasureDecodingStep call only
     natives that EcxNative declares."""
-    declared = set(re.findall(r"public static native [\w\[\]]+ (\w+)\(", JAVA_SRC))
+    public = set(re.findall(r"public static native [\w\[\]]+ (\w+)\(", JAVA_SRC))
+    private = set(re.findall(r"\n    static native [\w\[\]]+ (\w+)\(", JAVA_SRC))
     for f in (ROOT / "jni").rglob("*.java"):
         if f.name == "EcxNative.java":
             continue
+        same_package = "package com.backblaze.erasure.ecx;" in f.read_text()
         for used in re.findall(r"EcxNative\.(\w+)\(", f.read_text()):
-            assert used in declared, (f.name, used)
+            assert used in public or (same_package and used in private), (f.name, used)
     loop = (ROOT / "jni" / "com" / "backblaze" / "erasure" / "EcxCodingLoop.java").read_text()
     assert "extends CodingLoopBase" in loop and "codeSomeShards" in loop and "checkSomeShards" in loop
 
@@ -101,3 +103,25 @@ def test_forwarders_compile():
     finally:
         shutil.rmtree(include, ignore_errors=True)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_no_public_native_takes_a_raw_host_address():
+    """Round-4 verdict item: a Java caller must not bypass the ByteBuffer capacity checks.
+    Every host-batch native that takes raw host addresses (long in / long out), and
+    directAddress / wrapAddress, are package-private; the public host-batch natives take
+    direct ByteBuffers whose capacity the forwarder reads itself (ClayCoordinator.kt:378-390)."""
+    public = dict(re.findall(r"public static native [\w\[\]]+ (\w+)\(([^)]*)\);", JAVA_SRC))
+    for name in ("directAddress", "wrapAddress", "mapApplyBatchHost", "clayPerformCodingBatchHost",
+                 "mapApplyBatchHostDevices", "clayPerformCodingBatchHostDevices"):
+        assert name not in public, name
+        assert re.search(r"\n    static native [\w\[\]]+ %s\(" % name, JAVA_SRC), name
+    host_batch = {n: p for n, p in public.items() if "BatchHost" in n}
+    assert set(host_batch) == {"mapApplyBatchHostBuffer", "clayPerformCodingBatchHostBuffer",
+                               "mapApplyBatchHostDevicesBuffer", "clayPerformCodingBatchHostDevicesBuffer"}
+    for n, params in host_batch.items():
+        assert "ByteBuffer in" in params and "ByteBuffer out" in params, n
+        assert "long in," not in params and "long out," not in params, n
+    # the generated C forwarder reads the capacity of every ByteBuffer it is given
+    for n in host_batch:
+        body = re.search(r"JNICALL Java_%s_%s\(.*?\n\}" % (gen_jni.JCLASS, n), C_SRC, flags=re.S).group(0)
+        assert body.count("direct_check(") == 2, n

@@ -304,6 +304,62 @@ def test_map_batch_host_buffer_extent_checks(J):
         J.call("mapDestroy", mp)
 
 
+def test_clay_batch_host_devices_buffer_checks(J):
+    """clayPerformCodingBatchHostDevicesBuffer: the same capacity checks as the one-GPU form,
+    plus the device list -- shorter than ndev, null, or ndev < 0 -- refused before anything is
+    pinned or copied; a valid call reaches the export (the devices, or ECX_E_DEVICE)."""
+    clay = handle(J, "clayCreate", 4, 2, J.ints([1]), 1)
+    try:
+        S, B = 3, 256
+        iss, isl, oss, osl, _, _ = clay_batch_layout(S, B)
+        inp, out = rnd(S * iss, 1), np.zeros(S * oss, np.uint8)
+        need_in = (S - 1) * iss + 47 * isl + B
+        J.reset()
+        call = lambda i, o, devs, nd: J.call("clayPerformCodingBatchHostDevicesBuffer", clay, i, iss, isl, o,  # noqa: E731
+                                             oss, osl, S, B, devs, nd)
+        assert call(J.direct(inp, need_in - 1), J.direct(out), J.ints([0]), 1) == IDX
+        assert call(J.direct(inp), J.direct(out), J.ints([0]), 2) == ILL   # list shorter than ndev
+        assert call(J.direct(inp), J.direct(out), None, 1) == NUL
+        assert call(J.direct(inp), J.direct(out), J.ints([0]), -1) == ILL
+        assert call(J.array(inp), J.direct(out), J.ints([0]), 1) == NUL     # heap buffer
+        assert J.counters()["pins"] == 0 and (out == 0).all()
+        st = call(J.direct(inp), J.direct(out), J.ints([0, 0]), 2)
+        assert st == (OK if has_device(J) else DEV), st
+        if has_device(J):
+            assert call(J.direct(inp), J.direct(out), J.ints([1 << 20]), 1) == ILL  # unknown device id
+    finally:
+        J.call("clayDestroy", clay)
+
+
+def test_codec_reference_survives_other_releases(J):
+    """The registry side of ADVICE r04 (EcxPartialSums / EcxClayCodeErasureDecodingStep close):
+    two handles of one (k, m) codec are one shared object; releasing one and then more than
+    64 other codecs (the idle cache) leaves the other usable -- which is why the Java close()
+    now releases at most once (asserted on the Java sources below)."""
+    a = handle(J, "rsCreate", 6, 3)
+    b = handle(J, "rsCreate", 6, 3)
+    assert a == b
+    J.call("rsDestroy", a)
+    for k in range(2, 2 + 70):
+        h = handle(J, "rsCreate", k, 1)
+        J.call("rsDestroy", h)
+    k_, m_ = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    assert J.call("rsShape", b, J.array(k_), J.array(m_)) == OK and (k_[0], m_[0]) == (6, 3)
+    mat = np.zeros(9 * 6, np.uint8)
+    assert J.call("rsMatrix", b, J.array(mat)) == OK
+    assert (mat.reshape(9, 6)[:6] == np.eye(6, dtype=np.uint8)).all()
+    J.call("rsDestroy", b)
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1] / "jni"
+    for f, field in (("com/backblaze/erasure/ecx/EcxPartialSums.java", "rs"),
+                     ("distributed/erasure/coding/clay/EcxClayCodeErasureDecodingStep.java", "clay")):
+        src = (root / f).read_text()
+        close = src[src.index("public synchronized void close()"):]
+        close = close[:close.index("\n    }\n")]
+        assert "if (%s == 0)" % field in close and "%s = 0;" % field in close, f
+        assert "private long %s;" % field in src and "IllegalStateException" in src, f
+
+
 def test_java_wrapper_uses_the_checked_variant():
     """EcxClayCodeErasureDecodingStep.performCodingBatchHost goes through the capacity-checked
     native and checks the same extent in Java first (ArrayIndexOutOfBoundsException /
@@ -411,6 +467,29 @@ def test_clay_batch_host_buffer_via_jni_vs_oracle(J):
             ins = [None if i % n == 1 else inp[s_ * iss + i * B:s_ * iss + (i + 1) * B].copy() for i in range(n * a)]
             ref = [np.zeros(B, np.uint8) for _ in range(a)]
             O.Clay(4, 2, [1]).perform_coding(ins, ref, B)
+            for z in range(a):
+                assert (out[s_ * oss + z * B:s_ * oss + (z + 1) * B] == ref[z]).all(), (s_, z)
+    finally:
+        J.call("clayDestroy", clay)
+
+
+@pytest.mark.gpu
+def test_clay_batch_host_devices_buffer_via_jni_vs_oracle(J):
+    """The multi-GPU forwarder over device list [0, 0] (two workers), a ragged 5 stripes:
+    every repaired sub-chunk equals the oracle's performCoding."""
+    clay = handle(J, "clayCreate", 4, 2, J.ints([4]), 1)
+    try:
+        S, B, n, a = 5, 4096, 6, 8
+        iss, isl, oss, osl, _, _ = clay_batch_layout(S, B)
+        inp = rnd(S * iss, 13)
+        out = np.full(S * oss, 0x5A, np.uint8)
+        st = J.call("clayPerformCodingBatchHostDevicesBuffer", clay, J.direct(inp), iss, isl, J.direct(out), oss, osl,
+                    S, B, J.ints([0, 0]), 2)
+        assert st == OK, st
+        for s_ in range(S):
+            ins = [None if i % n == 4 else inp[s_ * iss + i * B:s_ * iss + (i + 1) * B].copy() for i in range(n * a)]
+            ref = [np.zeros(B, np.uint8) for _ in range(a)]
+            O.Clay(4, 2, [4]).perform_coding(ins, ref, B)
             for z in range(a):
                 assert (out[s_ * oss + z * B:s_ * oss + (z + 1) * B] == ref[z]).all(), (s_, z)
     finally:
