@@ -78,6 +78,10 @@ WORKLOADS = {
     "rs173check": ("MB/s RS(17,3) isParityCorrect (device-resident), 200,000-B shards, data bytes checked / 10^6 "
                    "(ReedSolomonBenchmark convention), 1/2/4/8 GPU", 4096, 1 << 15),
 }
+# ecx_tune keys the product library always accepts (include/ecx_tune.h); --tune of any other key
+# opts this process in to the shape knobs (ECX_SHAPE_KNOBS=1)
+DEPLOYMENT_KEYS = {"layout_select", "plan_cache", "roctx", "host_chunk_kib", "host_buffers", "host_gather_kib",
+                   "host_zero_copy", "host_contexts"}
 # the one published reference number for a workload: vs_baseline = value / it
 PUBLISHED = {"rs173": 525.7}  # MB/s, RS(17,3) encodeParity, InputOutputByteTableCodingLoop (rs/README.md:53)
 
@@ -1023,7 +1027,7 @@ def main():
     import torch.distributed as dist
 
     import rpamd
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=any(kv.partition("=")[0] not in DEPLOYMENT_KEYS for kv in args.tune))
 
     # ECX_BENCH_BACKEND=gloo rehearses the multi-process path on a box with fewer
     # GPUs than ranks (ranks share devices round-robin); the default is RCCL, which

@@ -3,6 +3,14 @@
  * Not part of the reference's coding interface (include/ecx.h is the boundary);
  * results are bit-identical for every setting, only speed changes.
  *
+ * Two classes of keys.  DEPLOYMENT keys -- "layout_select", "plan_cache", "roctx" and the
+ * host_* keys -- are always accepted.  Every other key below is a SHAPE key: the product
+ * library accepts it only when the process set ECX_SHAPE_KNOBS=1 in its environment before
+ * its first ecx_tune call (read once; tests, bench.py --tune and the scripts/ A/B harnesses
+ * do), and otherwise refuses it with ECX_E_ILLEGAL_ARGUMENT -- so no caller sharing the
+ * process (another library in the same JVM) can reshape every other caller's launches.  The
+ * diagnostic library (make DIAG=1) accepts every key.
+ *
  *   "depth"            16-B loads per lane in the kernel's load ring: 0 = per map (default:
  *                      20 for a single full tile of 17-20 entries, 8 when every tile has >= 12
  *                      entries, else 4), or force 2 / 4 / 8 / 10 / 12 / 16 / 20 / 24 (2: 8-row

@@ -1167,9 +1167,28 @@ bool lab_key(const std::string &k) {
            k == "rtc_diag" || k == "occ_lds";
 }
 
+// Deployment knobs (host pipeline, per-call plan cache, markers, the layout selection's on/off):
+// what a production caller may set.  Every other key changes a kernel's launch shape -- results
+// are identical, only speed differs -- and is accepted only by the diagnostic library or when the
+// process opted in with ECX_SHAPE_KNOBS=1 in its environment (read once, at the first ecx_tune), so
+// one library loaded into a JVM cannot reshape every other caller's launches.
+bool deployment_key(const std::string &k) {
+    return k == "host_chunk_kib" || k == "host_buffers" || k == "host_gather_kib" || k == "host_zero_copy" ||
+           k == "host_contexts" || k == "roctx" || k == "plan_cache" || k == "layout_select";
+}
+
+bool shape_knobs_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("ECX_SHAPE_KNOBS");
+        return ECX_DIAG || (v && std::strcmp(v, "1") == 0);
+    }();
+    return on;
+}
+
 // One ecx_tune key, under the tuning lock.
 int set_tune(Tuning &t, const std::string &k, int value) {
     if (!ECX_DIAG && lab_key(k)) return ECX_E_ILLEGAL_ARGUMENT;
+    if (!deployment_key(k) && !shape_knobs_enabled()) return ECX_E_ILLEGAL_ARGUMENT;
     if (k == "depth") {
         if (value != 0 && value != 2 && value != 4 && value != 8 && value != 10 && value != 12 && value != 16 &&
             value != 20 && value != 24)

@@ -9,7 +9,12 @@ NAME = "repair_pipelining_amd"
 PKG_DIR = Path(__file__).resolve().parent / "repair-pipelining_amd"
 
 
-def load():
+def load(shape_knobs: bool = False):
+    """The package; with ``shape_knobs`` the process opts in to libecx's launch-shape knobs
+    (ECX_SHAPE_KNOBS=1, include/ecx_tune.h), read by the library at its first ecx_tune call."""
+    if shape_knobs:
+        import os
+        os.environ["ECX_SHAPE_KNOBS"] = "1"
     if NAME in sys.modules:
         return sys.modules[NAME]
     spec = importlib.util.spec_from_file_location(NAME, PKG_DIR / "__init__.py",

@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     for kv in args.tune:
         k_, _, v_ = kv.partition("=")
         ecx.tune(k_, int(v_))

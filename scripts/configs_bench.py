@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--only", default=None, help="substring filter on the config names")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     lib = ecx.lib()
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
     cs = cases(ecx, torch)

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--depths", default="0,8,12,20")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     depths = [int(d) for d in args.depths.split(",")]
     cases = []
     B, P = 32768, 1 << 14

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--variants", default="0:1,4:1,8:1")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     lib = ecx.lib()
     import ctypes
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]

@@ -143,7 +143,7 @@ def main():
     ap.add_argument("--pitches", default=None, help="comma-separated shard+pad byte pairs as L:pad (default: all)")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     buf = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")
     ecx.fill_random(buf, buf.numel(), 7)
     for kind in args.cases.split(","):

@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     lib = ecx.lib()
     lib.ecx_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
     modes = args.mode.split(",") if args.mode else list(MODES)

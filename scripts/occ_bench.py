@@ -36,7 +36,7 @@ def main():
     args = ap.parse_args()
     sets = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv) for s in args.sets.split(";")]
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     for name, k, m, erased, L, pitch in CASES:
         n = k + m
         rs = ecx.ReedSolomon.create(k, m)

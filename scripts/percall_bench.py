@@ -26,7 +26,7 @@ def timeit(fn, reps=50):
 
 def main():
     import numpy as np
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     rng = np.random.default_rng(0)
     cases = []
     for L in (4096, 32768, 1 << 20):

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--pads", default="0,4096,8192,65536")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     buf = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")
     ecx.fill_random(buf, buf.numel(), 7)
     rs = ecx.ReedSolomon.create(12, 4)

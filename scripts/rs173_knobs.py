@@ -46,7 +46,7 @@ def main():
     args = ap.parse_args()
     knobs = {"knobs": KNOBS, "xcd": KNOBS_XCD, "default": [{}], "shapes": KNOBS_SHAPES, "t256": KNOBS_T256}[args.set]
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     K, M = args.k, args.m
     shard = args.shard
     p = shard + args.pad

@@ -15,7 +15,7 @@ import rpamd  # noqa: E402
 
 def main():
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     rs = ecx.ReedSolomon.create(12, 4)
     dmap = rs.decode_map([False, False] + [True] * 14)
     total = 16 << 30  # bytes of stripes resident per variant (6 variants: ~100 GB of HBM)

@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--case", default="both", choices=["rs173", "rs124", "both"])
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     if args.case in ("rs173", "both"):
         for pitch in (200000, 262144):
             run_case(ecx, torch, "RS(17,3) encode", 17, 3, min(pitch, 200000) if pitch == 200000 else pitch, pitch,

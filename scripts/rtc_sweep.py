@@ -29,7 +29,7 @@ def main():
                     "plane-group kernel shapes only")
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     k, m, v, b, a = 10, 4, 2, 4096, 256
     n, P = k + m, args.pool
     pool = torch.empty((P, n * a, b), dtype=torch.uint8, device="cuda")

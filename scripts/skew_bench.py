@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     cases = []
     rs = ecx.ReedSolomon.create(12, 4)
     dmap = rs.decode_map([False, False] + [True] * 14)

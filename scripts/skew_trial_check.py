@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     import torch
-    ecx = rpamd.load()
+    ecx = rpamd.load(shape_knobs=True)
     buf = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")
     ecx.fill_random(buf, buf.numel(), 7)
     present = [False, False] + [True] * 14

@@ -1,11 +1,15 @@
 """pytest configuration: the `gpu` marker, repository import paths, and the
 package loader for the hyphenated package directory `repair-pipelining_amd/`."""
+import os
 import sys
 from pathlib import Path
 
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
+# The tests force launch shapes (every shape must give the same bytes), so this process opts in
+# to libecx's shape knobs (include/ecx_tune.h); test_abi checks a process without the opt-in.
+os.environ["ECX_SHAPE_KNOBS"] = "1"
 for p in (ROOT, ROOT / "oracle"):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
@@ -40,7 +44,7 @@ def kats():
 def ecx():
     """The product package (repair-pipelining_amd/), loaded via rpamd."""
     import rpamd
-    return rpamd.load()
+    return rpamd.load(shape_knobs=True)
 
 
 def shortened_clay_oracle(k, m, v, erased_real, inputs_real, B):

@@ -270,3 +270,39 @@ def test_is_parity_correct_batch_argument_checks(ecx):
     assert lib.ecx_rs_is_parity_correct_batch(rs._h, None, 20 * 64, 64, 0, 0, 64, None, None) == 0
     if not _has_device(ecx):
         assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, 1, 0, 64, 16, None) == -10
+
+
+def test_shape_knobs_need_the_opt_in():
+    """Round-4 verdict item 7: in a process without ECX_SHAPE_KNOBS=1 the product library
+    accepts only the deployment keys (layout_select, plan_cache, roctx, host_*) and refuses
+    every launch-shape key; with the opt-in it accepts them (a fresh process each way: the
+    library reads the variable once)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, ctypes
+sys.path.insert(0, %r)
+import rpamd
+lib = rpamd.load().lib()
+f = lib.ecx_tune
+f.argtypes, f.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+out = {}
+for k, v in [("layout_select", 1), ("plan_cache", 256), ("roctx", 0), ("host_chunk_kib", 65536),
+             ("host_buffers", 3), ("host_gather_kib", 512), ("host_zero_copy", 1), ("host_contexts", 1),
+             ("depth", 0), ("nontemporal", 1), ("xcd_group", 0), ("stagger", 0), ("block_threads", 0),
+             ("skew_chunks", 1), ("wide_tiles", 1), ("lds_tables", 1), ("store_scope", 0), ("rtc_nt", 5),
+             ("clay_rtc", 1), ("map_planes", 1), ("small_tiles", 2), ("chunk_major", 0)]:
+    out[k] = f(k.encode(), v)
+print(out)
+''' % str(ROOT)
+    env = {k: v for k, v in os.environ.items() if k != "ECX_SHAPE_KNOBS"}
+    deploy = {"layout_select", "plan_cache", "roctx", "host_chunk_kib", "host_buffers", "host_gather_kib",
+              "host_zero_copy", "host_contexts"}
+    for opt_in in (False, True):
+        e = dict(env, ECX_SHAPE_KNOBS="1") if opt_in else env
+        r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got = eval(r.stdout.strip().splitlines()[-1])
+        for k, st in got.items():
+            assert st == (0 if (k in deploy or opt_in) else -1), (opt_in, k, st)
