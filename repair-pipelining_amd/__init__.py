@@ -484,11 +484,11 @@ class GfMap:
         on a worker thread of its own; synchronous."""
         self._check(inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
                     byte_count)
-        devs = np.ascontiguousarray(list(devices), np.int32)
+        devs = list(devices)
+        arr = np.ascontiguousarray(devs + [0], np.int32)  # never a null list: an empty one is ndev 0
         check(lib().ecx_map_apply_batch_host_devices(self._h, _host_ptr(inp), in_stripe_stride, in_slot_stride,
                                                      _host_ptr(out), out_stripe_stride, out_slot_stride, nstripes,
-                                                     byte_count, devs.ctypes.data if len(devs) else None,
-                                                     len(devs)))
+                                                     byte_count, arr.ctypes.data, len(devs)))
 
 
 # ---------------------------------------------------------------- ReedSolomon.java
@@ -773,11 +773,12 @@ class ClayCodeErasureDecodingStep:
         thread and pipe per device entry."""
         self._check_batch(inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
                           bufSize)
-        devs = np.ascontiguousarray(list(devices), np.int32)
+        devs = list(devices)
+        arr = np.ascontiguousarray(devs + [0], np.int32)  # never a null list: an empty one is ndev 0
         check(lib().ecx_clay_perform_coding_batch_host_devices(self._h, _host_ptr(inp), in_stripe_stride,
                                                                in_sub_stride, _host_ptr(out), out_stripe_stride,
-                                                               out_sub_stride, nstripes, bufSize,
-                                                               devs.ctypes.data if len(devs) else None, len(devs)))
+                                                               out_sub_stride, nstripes, bufSize, arr.ctypes.data,
+                                                               len(devs)))
 
 
 class JavaRandom:

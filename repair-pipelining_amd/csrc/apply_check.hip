@@ -94,7 +94,8 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     if (nbytes <= 0 || cm.map().n_out == 0) return;
     // Ring depth: the map's own (20 for a single tile of 17-20 entries, 8 or 4 otherwise);
     // accumulator rows: 4 when every tile has at most 4 (RS with m <= 4), else 8.
-    int depth = cm.preferred_depth();
+    const Tuning &tu = tuning();
+    int depth = tu.depth == 4 || tu.depth == 8 || tu.depth == 20 ? tu.depth : cm.preferred_depth();
     if (depth != 4 && depth != 8 && depth != 20) depth = depth > 8 ? 20 : 4;
     const int rows = cm.max_tile_rows() <= 4 ? 4 : kTileRows;
     const bool aligned = aligned16(in) && in_stripe_stride % 16 == 0 && in_slot_stride % 16 == 0;
@@ -115,12 +116,12 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.out_slot_stride = 0;
     a.nbytes = nbytes;
     a.n_tiles = cm.n_tiles();
-    a.stagger = 0;
+    a.stagger = tu.stagger;
     // inputs not 128-B aligned share a boundary line between neighbouring chunks: runs of
     // consecutive units per XCD keep both fetches in one L2 (as launch_apply_core does)
     const bool misaligned128 = ((uintptr_t)in % 128) != 0 || in_stripe_stride % 128 != 0 || in_slot_stride % 128 != 0;
-    a.xcd_group = misaligned128 ? 3 : 0;
-    a.xcd_run = tuning().xcd_run;
+    a.xcd_group = tu.xcd_group == 3 ? 3 : (tu.xcd_misaligned && misaligned128 ? 3 : 0);
+    a.xcd_run = tu.xcd_run;
     a.tail_chunk = fuse_tail ? full : -1;
     auto run = [&](bool safe, const DevicePlan &p, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;
