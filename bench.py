@@ -283,7 +283,7 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
 # for its kernel family is stale.
 COMMON_SOURCES = ["engine.hpp", "engine.cpp", "codes.cpp", "codes.hpp"]
 COMPOSED_SOURCES = ["kernels.hip", "apply.hpp", "apply_launch.inc", "apply_t256.hip", "apply_t64.hip",
-                    "apply_skew.hip", "apply_bits.hip", "apply_lut.hip", "bits.hpp"]
+                    "apply_skew.hip", "apply_bits.hip", "apply_lut.hip", "bits.hpp", "apply_check.hip"]
 RTC_SOURCES = ["clay_rtc.hpp", "clay_rtc.cpp"]
 # k_map_planes: its generator, the shared prelude (clay_rtc.cpp) and launch_apply's choice (kernels.hip)
 PLANES_SOURCES = RTC_SOURCES + ["map_rtc.hpp", "map_rtc.cpp", "kernels.hip"]
@@ -305,11 +305,13 @@ def kernel_source_hash(kernel: str = "") -> str:
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(workload: str, pool: int, kernel: str):
+def pmc_traffic(workload: str, pool: int, kernel: str, shape: str = None):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (scripts/pmc.sh + scripts/pmc_summary.py), used only if it was taken on this
-    workload, pool size and kernel instance AND on the current kernel sources.
-    Returns (bytes or None, why-not)."""
+    workload, pool size and FULL launch shape (kernel instance plus the unit order its name
+    does not encode, ecx_last_launch_shape) AND on the current kernel sources.  A workload's
+    entry keeps one profile per shape profiled (by_shape: every candidate of the per-layout
+    selection, scripts/pmc.sh --candidates).  Returns (bytes or None, why-not)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None, "no PMC profile"
@@ -318,6 +320,10 @@ def pmc_traffic(workload: str, pool: int, kernel: str):
         w = d.get("workloads", {}).get(workload)
         if w is None:
             return None, "no PMC profile for this workload"
+        if shape is not None and shape in w.get("by_shape", {}):
+            w = w["by_shape"][shape]
+        elif shape is not None and w.get("launch_shape") not in (None, shape):
+            return None, "no PMC profile for this launch shape (%s)" % shape
         if w.get("kernel_source_hash") != kernel_source_hash(kernel):
             return None, "stale: PMC profile taken on other kernel sources"
         if w.get("pool_stripes") != pool or w.get("kernel") != kernel:
@@ -1103,7 +1109,9 @@ def main():
         torch.cuda.synchronize()
         kernel = ecx.last_kernel()
         choice, med = gm.layout_choice(pitch, with_times=True)
-        launch_shape = {"layout_select": choice, "candidate_median_ms": med, "kernel": kernel}
+        state, dropped = gm.layout_state(pitch)
+        launch_shape = {"layout_select": choice, "candidate_median_ms": med, "kernel": kernel,
+                        "state": state, "probes_dropped": dropped}
         if not args.no_verify and not wl.verify():
             raise SystemExit("output differs from the erased originals after the layout selection")
 
@@ -1113,6 +1121,7 @@ def main():
     torch.cuda.synchronize()
     if args.warmup:
         kernel = ecx.last_kernel()  # after the layout selection: the instance the timed region runs
+    shape = ecx.last_launch_shape()  # the kernel instance plus the unit order (stagger, XCD runs)
 
     stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -1144,7 +1153,7 @@ def main():
     total_stripes = stripes_per_step * args.steps * world
     metric_bytes = wl.metric_bytes or wl.unit_bytes
     value = total_stripes * metric_bytes / el / wl.metric_scale
-    traffic, traffic_note = pmc_traffic(args.workload, P, kernel)
+    traffic, traffic_note = pmc_traffic(args.workload, P, kernel, shape)
 
     # per-rank rates, so an N-GPU efficiency shortfall can be attributed to a rank
     per_rank = [own_el]
@@ -1188,7 +1197,8 @@ def main():
 
     if rank == 0 and args.meta:
         Path(args.meta).write_text(json.dumps({
-            "workload": args.workload, "kernel": kernel, "pool_stripes": P, "unit_bytes": wl.unit_bytes,
+            "workload": args.workload, "kernel": kernel, "launch_shape": shape, "tune": args.tune,
+            "pool_stripes": P, "unit_bytes": wl.unit_bytes,
             "write_bytes_per_unit": wl.write_bytes, "algorithmic_bytes_per_launch": per_launch_bytes,
             "kernel_source_hash": kernel_source_hash(kernel), "avg_launch_ms": launch_ms}) + "\n")
     if rank == 0:
@@ -1224,7 +1234,7 @@ def main():
                 "avg_launch_ms": round(launch_ms, 4),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "measured_ceilings": probes,
-                "launch_shape": launch_shape,
+                "launch_shape": dict(launch_shape or {}, name=shape),
                 "frac_of_mix_model": round(achieved / probes["mix_model_GBps"], 4) if probes else None,
             },
             "repaired_output_GiBps": round(total_stripes * wl.write_bytes / el / 2**30, 3),

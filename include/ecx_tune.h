@@ -177,18 +177,26 @@ int ecx_map_selftest(const struct ecx_map *map, uint64_t seed);
  * kernel), tile groups, and the summed group unions (= input loads of the LDS kernel). */
 int ecx_map_plan_stats(const struct ecx_map *map, int *n_tiles, int *n_entries, int *n_groups, int *union_total);
 /* The launch shape "layout_select" kept for the most recently selected batch layout of
- * `map` with input slot pitch `slot_pitch`: -1 = none chosen yet (still exploring, or not
- * eligible); else the static rules' shape (-1 is never returned for that: see below) is
- * reported as 0x100, and any other as shape + 8 * stagger, shape 0 = 256-thread workgroups
- * over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups over 1 KiB chunks.  With
- * median_ms (n entries), the median launch time of each candidate in the selector's order
- * (-1 = unsampled). */
+ * `map` with input slot pitch `slot_pitch`: 0x200 = none chosen yet (still exploring, or not
+ * eligible); the static rules' shape = 0x100; any other = shape + 8 * stagger, shape 0 =
+ * 256-thread workgroups over 4 KiB chunks, 1 = skewed chunks, 2 = one-wave workgroups over
+ * 1 KiB chunks.  With median_ms (n entries), the median launch time of each candidate in the
+ * selector's order (-1 = unsampled).  Negative: a status (null map, pitch <= 0, n < 0). */
 int ecx_map_layout_choice(const struct ecx_map *map, int64_t slot_pitch, float *median_ms, int n);
+/* State of that layout's selection: -1 none yet, 0 exploring, 1 chosen, 2 re-validating, 3
+ * re-validated (final), 4 contended (probes kept overlapping other streams' launches: the static
+ * rules, untimed); `dropped` = timing probes discarded because another stream of the device
+ * launched while they were in flight.  Either pointer may be NULL. */
+int ecx_map_layout_state(const struct ecx_map *map, int64_t slot_pitch, int *state, int *dropped);
 /* The kernel instance of the last full-chunk launch this thread enqueued, named as
  * rocprofv3 names it (e.g. "k_gf_apply<false, true, 1, 20, false, 256, 8>"), copied
  * NUL-terminated into buf.  Returns its length (0 = no launch yet), or
  * ECX_E_ILLEGAL_ARGUMENT if buf is null or shorter than length + 1. */
 int ecx_last_kernel(char *buf, int len);
+/* The same launch's full shape: the kernel instance followed by the unit order its name does not
+ * encode -- "k_gf_apply<...> stagger=G xcd_group=X xcd_run=R [skew=K]" for the composed-map
+ * kernels, the bare name for the generated Clay kernels.  Same buffer contract. */
+int ecx_last_launch_shape(char *buf, int len);
 /* The per-helper-plane Clay repair kernel (ecx_tune "clay_rtc"): builds the clay
  * step's repair program (checked against the composed reference map), generates the
  * kernel source and compiles it with hiprtc for gfx950 -- no device needed.  Returns

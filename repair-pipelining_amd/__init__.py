@@ -228,6 +228,15 @@ def last_kernel() -> str:
     return buf.value.decode() if check(f(buf, len(buf))) > 0 else ""
 
 
+def last_launch_shape() -> str:
+    """That launch's full shape: kernel instance plus the unit order its name does not encode
+    ("... stagger=G xcd_group=X xcd_run=R"; ecx_last_launch_shape)."""
+    f = lib().ecx_last_launch_shape
+    f.argtypes, f.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
+    buf = ctypes.create_string_buffer(512)
+    return buf.value.decode() if check(f(buf, len(buf))) > 0 else ""
+
+
 def probe_bandwidth(kind: int, src, dst, nbytes: int, nontemporal: bool = True, stream=None) -> None:
     """Pure-bandwidth probe kernels (include/ecx_tune.h): kind 0 = read-only stream of
     `src`, kind 1 = copy src -> dst; nbytes a multiple of 16 KiB.  Diagnostics only."""
@@ -451,10 +460,20 @@ class GfMap:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
         f.restype = ctypes.c_int
         ms = (ctypes.c_float * 8)()
-        c = f(self._h, int(slot_pitch), ms if with_times else None, 8 if with_times else 0)
-        if c < -1:
-            check(c)
+        c = check(f(self._h, int(slot_pitch), ms if with_times else None, 8 if with_times else 0))
+        if c == 0x200:
+            c = -1  # none chosen yet
         return (c, [round(float(x), 4) for x in ms]) if with_times else c
+
+    def layout_state(self, slot_pitch: int):
+        """(state, dropped probes) of that layout's selection (ecx_map_layout_state): state -1
+        none yet, 0 exploring, 1 chosen, 2 re-validating, 3 re-validated, 4 contended."""
+        f = lib().ecx_map_layout_state
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        f.restype = ctypes.c_int
+        st, dr = ctypes.c_int(), ctypes.c_int()
+        check(f(self._h, int(slot_pitch), ctypes.byref(st), ctypes.byref(dr)))
+        return st.value, dr.value
 
     def _check(self, inp, iss, isl, out, oss, osl, nstripes, nbytes):
         mi, mo = self.max_slots()

@@ -92,11 +92,12 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     if (nstripes <= 0) return;
     check_hip(hipMemsetAsync(verdict, 1, (size_t)nstripes, stream), "hipMemsetAsync (verdicts)");
     if (nbytes <= 0 || cm.map().n_out == 0) return;
-    // Ring depth: the map's own (20 for a single tile of 17-20 entries, 8 or 4 otherwise);
-    // accumulator rows: 4 when every tile has at most 4 (RS with m <= 4), else 8.
+    // Ring depth 4 (forced 8 / 20 with ecx_tune "depth"): on RS(17,3) 200,000-B shards depth 4 reads
+    // 0.83 of HBM, depth 8 and 20 0.80 -- the short ring leaves registers for more resident waves
+    // (profiles/r05_check_sweep.jsonl).  Accumulator rows: 4 when every tile has at most 4 (RS with
+    // m <= 4), else 8.
     const Tuning &tu = tuning();
-    int depth = tu.depth == 4 || tu.depth == 8 || tu.depth == 20 ? tu.depth : cm.preferred_depth();
-    if (depth != 4 && depth != 8 && depth != 20) depth = depth > 8 ? 20 : 4;
+    const int depth = tu.depth == 8 || tu.depth == 20 ? tu.depth : 4;
     const int rows = cm.max_tile_rows() <= 4 ? 4 : kTileRows;
     const bool aligned = aligned16(in) && in_stripe_stride % 16 == 0 && in_slot_stride % 16 == 0;
     const int64_t full = aligned ? nbytes / kChunkBytes : 0;
@@ -148,6 +149,7 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
             }
         }
     };
+    const uint64_t notes0 = kernel_notes();
     if (fuse_tail) {
         run(false, plan, 0, full + 1);
     } else {
@@ -155,7 +157,13 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         a.tail_chunk = -1;
         run(true, plan4, full, (tail + kChunkBytes - 1) / kChunkBytes);  // (not noted: byte-safe)
     }
+    if (kernel_notes() != notes0)
+        set_last_shape_order("stagger=" + std::to_string(a.stagger) + " xcd_group=" + std::to_string(a.xcd_group) +
+                             " xcd_run=" + std::to_string(a.xcd_group == 3 ? a.xcd_run : 0));
     check_hip(hipGetLastError(), "k_gf_check launch");
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    note_device_launch(dev, stream);
 }
 
 }  // namespace ecx

@@ -953,6 +953,9 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
                     r->launch(sh, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
                               nstripes, done / kChunkBytes, (hipStream_t)stream);
                     rtc_kernel = r->kernel_name(sh);
+                    int dev = 0;
+                    check_hip(hipGetDevice(&dev), "hipGetDevice");
+                    note_device_launch(dev, (hipStream_t)stream);
                 }
             }
         }
@@ -1368,14 +1371,36 @@ int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_
 int ecx_build_diag(void) { return ECX_DIAG ? 1 : 0; }
 
 int ecx_map_layout_choice(const ecx_map *map, int64_t slot_pitch, float *median_ms, int n) {
-    if (!map || slot_pitch <= 0 || n < 0) return ECX_E_ILLEGAL_ARGUMENT;
-    std::vector<float> ms;
-    const int c = const_cast<ecx_map *>(map)->cm.layout_choice(slot_pitch, median_ms ? &ms : nullptr);
-    if (median_ms)
-        for (int i = 0; i < n; ++i) median_ms[i] = i < (int)ms.size() ? ms[i] : -1.f;
-    if (c < 0) return -1;
-    const int code = layout_candidate_code(c);
-    return code == -1 ? 0x100 : code;  // 0x100 = the static rules' shape
+    return guarded(__func__, [&]() -> int {
+        if (!map) throw Error(ECX_E_NULL, "null map");
+        if (slot_pitch <= 0 || n < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "slot pitch or count");
+        std::vector<float> ms;
+        const int c = const_cast<ecx_map *>(map)->cm.layout_choice(slot_pitch, median_ms ? &ms : nullptr);
+        if (median_ms)
+            for (int i = 0; i < n; ++i) median_ms[i] = i < (int)ms.size() ? ms[i] : -1.f;
+        if (c < 0) return 0x200;  // none chosen yet (or the layout is not selected per launch)
+        const int code = layout_candidate_code(c);
+        return code == -1 ? 0x100 : code;  // 0x100 = the static rules' shape
+    });
+}
+
+int ecx_map_layout_state(const ecx_map *map, int64_t slot_pitch, int *state, int *dropped) {
+    return guarded(__func__, [&]() -> int {
+        if (!map) throw Error(ECX_E_NULL, "null map");
+        if (slot_pitch <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "slot pitch");
+        int st = -1, dr = 0;
+        const int c = const_cast<ecx_map *>(map)->cm.layout_choice(slot_pitch, nullptr, &st, &dr);
+        if (state) *state = c < 0 ? -1 : st;
+        if (dropped) *dropped = c < 0 ? 0 : dr;
+        return ECX_OK;
+    });
+}
+
+int ecx_last_launch_shape(char *buf, int len) {
+    const std::string k = last_launch_shape();
+    if (!buf || len < (int)k.size() + 1) return ECX_E_ILLEGAL_ARGUMENT;
+    std::memcpy(buf, k.c_str(), k.size() + 1);
+    return (int)k.size();
 }
 
 int ecx_last_kernel(char *buf, int len) {

@@ -27,8 +27,21 @@ void update_tuning(const std::function<void(Tuning &)> &f) {
 }
 
 static thread_local std::string g_last_kernel;
-void set_last_kernel(std::string name) { g_last_kernel = std::move(name); }
+namespace {
+thread_local std::string g_last_shape_order;  // the unit order of the last noted launch
+thread_local uint64_t g_kernel_notes = 0;
+}  // namespace
+void set_last_kernel(std::string name) {
+    g_last_kernel = std::move(name);
+    g_last_shape_order.clear();
+    ++g_kernel_notes;
+}
 const std::string &last_kernel() { return g_last_kernel; }
+uint64_t kernel_notes() { return g_kernel_notes; }
+void set_last_shape_order(std::string order) { g_last_shape_order = std::move(order); }
+std::string last_launch_shape() {
+    return g_last_shape_order.empty() ? g_last_kernel : g_last_kernel + " " + g_last_shape_order;
+}
 
 void check_hip(hipError_t e, const char *what) {
     if (e != hipSuccess) throw Error(ECX_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
@@ -403,8 +416,8 @@ const uint8_t *zero_page_for_current_device() {
 CompiledMap::~CompiledMap() {
     for (auto &kv : layout_sel_)
         for (auto &p : kv.second.pending) {
-            (void)hipEventDestroy(p.e0);
-            (void)hipEventDestroy(p.e1);
+            if (p.e0) (void)hipEventDestroy(p.e0);
+            if (p.e1) (void)hipEventDestroy(p.e1);
         }
     for (auto &kv : dev_) {
         int cur = 0;
@@ -666,37 +679,124 @@ MapPlanes *CompiledMap::planes() {
 }
 
 namespace {
-constexpr float kLayoutMargin = 0.98f;  // another shape replaces the static rules' only if 2 % faster
-constexpr size_t kMaxLayouts = 64;      // layouts selected per map; past that, new ones use the static rules
+constexpr float kLayoutMargin = 0.98f;   // another shape replaces the static rules' only if 2 % faster
+constexpr size_t kMaxLayouts = 64;       // layouts selected per map; past that, new ones use the static rules
+constexpr int kLayoutMaxDropped = 64;    // contaminated probes before a layout is declared contended
+constexpr int64_t kLayoutRevalidate = 512;  // launches after a choice before its one re-validation
 
 float median_of(std::vector<float> v) {
     std::sort(v.begin(), v.end());
     return v.empty() ? -1.f : v[v.size() / 2];
 }
+
+struct DevLaunches {
+    uint64_t serial = 0;
+    std::map<hipStream_t, uint64_t> last;  // stream -> serial of its latest launch
+};
+std::mutex g_launch_mu;
+std::map<int, DevLaunches> g_launches;
 }  // namespace
 
-int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, bool *time) {
-    std::lock_guard<std::mutex> lk(mu_);
-    *time = false;
-    if (!layout_sel_.count(key) && layout_sel_.size() >= kMaxLayouts) return 0;  // bounded: the static rules
-    LayoutSel &s = layout_sel_[key];
-    if ((int)s.ms.size() != n_cand) s.ms.assign(n_cand, {});
-    if (s.chosen >= 0) return s.chosen;
+uint64_t note_device_launch(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    DevLaunches &d = g_launches[dev];
+    d.last[s] = ++d.serial;
+    return d.serial;
+}
+
+uint64_t stream_last_launch(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    auto it = g_launches.find(dev);
+    if (it == g_launches.end()) return 0;
+    auto jt = it->second.last.find(s);
+    return jt == it->second.last.end() ? 0 : jt->second;
+}
+
+bool other_stream_launched_since(int dev, hipStream_t s, uint64_t since) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    auto it = g_launches.find(dev);
+    if (it == g_launches.end()) return false;
+    for (const auto &kv : it->second.last)
+        if (kv.first != s && kv.second > since) return true;
+    return false;
+}
+
+// Reads the finished probes of `s` (non-blocking): clean timings go to the exploration's
+// per-candidate lists, or to the re-validation's pair; contaminated ones are counted and dropped.
+void CompiledMap::harvest(LayoutSel &s, int n_cand) {
     for (auto it = s.pending.begin(); it != s.pending.end();) {
+        if (!it->e1) {  // reserved, not yet launched
+            ++it;
+            continue;
+        }
         const hipError_t q = hipEventQuery(it->e1);
         if (q == hipErrorNotReady) {
             ++it;
             continue;
         }
         float ms = 0.f;
-        if (q == hipSuccess && hipEventElapsedTime(&ms, it->e0, it->e1) == hipSuccess && ms > 0.f)
+        const bool timed = q == hipSuccess && hipEventElapsedTime(&ms, it->e0, it->e1) == hipSuccess && ms > 0.f;
+        if (!timed) (void)hipGetLastError();  // a failed probe is dropped; its candidate is timed again
+        else if (other_stream_launched_since(it->dev, it->stream, it->since)) ++s.dropped;
+        else if (s.state == kLayoutRevalidating) {
+            if (it->cand == s.reval_alt) s.reval_ms[0].push_back(ms);
+            else if (it->cand == s.chosen) s.reval_ms[1].push_back(ms);
+        } else if (s.state == kLayoutExploring && it->cand < n_cand) {
             s.ms[it->cand].push_back(ms);
-        else
-            (void)hipGetLastError();  // a failed probe is dropped; its candidate is timed again
+        }
         (void)hipEventDestroy(it->e0);
         (void)hipEventDestroy(it->e1);
         it = s.pending.erase(it);
     }
+}
+
+int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, int dev,
+                                  hipStream_t stream, uint64_t *ticket) {
+    std::lock_guard<std::mutex> lk(mu_);
+    *ticket = 0;
+    if (!layout_sel_.count(key) && layout_sel_.size() >= kMaxLayouts) return 0;  // bounded: the static rules
+    LayoutSel &s = layout_sel_[key];
+    if ((int)s.ms.size() != n_cand) s.ms.assign(n_cand, {});
+    harvest(s, n_cand);  // also after the choice, so late probes free their events
+    auto reserve = [&](int cand) {
+        *ticket = ++ticket_serial_;
+        s.pending.push_back({cand, nullptr, nullptr, *ticket, dev, stream, stream_last_launch(dev, stream)});
+        return cand;
+    };
+    auto in_flight = [&](int cand) {
+        int n = 0;
+        for (const auto &p : s.pending) n += p.cand == cand;
+        return n;
+    };
+    if (s.state == kLayoutContended || s.state == kLayoutRevalidated) return s.chosen;
+    if (s.state == kLayoutChosen) {
+        if (s.chosen == s.reval_alt || ++s.steady < kLayoutRevalidate) return s.chosen;
+        s.state = kLayoutRevalidating;  // once: the kept shape against its alternative, clean timings
+    }
+    if (s.dropped >= kLayoutMaxDropped) {
+        // another stream keeps the device busy while probes run: no timing here is trustworthy
+        s.chosen = 0;
+        s.state = kLayoutContended;
+        s.serial = ++layout_serial_;
+        return 0;
+    }
+    if (s.state == kLayoutRevalidating) {
+        const int have[2] = {(int)s.reval_ms[0].size() + in_flight(s.reval_alt),
+                             (int)s.reval_ms[1].size() + in_flight(s.chosen)};
+        if ((int)s.reval_ms[0].size() >= samples && (int)s.reval_ms[1].size() >= samples) {
+            const float alt = median_of(s.reval_ms[0]), kept = median_of(s.reval_ms[1]);
+            // a shape other than the static rules (candidate 0) must keep beating them by the margin;
+            // a kept static choice is replaced only by a runner-up that beats it by the margin
+            const bool keep = s.reval_alt == 0 ? kept < kLayoutMargin * alt : !(alt < kLayoutMargin * kept);
+            if (!keep) s.chosen = s.reval_alt;
+            s.state = kLayoutRevalidated;
+            s.serial = ++layout_serial_;
+            return s.chosen;
+        }
+        if (have[0] >= samples && have[1] >= samples) return s.chosen;  // all in flight: untimed
+        return reserve(have[0] <= have[1] ? s.reval_alt : s.chosen);
+    }
+    // exploring
     std::vector<int> queued(n_cand, 0);
     bool done = true;
     for (int c = 0; c < n_cand; ++c) {
@@ -705,7 +805,7 @@ int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand,
     }
     if (done) {
         const float base = median_of(s.ms[0]);
-        int best = 0;
+        int best = 0, second = -1;
         float best_ms = base;
         for (int c = 1; c < n_cand; ++c) {
             const float m = median_of(s.ms[c]);
@@ -714,7 +814,12 @@ int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand,
                 best_ms = m;
             }
         }
+        for (int c = 0; c < n_cand; ++c)  // the runner-up: what a kept static choice is re-checked against
+            if (c != best && (second < 0 || median_of(s.ms[c]) < median_of(s.ms[second]))) second = c;
         s.chosen = best;
+        s.reval_alt = best != 0 ? 0 : (second >= 0 ? second : 0);
+        s.state = kLayoutChosen;
+        s.steady = 0;
         s.serial = ++layout_serial_;
         return best;
     }
@@ -723,16 +828,33 @@ int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand,
     for (int k = 1; k < n_cand; ++k)
         if (queued[k] < queued[c]) c = k;
     if (queued[c] >= samples) return 0;  // every probe is in flight: the static rules, untimed
-    *time = true;
-    return c;
+    return reserve(c);
 }
 
-void CompiledMap::add_layout_probe(const std::array<int64_t, 8> &key, int cand, hipEvent_t e0, hipEvent_t e1) {
+void CompiledMap::fill_layout_probe(const std::array<int64_t, 8> &key, uint64_t ticket, hipEvent_t e0,
+                                    hipEvent_t e1) {
     std::lock_guard<std::mutex> lk(mu_);
-    layout_sel_[key].pending.push_back({cand, e0, e1});
+    for (auto &p : layout_sel_[key].pending)
+        if (p.ticket == ticket) {
+            p.e0 = e0;
+            p.e1 = e1;
+            return;
+        }
+    (void)hipEventDestroy(e0);  // not reserved (cannot happen): drop the events
+    (void)hipEventDestroy(e1);
 }
 
-int CompiledMap::layout_choice(int64_t pitch, std::vector<float> *ms) {
+void CompiledMap::cancel_layout_probe(const std::array<int64_t, 8> &key, uint64_t ticket) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto &v = layout_sel_[key].pending;
+    for (auto it = v.begin(); it != v.end(); ++it)
+        if (it->ticket == ticket) {
+            v.erase(it);
+            return;
+        }
+}
+
+int CompiledMap::layout_choice(int64_t pitch, std::vector<float> *ms, int *state, int *dropped) {
     std::lock_guard<std::mutex> lk(mu_);
     const LayoutSel *latest = nullptr;
     for (const auto &kv : layout_sel_)
@@ -743,6 +865,8 @@ int CompiledMap::layout_choice(int64_t pitch, std::vector<float> *ms) {
         ms->clear();
         for (const auto &v : latest->ms) ms->push_back(median_of(v));
     }
+    if (state) *state = latest->state;
+    if (dropped) *dropped = latest->dropped;
     return latest->chosen;
 }
 

@@ -152,33 +152,57 @@ public:
     const std::vector<int> &used_in_slots();
     const std::vector<int> &used_out_slots();
     // Per-layout launch-shape selection (kernels.hip launch_apply, ecx_tune "layout_select"):
-    // the candidate to run for this call of the batch layout `key`.  Finished timing probes
-    // are harvested first (non-blocking); once every one of the n_cand candidates has
-    // `samples` timings the fastest median is kept (candidate 0 -- the static rules --
-    // unless another is faster by kLayoutMargin).  At most kMaxLayouts layouts are selected per
-    // map (later ones get candidate 0, untimed).  While exploring, the least-sampled
-    // candidate is returned with *time set: the caller brackets that launch with two
-    // events on its stream and hands them to add_layout_probe.
-    int next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, bool *time);
-    void add_layout_probe(const std::array<int64_t, 8> &key, int cand, hipEvent_t e0, hipEvent_t e1);
+    // the candidate to run for this call of the batch layout `key` on `stream` of device `dev`.
+    // Finished timing probes are harvested first (non-blocking).  A probe is DROPPED, not
+    // counted, when another stream of the same device enqueued a libecx launch between this
+    // stream's previous launch and the harvest (note_device_launch): its kernel may have shared
+    // the GPU with the probe.  Once every one of the n_cand candidates has `samples` clean
+    // timings the fastest median is kept (candidate 0 -- the static rules -- unless another is
+    // faster by kLayoutMargin); after kLayoutMaxDropped dropped probes the layout is CONTENDED
+    // and keeps candidate 0 untimed.  A kept shape other than the static rules is re-validated
+    // once, after kLayoutRevalidate further launches: `samples` clean timings each of it and
+    // of the static rules, and the static rules return unless the kept shape still wins by the
+    // margin.  At most kMaxLayouts layouts are selected per map (later ones get candidate 0,
+    // untimed).  When the call is to be timed, *ticket is set to a non-zero probe slot
+    // reserved in the layout's pending list (so concurrent callers are never handed the same
+    // probe twice): the caller brackets its launch with two events on `stream` and hands them
+    // to fill_layout_probe, or gives the slot back with cancel_layout_probe.
+    int next_layout_pick(const std::array<int64_t, 8> &key, int n_cand, int samples, int dev, hipStream_t stream,
+                         uint64_t *ticket);
+    void fill_layout_probe(const std::array<int64_t, 8> &key, uint64_t ticket, hipEvent_t e0, hipEvent_t e1);
+    void cancel_layout_probe(const std::array<int64_t, 8> &key, uint64_t ticket);
     // The candidate kept for the most recently selected layout with input slot pitch
     // `pitch`, -1 if none yet; with `ms`, the per-candidate median launch times (ms, -1 =
-    // unsampled) of that layout.
-    int layout_choice(int64_t pitch, std::vector<float> *ms = nullptr);
+    // unsampled) of that layout; with `state` its state (LayoutState) and with `dropped` the
+    // probes it dropped as contaminated.
+    int layout_choice(int64_t pitch, std::vector<float> *ms = nullptr, int *state = nullptr, int *dropped = nullptr);
+    enum LayoutState { kLayoutExploring = 0, kLayoutChosen = 1, kLayoutRevalidating = 2, kLayoutRevalidated = 3,
+                       kLayoutContended = 4 };
 
 private:
     struct LayoutSel {
         struct Probe {
             int cand;
-            hipEvent_t e0, e1;
+            hipEvent_t e0, e1;   // null until fill_layout_probe
+            uint64_t ticket;
+            int dev;
+            hipStream_t stream;
+            uint64_t since;      // the stream's last launch serial before this probe (note_device_launch)
         };
-        std::vector<std::vector<float>> ms;  // per candidate: launch times of its probes
-        std::vector<Probe> pending;          // probes whose end event has not completed yet
+        std::vector<std::vector<float>> ms;  // per candidate: clean launch times of its probes
+        std::vector<Probe> pending;          // reserved or unfinished probes
         int chosen = -1;
+        int state = kLayoutExploring;
+        int dropped = 0;                     // probes discarded as contaminated
+        int64_t steady = 0;                  // launches since the choice (re-validation trigger)
+        int reval_alt = 0;                   // the shape the kept one is re-validated against
+        std::vector<float> reval_ms[2];      // re-validation timings: [0] the alternative, [1] the kept shape
         uint64_t serial = 0;                 // order of the choices (layout_choice reports the latest)
     };
+    void harvest(LayoutSel &s, int n_cand);
     std::map<std::array<int64_t, 8>, LayoutSel> layout_sel_;
     uint64_t layout_serial_ = 0;
+    uint64_t ticket_serial_ = 0;
     LinearMap map_;
     std::unique_ptr<CompiledMap> compact_;
     std::unique_ptr<MapPlanes> planes_;
@@ -334,6 +358,12 @@ void update_tuning(const std::function<void(Tuning &)> &f);
 // Diagnostics: bench.py's roofline.kernel and its PMC-profile match (ecx_last_kernel).
 void set_last_kernel(std::string name);
 const std::string &last_kernel();
+// The full launch shape of that launch: the kernel instance plus the unit order the kernel name
+// does not encode ("stagger=G xcd_group=X xcd_run=R"), set by the launcher after the kernel is
+// noted (ecx_last_launch_shape; bench.py's roofline.launch_shape and its PMC-profile key).
+uint64_t kernel_notes();  // set_last_kernel calls on this thread so far
+void set_last_shape_order(std::string order);
+std::string last_launch_shape();
 inline std::string kernel_param(bool v) { return v ? "true" : "false"; }
 inline std::string kernel_param(int v) { return std::to_string(v); }
 template <typename... P>
@@ -345,6 +375,15 @@ void note_kernel(const char *name, P... params) {
     s += '>';
     set_last_kernel(std::move(s));
 }
+
+// Per-device launch registry (engine.cpp), read by the layout selection's contamination check:
+// every batch launch of the library (launch_apply, launch_check, the generated Clay kernels)
+// records its stream here.  note_device_launch returns the launch's serial; stream_last_launch
+// the serial of a stream's latest launch (0 = none); other_stream_launched_since whether a
+// stream other than `s` on device `dev` launched after serial `since`.
+uint64_t note_device_launch(int dev, hipStream_t s);
+uint64_t stream_last_launch(int dev, hipStream_t s);
+bool other_stream_launched_since(int dev, hipStream_t s, uint64_t since);
 
 // Enqueue out = M * in over nstripes stripes (kernels.hip).
 // The launch_apply_core pick of per-layout candidate `cand` (kernels.hip kLayoutCand):

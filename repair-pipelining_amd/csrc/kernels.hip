@@ -512,6 +512,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
             else launch_shape_t<kBlockThreads>(s, grid, lds, stream, a);
         }
     };
+    const uint64_t notes0 = kernel_notes();
     int64_t first = 0;  // first full chunk left to the one-chunk kernels
     // a layout probe's start: after the host-side work (plan upload on first use), so the
     // probe times the kernels alone; a failed record only drops that probe
@@ -568,6 +569,10 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         run(false, first, full - first);
         run(true, full, tail_chunks);
     }
+    if (kernel_notes() != notes0 && !planes)  // a composed-map kernel of record was launched here
+        set_last_shape_order("stagger=" + std::to_string(a.stagger) + " xcd_group=" + std::to_string(a.xcd_group) +
+                             " xcd_run=" + std::to_string(a.xcd_group == 3 ? a.xcd_run : 0) +
+                             (skew ? " skew=" + std::to_string(skew) : std::string()));
     check_hip(hipGetLastError(), "k_gf_apply launch");
 }
 }  // namespace
@@ -614,48 +619,53 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         }
         select = cap == hipStreamCaptureStatusNone;
     }
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
     if (!select) {
         launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
                           nbytes, stream, accumulate, -1);
+        note_device_launch(dev, stream);
         return;
     }
-    int dev = 0;
-    check_hip(hipGetDevice(&dev), "hipGetDevice");
     // A layout is its strides, the size class of the shard (log2 of the byte count) and of the
     // batch (log2 of its input bytes), the mode and the device: callers whose batch sizes vary
     // from call to call share one selection instead of exploring anew at every size.
     auto log2i = [](int64_t v) { return (int64_t)(63 - __builtin_clzll((unsigned long long)std::max<int64_t>(v, 1))); };
     const std::array<int64_t, 8> key{in_slot_stride, in_stripe_stride, out_slot_stride, out_stripe_stride,
                                      log2i(nbytes), log2i(nstripes * in_bytes), (int64_t)accumulate, (int64_t)dev};
-    bool time = false;
-    const int cand = cm.next_layout_pick(key, kLayoutNCand, kLayoutSamples, &time);
+    uint64_t ticket = 0;
+    const int cand = cm.next_layout_pick(key, kLayoutNCand, kLayoutSamples, dev, stream, &ticket);
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (time) {
+    if (ticket) {
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
             (void)hipGetLastError();
             if (e0) (void)hipEventDestroy(e0);
             if (e1) (void)hipEventDestroy(e1);
             e0 = e1 = nullptr;
-            time = false;
+            cm.cancel_layout_probe(key, ticket);
+            ticket = 0;
         }
     }
     try {
         launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
-                          nbytes, stream, accumulate, kLayoutCand[cand], time ? e0 : nullptr);
+                          nbytes, stream, accumulate, kLayoutCand[cand], ticket ? e0 : nullptr);
     } catch (...) {
-        if (time) {
+        if (ticket) {
             (void)hipEventDestroy(e0);
             (void)hipEventDestroy(e1);
+            cm.cancel_layout_probe(key, ticket);
         }
         throw;
     }
-    if (time) {
+    note_device_launch(dev, stream);
+    if (ticket) {
         if (hipEventRecord(e1, stream) == hipSuccess) {
-            cm.add_layout_probe(key, cand, e0, e1);
+            cm.fill_layout_probe(key, ticket, e0, e1);
         } else {
             (void)hipGetLastError();
             (void)hipEventDestroy(e0);
             (void)hipEventDestroy(e1);
+            cm.cancel_layout_probe(key, ticket);
         }
     }
 }

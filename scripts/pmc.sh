@@ -14,21 +14,47 @@ OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-WORKLOADS="${*:-clay42 clay104 rs124 lrc clay42x2 rs173 lrcenc rs173check}"
+# --candidates: instead, every launch shape the per-layout selection can keep for the many-stream
+# RS / LRC-encode maps (kernels.hip kLayoutCand), each forced by its ecx_tune keys, FETCH and
+# WRITE passes only; pmc_summary.py files them under the workload's by_shape profiles, keyed by
+# the full launch shape (kernel instance + stagger + XCD runs) bench.py reports.
+CANDIDATES=0
+if [ "${1:-}" = "--candidates" ]; then CANDIDATES=1; shift; fi
+if [ $CANDIDATES = 1 ]; then
+  WORKLOADS="${*:-rs124 rs173 lrcenc}"
+else
+  WORKLOADS="${*:-clay42 clay104 rs124 lrc clay42x2 rs173 lrcenc rs173check}"
+fi
+# the selection's candidates (kLayoutCand order): static rules, 256-thread / 4 KiB, skewed chunks,
+# one wave / 1 KiB, one wave + stagger 2, one wave + stagger 8, 256-thread + stagger 4
+CAND_TUNES=("layout_select=0" "block_threads=256 skew_chunks=0" "block_threads=256 skew_chunks=4"
+            "block_threads=64 skew_chunks=0" "block_threads=64 skew_chunks=0 stagger=2"
+            "block_threads=64 skew_chunks=0 stagger=8" "block_threads=256 skew_chunks=0 stagger=4")
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
 for W in $WORKLOADS; do
   case $W in
     clay42|clay42x2) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; rs173|rs173check) POOL=4096 ;; lrcenc) POOL=32768 ;; lrc) POOL=32768 ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
-  i=0
-  for C in FETCH_SIZE WRITE_SIZE "$SQ"; do
-    D="$OUT/pmc_${W}_$i"; mkdir -p "$D"
-    timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
-        -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 --e2e-seconds 0 \
-           --stripes-per-step $((POOL * 16)) --no-probes --meta "$D/meta.json" > "$D.log" 2>&1
-    rc=$?; echo "pmc $W pass$i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D.log"; exit $rc; }
-    i=$((i + 1))
+  if [ $CANDIDATES = 1 ]; then NC=${#CAND_TUNES[@]}; else NC=1; fi
+  for ((c = 0; c < NC; c++)); do
+    TUNE=(); TAG=""
+    if [ $CANDIDATES = 1 ]; then
+      for kv in ${CAND_TUNES[$c]}; do TUNE+=(--tune "$kv"); done
+      TAG="_c$c"
+      PASSES=(FETCH_SIZE WRITE_SIZE)
+    else
+      PASSES=(FETCH_SIZE WRITE_SIZE "$SQ")
+    fi
+    i=0
+    for C in "${PASSES[@]}"; do
+      D="$OUT/pmc_${W}${TAG}_$i"; mkdir -p "$D"
+      timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
+          -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 --e2e-seconds 0 \
+             --stripes-per-step $((POOL * 16)) --no-probes --meta "$D/meta.json" "${TUNE[@]}" > "$D.log" 2>&1
+      rc=$?; echo "pmc $W$TAG pass$i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D.log"; exit $rc; }
+      i=$((i + 1))
+    done
   done
 done
 exit 0

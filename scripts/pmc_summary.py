@@ -42,7 +42,7 @@ def main(src=None, out_table="profiles/r02_pmc_workloads.json"):
     traffic = json.loads(old.read_text()).get("workloads", {}) if old.exists() else {}
     old_t = ROOT / out_table
     table = json.loads(old_t.read_text()).get("workloads", {}) if old_t.exists() else {}
-    for meta_f in sorted(glob.glob(str(src / "pmc_*_0" / "meta.json"))):
+    for meta_f in sorted(glob.glob(str(src / "pmc_*_0" / "meta.json")), key=lambda f: ("_c" in f, f)):
         d0 = Path(meta_f).parent
         w = json.loads(Path(meta_f).read_text())
         name, kernel = w["workload"], w["kernel"]
@@ -52,13 +52,25 @@ def main(src=None, out_table="profiles/r02_pmc_workloads.json"):
         rd, wr = 2 * fetch * 1024, write * 1024
         algo = w["algorithmic_bytes_per_launch"]
         algo_wr = w["pool_stripes"] * w["write_bytes_per_unit"]
-        traffic[name] = {
-            "kernel": kernel, "pool_stripes": w["pool_stripes"], "kernel_source_hash": w["kernel_source_hash"],
+        shape = w.get("launch_shape") or kernel
+        entry = {
+            "kernel": kernel, "launch_shape": shape, "tune": w.get("tune", []), "pool_stripes": w["pool_stripes"],
+            "kernel_source_hash": w["kernel_source_hash"],
             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
             "algorithmic_bytes_per_launch": algo, "traffic_over_algorithmic": (rd + wr) / algo,
-            "read_over_algorithmic_read": rd / (algo - algo_wr), "write_over_algorithmic_write": wr / algo_wr,
+            "read_over_algorithmic_read": rd / (algo - algo_wr),
+            "write_over_algorithmic_write": wr / algo_wr if algo_wr else None,
         }
-        t = dict(traffic[name])
+        # one profile per full launch shape (the selection's candidates); the workload's own
+        # fields are the shape its default (untuned) run launches
+        by_shape = dict(traffic.get(name, {}).get("by_shape", {}))
+        by_shape[shape] = entry
+        if not w.get("tune") or name not in traffic:
+            traffic[name] = dict(entry)
+        else:
+            traffic[name] = dict(traffic[name])
+        traffic[name]["by_shape"] = by_shape
+        t = dict(entry)
         sq_dir = Path(base + "_2")
         if sq_dir.exists():
             rows = rows_for(sq_dir, kernel)
@@ -74,7 +86,7 @@ def main(src=None, out_table="profiles/r02_pmc_workloads.json"):
             t["active_valu_over_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
             t["effective_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9  # GRBM sums the 8 XCDs
         t["bench_avg_launch_ms"] = w["avg_launch_ms"]
-        table[name] = t
+        table[name if not w.get("tune") else "%s [%s]" % (name, shape)] = t
     # workloads not re-profiled in this run keep their entries (and their own hashes)
     out = {"correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane streaming reads); "
                          "write = WRITE_SIZE x 1024",

@@ -2156,3 +2156,51 @@ def test_clay_rtc_nontemporal_policies_vs_oracle(ecx, torch_dev, e, B, S):
     inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
     ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
     assert all((outs[0][S - 1, z] == ref[z]).all() for z in range(a))
+
+
+def test_layout_selection_two_streams(ecx, torch_dev):
+    """Round-4 verdict item 3: two threads, each on its own stream, drive one batch layout of
+    one map at once (RS(12,4) encode in place, 1 MiB shards, 384 MiB per batch -- eligible for
+    the per-layout selection).  Every launch computes the same bytes whatever candidate it
+    runs, so both pools end with the oracle's parity; the selection still concludes (a kept
+    shape, or the static rules once the probes kept overlapping the other stream's launches:
+    state 4, "contended"), and no timing that overlapped the other stream was used."""
+    import threading
+    torch = torch_dev
+    k, m, L, S = 12, 4, 1 << 20, 24
+    rs = ecx.ReedSolomon.create(k, m)
+    emap = rs.encode_map()
+    pools = [torch.empty((S, 16, L), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for i, p in enumerate(pools):
+        ecx.fill_random(p, p.numel(), 300 + i)
+    torch.cuda.synchronize()
+    errors = []
+
+    def drive(i):
+        try:
+            st = torch.cuda.Stream()
+            for _ in range(100):
+                emap.apply_batch(pools[i], 16 * L, L, pools[i], 16 * L, L, S, L, stream=st)
+            st.synchronize()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=drive, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    choice = emap.layout_choice(L)
+    state, dropped = emap.layout_state(L)
+    assert choice != -1 and state in (1, 3, 4), (choice, state, dropped)
+    assert dropped > 0  # the two streams' launches overlapped: those probes were not used
+    for p in pools:
+        for s in (0, S - 1):
+            host = p[s].cpu().numpy()
+            ref = [host[i].copy() for i in range(16)]
+            for i in range(k, 16):
+                ref[i][:] = 0
+            O.ReedSolomon(k, m).encode_parity(ref, 0, L)
+            assert all((ref[i] == host[i]).all() for i in range(k, 16)), s
