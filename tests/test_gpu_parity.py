@@ -2179,9 +2179,9 @@ def test_layout_selection_two_streams(ecx, torch_dev):
     def drive(i):
         try:
             st = torch.cuda.Stream()
-            for _ in range(100):
+            for _ in range(120):  # each caller waits for its launch, as a synchronous caller does:
                 emap.apply_batch(pools[i], 16 * L, L, pools[i], 16 * L, L, S, L, stream=st)
-            st.synchronize()
+                st.synchronize()  # finished probes are harvested on the next call
         except Exception as e:  # noqa: BLE001 - reported below
             errors.append(e)
 
