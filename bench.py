@@ -81,7 +81,7 @@ WORKLOADS = {
 # ecx_tune keys the product library always accepts (include/ecx_tune.h); --tune of any other key
 # opts this process in to the shape knobs (ECX_SHAPE_KNOBS=1)
 DEPLOYMENT_KEYS = {"layout_select", "plan_cache", "roctx", "host_chunk_kib", "host_buffers", "host_gather_kib",
-                   "host_zero_copy", "host_contexts"}
+                   "host_zero_copy", "host_contexts", "host_exec_kib"}
 # the one published reference number for a workload: vs_baseline = value / it
 PUBLISHED = {"rs173": 525.7}  # MB/s, RS(17,3) encodeParity, InputOutputByteTableCodingLoop (rs/README.md:53)
 

@@ -4,7 +4,7 @@
  * results are bit-identical for every setting, only speed changes.
  *
  * Two classes of keys.  DEPLOYMENT keys -- "layout_select", "plan_cache", "roctx" and the
- * host_* keys -- are always accepted.  Every other key below is a SHAPE key: the product
+ * host_* keys (host_exec_kib included) -- are always accepted.  Every other key below is a SHAPE key: the product
  * library accepts it only when the process set ECX_SHAPE_KNOBS=1 in its environment before
  * its first ecx_tune call (read once; tests, bench.py --tune and the scripts/ A/B harnesses
  * do), and otherwise refuses it with ECX_E_ILLEGAL_ARGUMENT -- so no caller sharing the
@@ -120,6 +120,12 @@
  *   "host_gather_kib"  per-call host entry points: byte counts up to this many KiB are gathered
  *                      through pinned staging (one H2D / one D2H); 0 = always per-slot copies
  *                      (default 512)
+ *   "host_exec_kib"    per-call host entry points (the CodingLoop / ReedSolomon / Clay byte[][] calls):
+ *                      byte counts up to this many KiB run on the calling thread (host_exec.cpp:
+ *                      AVX-512 GFNI affine multiplies, else AVX2 nibble tables) instead of a device
+ *                      round trip -- below the measured per-call crossover (default 8; 0 = every
+ *                      call on the device).  Never a fallback: without a HIP device these calls
+ *                      fail with ECX_E_DEVICE like the device path
  *   "host_zero_copy"   per-call host entry points on the gather path: 1 = the kernel reads and
  *                      writes the pinned staging area over PCIe (no DMA copies; default);
  *                      0 = one H2D and one D2H copy
@@ -165,6 +171,9 @@ extern "C" {
 int ecx_tune(const char *key, int value); /* 0, or ECX_E_ILLEGAL_ARGUMENT for an unknown key */
 /* 1 in the diagnostic library (make DIAG=1, libecx_diag.so), 0 in the product library. */
 int ecx_build_diag(void);
+/* The per-call host executor's instruction set ("host_exec_kib"): 2 AVX-512BW + GFNI, 1 AVX2,
+ * 0 scalar. */
+int ecx_host_exec_isa(void);
 /* Pure-bandwidth probes over nbytes (multiple of 16 KiB) of device memory:
  * kind 0 = read-only stream, kind 1 = copy src -> dst.  Enqueued on `stream`. */
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream);

@@ -1177,7 +1177,7 @@ bool lab_key(const std::string &k) {
 // one library loaded into a JVM cannot reshape every other caller's launches.
 bool deployment_key(const std::string &k) {
     return k == "host_chunk_kib" || k == "host_buffers" || k == "host_gather_kib" || k == "host_zero_copy" ||
-           k == "host_contexts" || k == "roctx" || k == "plan_cache" || k == "layout_select";
+           k == "host_contexts" || k == "host_exec_kib" || k == "roctx" || k == "plan_cache" || k == "layout_select";
 }
 
 bool shape_knobs_enabled() {
@@ -1334,6 +1334,10 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.lds_lut = value;
     }
+    else if (k == "host_exec_kib") {
+        if (value < 0 || value > (1 << 20)) return ECX_E_ILLEGAL_ARGUMENT;
+        t.host_exec_max = (int64_t)value << 10;
+    }
     else if (k == "host_buffers") {
         if (value < 1 || value > 8) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_buffers = value;
@@ -1369,6 +1373,8 @@ int ecx_map_plan_stats(const ecx_map *map, int *n_tiles, int *n_entries, int *n_
 }
 
 int ecx_build_diag(void) { return ECX_DIAG ? 1 : 0; }
+
+int ecx_host_exec_isa(void) { return host_exec_isa(); }
 
 int ecx_map_layout_choice(const ecx_map *map, int64_t slot_pitch, float *median_ms, int n) {
     return guarded(__func__, [&]() -> int {

@@ -1022,10 +1022,29 @@ struct DrainOnUnwind {
 };
 }  // namespace
 
+bool host_exec_wanted(int64_t byte_count) {
+    const int64_t max = tuning().host_exec_max;
+    if (max <= 0 || byte_count <= 0 || byte_count > max) return false;
+    static const int count = [] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) {
+            (void)hipGetLastError();
+            n = 0;
+        }
+        return n;
+    }();
+    if (count <= 0) throw Error(ECX_E_DEVICE, "hipGetDeviceCount: no HIP device");
+    return true;
+}
+
 void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
               int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return;
     check_host_buffers(cm.map(), inputs, outputs);
+    if (host_exec_wanted(byte_count)) {  // below the per-call crossover (host_exec.cpp)
+        host_exec_apply(cm.map(), inputs, outputs, offset, byte_count);
+        return;
+    }
     DeviceContext::Lease lease = DeviceContext::acquire();
     DeviceContext &ctx = *lease.ctx;
     DrainOnUnwind drain{ctx.stream};
@@ -1095,6 +1114,7 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
 bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count) {
     if (byte_count <= 0 || cm.map().n_out == 0) return true;
     check_host_buffers(cm.map(), inputs, nullptr);
+    if (host_exec_wanted(byte_count)) return host_exec_all_zero(cm.map(), inputs, offset, byte_count);
     DeviceContext::Lease lease = DeviceContext::acquire();
     DeviceContext &ctx = *lease.ctx;
     DrainOnUnwind drain{ctx.stream};

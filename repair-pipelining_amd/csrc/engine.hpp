@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "codes.hpp"
+#include "host_exec.hpp"
 
 namespace ecx {
 
@@ -345,6 +346,9 @@ struct Tuning {
     // profiles/r02_percall_sizes.jsonl)
     int64_t host_gather_max = 512 << 10;
     int host_contexts = 1;  // per-call host APIs: 1 = a pool of contexts (streams) leased per call, 0 = one per device
+    // per-call host APIs: byte counts up to this run on the calling thread (host_exec.cpp) instead of
+    // the device -- below the measured per-call crossover (profiles/r05_percall_threshold.jsonl); 0 = never
+    int64_t host_exec_max = 8 << 10;
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 // The process-wide tuning (include/ecx_tune.h).  tuning() returns a snapshot taken under
@@ -442,6 +446,11 @@ void run_host(CompiledMap &cm, const uint8_t *const *inputs, uint8_t *const *out
 // As run_host, but instead of copying outputs back, returns whether every
 // output byte is zero (used for checkSomeShards / isParityCorrect).
 bool run_host_all_zero(CompiledMap &cm, const uint8_t *const *inputs, int64_t offset, int64_t byte_count);
+
+// The per-call executor below the CPU/GPU crossover (host_exec.hpp): whether a per-call entry point
+// of `byte_count` bytes runs on the calling thread (Tuning::host_exec_max); throws ECX_E_DEVICE
+// when the process has no HIP device, as the device path would.
+bool host_exec_wanted(int64_t byte_count);
 
 // Host-memory batch over many stripes (host_pipe.cpp): the batch layout of
 // launch_apply, but `in`/`out` are host pointers.  Chunks of stripes are

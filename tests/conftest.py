@@ -18,6 +18,8 @@ for p in (ROOT, ROOT / "oracle"):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
     config.addinivalue_line("markers", "diag: needs the diagnostic library (make DIAG=1; ECX_LIB_PATH=.../libecx_diag.so)")
+    config.addinivalue_line("markers", "host_exec: exercises the per-call host executor (ecx_tune host_exec_kib); "
+                                       "every other test runs its per-call calls on the device")
 
 
 def pytest_runtest_setup(item):
@@ -27,6 +29,18 @@ def pytest_runtest_setup(item):
         import rpamd
         if not rpamd.load().is_diag():
             pytest.skip("diagnostic-library kernel (make DIAG=1, ECX_LIB_PATH=.../libecx_diag.so)")
+
+
+@pytest.fixture(autouse=True)
+def _per_call_on_device(request):
+    """Per-call entry points below the crossover run on the host executor by default
+    (ecx_tune "host_exec_kib"); the parity tests exercise the HIP kernels, so every test not
+    marked `host_exec` runs with the threshold at 0 (every call on the device)."""
+    import rpamd
+    ecx = rpamd.load(shape_knobs=True)
+    if request.node.get_closest_marker("host_exec") is None:
+        ecx.tune("host_exec_kib", 0)
+    yield
 
 
 def diag_build() -> bool:
