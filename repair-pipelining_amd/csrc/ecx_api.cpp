@@ -461,6 +461,11 @@ int ecx_code_single(const uint8_t *matrix_rows, int row_length, const uint8_t *i
         if (index < 0 || index >= row_length || output_index < 0) throw Error(ECX_E_INDEX, "matrix index");
         if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
         const uint8_t c = matrix_rows[(size_t)output_index * row_length + index];
+        if (host_exec_wanted(byte_count)) {  // below the per-call crossover: no plan, no device round trip
+            if (!input || !output) throw Error(ECX_E_NULL, "null buffer");
+            host_exec_scale(c, input + offset, output + offset, byte_count, !is_first_time);
+            return ECX_OK;
+        }
         const uint8_t row[2] = {c, (uint8_t)(is_first_time ? 0 : 1)};
         const std::shared_ptr<CompiledMap> cm = cached_plan(dense_map(row, 1, 2));
         const uint8_t *ins[2] = {input, output};
@@ -570,6 +575,11 @@ int ecx_rs_encode_parity_single(ecx_rs *rs, const uint8_t *shard, uint8_t *outpu
         if (output_index < 0 || output_index >= c.m() || input_index < 0 || input_index >= c.k())
             throw Error(ECX_E_INDEX, "parity row / column index");
         if (offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid counts");
+        if (host_exec_wanted(byte_count)) {  // below the per-call crossover: no plan, no device round trip
+            if (!shard || !output) throw Error(ECX_E_NULL, "null buffer");
+            host_exec_scale(c.parity_row(output_index)[input_index], shard + offset, output + offset, byte_count, true);
+            return ECX_OK;
+        }
         const uint8_t row[2] = {c.parity_row(output_index)[input_index], 1};
         const std::shared_ptr<CompiledMap> cm = cached_plan(dense_map(row, 1, 2));
         const uint8_t *ins[2] = {shard, output};

@@ -4,6 +4,7 @@
 #include "map_rtc.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <exception>
 #include <functional>
@@ -21,9 +22,14 @@ Tuning tuning() {
     return g_tuning;
 }
 
+namespace {
+std::atomic<int64_t> g_host_exec_max{Tuning{}.host_exec_max};  // Tuning::host_exec_max, read per call
+}
+
 void update_tuning(const std::function<void(Tuning &)> &f) {
     std::lock_guard<std::mutex> g(g_tuning_mu);
     f(g_tuning);
+    g_host_exec_max.store(g_tuning.host_exec_max, std::memory_order_relaxed);
 }
 
 static thread_local std::string g_last_kernel;
@@ -1023,7 +1029,7 @@ struct DrainOnUnwind {
 }  // namespace
 
 bool host_exec_wanted(int64_t byte_count) {
-    const int64_t max = tuning().host_exec_max;
+    const int64_t max = g_host_exec_max.load(std::memory_order_relaxed);
     if (max <= 0 || byte_count <= 0 || byte_count > max) return false;
     static const int count = [] {
         int n = 0;

@@ -57,11 +57,31 @@ int isa_level() {  // 2: AVX-512BW + GFNI, 1: AVX2, 0: scalar
     return v;
 }
 
+// Per-coefficient tables, built once: the GFNI bit matrix and the two AVX2 nibble tables of every c.
+struct CoefTables {
+    uint64_t affine[256];
+    alignas(16) uint8_t lo[256][16], hi[256][16];
+    CoefTables() {
+        const Field &f = Field::get();
+        for (int c = 0; c < 256; ++c) {
+            affine[c] = affine_of((uint8_t)c);
+            for (int v = 0; v < 16; ++v) {
+                lo[c][v] = f.mul((uint8_t)c, (uint8_t)v);
+                hi[c][v] = f.mul((uint8_t)c, (uint8_t)(v << 4));
+            }
+        }
+    }
+};
+const CoefTables &tables() {
+    static const CoefTables t;
+    return t;
+}
+
 struct Coef {
     const uint8_t *in;  // input row at the block's first byte
     uint8_t c;
-    uint64_t affine;   // GFNI matrix of c
-    uint8_t lo[16], hi[16];  // nibble tables of c (AVX2)
+    uint64_t affine;          // GFNI matrix of c
+    const uint8_t *lo, *hi;   // nibble tables of c (AVX2)
 };
 
 __attribute__((target("avx512f,avx512bw,gfni"))) void row_gfni(const Coef *cf, int n, uint8_t *acc, int64_t len) {
@@ -100,8 +120,8 @@ __attribute__((target("avx2"))) void row_avx2(const Coef *cf, int n, uint8_t *ac
                 s = _mm256_xor_si256(s, x);
                 continue;
             }
-            const __m256i tl = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)cf[k].lo));
-            const __m256i th = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)cf[k].hi));
+            const __m256i tl = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i *)cf[k].lo));
+            const __m256i th = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i *)cf[k].hi));
             const __m256i l = _mm256_shuffle_epi8(tl, _mm256_and_si256(x, nib));
             const __m256i h = _mm256_shuffle_epi8(th, _mm256_and_si256(_mm256_srli_epi16(x, 4), nib));
             s = _mm256_xor_si256(s, _mm256_xor_si256(l, h));
@@ -128,40 +148,37 @@ void row_scalar(const Coef *cf, int n, uint8_t *acc, int64_t len) {
 // out rows (or, with `zero`, only whether every row is zero) of map `m` over [offset, offset+len)
 bool apply_rows(const LinearMap &m, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
                 int64_t len, bool zero) {
-    const Field &f = Field::get();
+    const CoefTables &t = tables();
     const int level = isa_level();
-    std::vector<std::vector<Coef>> rows((size_t)m.n_out);
-    for (int o = 0; o < m.n_out; ++o)
+    thread_local std::vector<Coef> coefs;    // row o's coefficients: coefs[first[o] .. first[o + 1])
+    thread_local std::vector<int> first;
+    thread_local std::vector<uint8_t> scratch;
+    coefs.clear();
+    first.assign((size_t)m.n_out + 1, 0);
+    for (int o = 0; o < m.n_out; ++o) {
+        first[(size_t)o] = (int)coefs.size();
         for (int j = 0; j < m.n_in; ++j) {
             const uint8_t c = m.at(o, j);
-            if (!c) continue;
-            Coef k;
-            k.in = inputs[m.in_slot[j]] + offset;
-            k.c = c;
-            k.affine = level == 2 ? affine_of(c) : 0;
-            if (level == 1)
-                for (int v = 0; v < 16; ++v) {
-                    k.lo[v] = f.mul(c, (uint8_t)v);
-                    k.hi[v] = f.mul(c, (uint8_t)(v << 4));
-                }
-            rows[(size_t)o].push_back(k);
+            if (c) coefs.push_back({inputs[m.in_slot[j]] + offset, c, t.affine[c], t.lo[c], t.hi[c]});
         }
-    thread_local std::vector<uint8_t> scratch;
+    }
+    first[(size_t)m.n_out] = (int)coefs.size();
     const int64_t blk = std::min<int64_t>(len, kBlock);
     if (scratch.size() < (size_t)(m.n_out * blk)) scratch.resize((size_t)(m.n_out * blk));
     for (int64_t b0 = 0; b0 < len; b0 += kBlock) {
         const int64_t w = std::min<int64_t>(kBlock, len - b0);
         for (int o = 0; o < m.n_out; ++o) {
-            std::vector<Coef> &r = rows[(size_t)o];
+            Coef *r = coefs.data() + first[(size_t)o];
+            const int n = first[(size_t)o + 1] - first[(size_t)o];
             uint8_t *acc = scratch.data() + (size_t)o * blk;
-            if (r.empty()) {
+            if (n == 0) {
                 std::memset(acc, 0, (size_t)w);
                 continue;
             }
-            if (level == 2) row_gfni(r.data(), (int)r.size(), acc, w);
-            else if (level == 1) row_avx2(r.data(), (int)r.size(), acc, w);
-            else row_scalar(r.data(), (int)r.size(), acc, w);
-            for (Coef &k : r) k.in += w;
+            if (level == 2) row_gfni(r, n, acc, w);
+            else if (level == 1) row_avx2(r, n, acc, w);
+            else row_scalar(r, n, acc, w);
+            for (int k = 0; k < n; ++k) r[k].in += w;
         }
         if (zero) {
             for (int o = 0; o < m.n_out; ++o) {
@@ -189,6 +206,24 @@ void host_exec_apply(const LinearMap &m, const uint8_t *const *inputs, uint8_t *
 
 bool host_exec_all_zero(const LinearMap &m, const uint8_t *const *inputs, int64_t offset, int64_t byte_count) {
     return apply_rows(m, inputs, nullptr, offset, byte_count, true);
+}
+
+void host_exec_scale(uint8_t c, const uint8_t *in, uint8_t *out, int64_t n, bool accumulate) {
+    const CoefTables &t = tables();
+    const int level = isa_level();
+    // out (=|^=) c * in, in blocks through a small stack buffer (out may alias in)
+    uint8_t acc[1024];
+    Coef k[2] = {{in, c, t.affine[c], t.lo[c], t.hi[c]}, {out, 1, t.affine[1], t.lo[1], t.hi[1]}};
+    const int terms = accumulate ? 2 : 1;
+    for (int64_t b0 = 0; b0 < n; b0 += (int64_t)sizeof(acc)) {
+        const int64_t w = std::min<int64_t>((int64_t)sizeof(acc), n - b0);
+        if (level == 2) row_gfni(k, terms, acc, w);
+        else if (level == 1) row_avx2(k, terms, acc, w);
+        else row_scalar(k, terms, acc, w);
+        std::memcpy(out + b0, acc, (size_t)w);
+        k[0].in += w;
+        k[1].in += w;
+    }
 }
 
 int host_exec_isa() { return isa_level(); }

@@ -13,6 +13,8 @@ void host_exec_apply(const LinearMap &m, const uint8_t *const *inputs, uint8_t *
                      int64_t byte_count);
 // whether every output row of the map over the range is zero (isParityCorrect / checkSomeShards)
 bool host_exec_all_zero(const LinearMap &m, const uint8_t *const *inputs, int64_t offset, int64_t byte_count);
+// the one-coefficient call of encodeParitySingle / code_single: out (=, or ^= with accumulate) c * in
+void host_exec_scale(uint8_t c, const uint8_t *in, uint8_t *out, int64_t n, bool accumulate);
 int host_exec_isa();  // 2 AVX-512BW + GFNI, 1 AVX2, 0 scalar
 // Test hook (tests/native/host_exec_check.cpp): run the given level (-1 = detect) if this CPU has it;
 // returns the level, or -1 when the CPU lacks it.  Not thread-safe; not exported by libecx.

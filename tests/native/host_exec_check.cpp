@@ -105,6 +105,24 @@ void check_level(int level) {
             expect(!host_exec_all_zero(chk, ins.data(), off, len), "one flipped byte makes it non-zero", level);
         }
     }
+    // the one-coefficient form (encodeParitySingle / code_single), assign and accumulate
+    for (int64_t len : {1, 34, 1023, 1024, 1025, 5000}) {
+        std::vector<uint8_t> y((size_t)len), x((size_t)len);
+        for (auto &v : y) v = (uint8_t)rng();
+        for (auto &v : x) v = (uint8_t)rng();
+        for (int acc = 0; acc < 2; ++acc) {
+            const uint8_t c = (uint8_t)(rng() | 2);
+            std::vector<uint8_t> want = x;
+            for (int64_t i = 0; i < len; ++i)
+                want[(size_t)i] = (uint8_t)((acc ? x[(size_t)i] : 0) ^ f.mul(c, y[(size_t)i]));
+            host_exec_scale(c, y.data(), x.data(), len, acc != 0);
+            expect(x == want, "host_exec_scale", level);
+        }
+        std::vector<uint8_t> want = y;  // in place: y = 3 * y
+        for (auto &v : want) v = f.mul(3, v);
+        host_exec_scale(3, y.data(), y.data(), len, false);
+        expect(y == want, "host_exec_scale in place", level);
+    }
     // aliasing: x ^= c * y (code_single's accumulate row [c, 1] over {y, x} written to x)
     for (int64_t len : {33, 4096, 9000}) {
         LinearMap m;
