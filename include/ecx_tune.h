@@ -43,10 +43,6 @@
  *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
  *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel; 2 = auto (default):
  *                      the small variant for maps of <= 2 rows over <= 4 inputs (LRC block repair)
- *   "pad_first"        padding entries of a tile's load ring (coefficient 0, appended to reach a multiple
- *                      of the ring depth: RS(17,3)'s 17 inputs on a ring of 8 read 24 times): 1 = re-read
- *                      the tile's first input at the lane's offset, an L2 hit on the workgroup's own
- *                      lines (default); 0 = read the device's shared 4 KiB zero page
  *   "plan_cache"       per-call entry points that receive or derive their coefficients per call
  *                      (ecx_code_some_shards, ecx_check_some_shards, ecx_code_single,
  *                      ecx_rs_encode_parity_single, ecx_rs_decode_missing_single): compiled plans

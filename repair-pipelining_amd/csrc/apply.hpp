@@ -245,9 +245,6 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
     // selecting the zero page.  Other kernels use 64-bit global addresses.
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t first_soff = 0;
-    // padding entries re-read the tile's first input (pad_first) or the shared zero page
-    const uint32_t first_slot = ecnt > 0 ? plan_ptr(a.entries)[(int64_t)ebeg * kEntryDwords] : 0u;
-    const uint8_t *pad = a.pad_first ? ib + (int64_t)first_slot * a.in_slot_stride : a.zero_page + zoff;
     if constexpr (TLDS && !SAFE) {
         rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(in_base), 0, 0x7FFFFFFF, 0x00020000);
         if (ecnt > 0) first_soff = plan_ptr(a.entries)[(int64_t)ebeg * kEntryDwords] * (uint32_t)a.in_slot_stride;
@@ -258,7 +255,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, cu32 *tile, uint6
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)zoff, (int)soff, NTL ? 2 : 0);
             return (u32x4){(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]};
         } else {
-            const uint8_t *p = slot == kDummySlot ? pad : ib + (int64_t)slot * a.in_slot_stride;
+            const uint8_t *p = slot == kDummySlot ? a.zero_page + zoff : ib + (int64_t)slot * a.in_slot_stride;
             return SAFE ? load_partial(p, valid) : ld16<NTL>(p);
         }
     };

@@ -39,10 +39,8 @@ __global__ void __launch_bounds__(kBlockThreads, ROWS < kTileRows ? (DEPTH >= 16
     cu32 *tile = plan_ptr(a.tiles) + __builtin_amdgcn_readfirstlane(tl) * kTileDwords;
     const uint8_t *ib =
         reinterpret_cast<const uint8_t *>(uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase))) + lane16;
-    const uint32_t first_slot = tile[1] > 0 ? plan_ptr(a.entries)[(int64_t)tile[0] * kEntryDwords] : 0u;
-    const uint8_t *pad = a.pad_first ? ib + (int64_t)first_slot * a.in_slot_stride : a.zero_page + lane16;
-    auto load = [&](uint32_t slot) -> u32x4 {  // padding entries: the first input again, or the zero page
-        const uint8_t *p = slot == kDummySlot ? pad : ib + (int64_t)slot * a.in_slot_stride;
+    auto load = [&](uint32_t slot) -> u32x4 {  // padding entries read the zero page
+        const uint8_t *p = slot == kDummySlot ? a.zero_page + lane16 : ib + (int64_t)slot * a.in_slot_stride;
         return SAFE ? load_partial(p, valid) : ld16<true>(p);
     };
     const int ecnt = (int)tile[1];  // padded to a multiple of DEPTH
@@ -126,7 +124,6 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     a.xcd_group = tu.xcd_group == 3 ? 3 : (tu.xcd_misaligned && misaligned128 ? 3 : 0);
     a.xcd_run = tu.xcd_run;
     a.tail_chunk = fuse_tail ? full : -1;
-    a.pad_first = tu.pad_first;
     auto run = [&](bool safe, const DevicePlan &p, int64_t chunk_begin, int64_t n_chunks) {
         if (n_chunks <= 0) return;
         a.entries = p.entries;

@@ -35,12 +35,9 @@ __global__ void __launch_bounds__(THREADS, ROWS * K <= 8 ? 5 : 4) k_gf_apply_ske
     cu32 *tile = plan_ptr(a.tiles);
     const uint8_t *ib = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)(a.in + s * a.in_stripe_stride + cbase))) +
                         lane16;
-    const uint32_t first_slot = tile[1] > 0 ? plan_ptr(a.entries)[(int64_t)tile[0] * kEntryDwords] : 0u;
     auto load = [&](uint32_t slot, int chunk) -> u32x4 {
-        const uint8_t *p = slot == kDummySlot
-                               ? (a.pad_first ? ib + (int64_t)first_slot * a.in_slot_stride + chunk * kChunkBytes
-                                              : a.zero_page + lane16)
-                               : ib + (int64_t)slot * a.in_slot_stride + chunk * kChunkBytes;
+        const uint8_t *p = slot == kDummySlot ? a.zero_page + lane16
+                                              : ib + (int64_t)slot * a.in_slot_stride + chunk * kChunkBytes;
         return ld16<NTL>(p);
     };
     u32x4 acc[K][ROWS];

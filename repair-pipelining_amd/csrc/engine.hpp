@@ -246,9 +246,6 @@ struct ApplyArgs {
     // runs in the same launch as the full chunks (-1: none), and its byte count (a multiple of 16)
     int64_t tail_chunk;
     int tail_bytes;
-    // padding entries (kDummySlot, coefficient 0): 1 = re-read the tile's first input at the lane's
-    // offset (an L2 hit on this workgroup's own lines), 0 = read the device's shared zero page
-    int pad_first;
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -349,9 +346,6 @@ struct Tuning {
     // profiles/r02_percall_sizes.jsonl)
     int64_t host_gather_max = 512 << 10;
     int host_contexts = 1;  // per-call host APIs: 1 = a pool of contexts (streams) leased per call, 0 = one per device
-    // k_gf_apply / _skew / k_gf_check padding loads: 1 = the tile's first input again (default), 0 = the
-    // shared zero page (every workgroup of the chip on the same 4 KiB)
-    int pad_first = 1;
     // per-call host APIs: byte counts up to this run on the calling thread (host_exec.cpp) instead of
     // the device -- below the measured per-call crossover (profiles/r05_percall_threshold.jsonl); 0 = never
     int64_t host_exec_max = 8 << 10;

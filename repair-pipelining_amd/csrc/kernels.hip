@@ -440,7 +440,6 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     a.accumulate = accumulate ? 1 : 0;
     a.tail_chunk = -1;
     a.tail_bytes = 0;
-    a.pad_first = tu.pad_first;
 
     bool tail_launch = false;  // the next non-safe run covers the partial last chunk (k_gf_apply_tail)
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
