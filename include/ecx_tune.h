@@ -174,6 +174,10 @@ int ecx_build_diag(void);
 /* The per-call host executor's instruction set ("host_exec_kib"): 2 AVX-512BW + GFNI, 1 AVX2,
  * 0 scalar. */
 int ecx_host_exec_isa(void);
+/* The stripe range [*begin, *end) that device entry j of `parts` takes in the multi-GPU host
+ * batches (ecx_*_batch_host_devices): contiguous ranges, the remainder on the first entries.
+ * Host-only; ECX_E_ILLEGAL_ARGUMENT for a bad request. */
+int ecx_stripe_range(int64_t nstripes, int parts, int j, int64_t *begin, int64_t *end);
 /* Pure-bandwidth probes over nbytes (multiple of 16 KiB) of device memory:
  * kind 0 = read-only stream, kind 1 = copy src -> dst.  Enqueued on `stream`. */
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream);

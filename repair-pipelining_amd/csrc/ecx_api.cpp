@@ -1386,6 +1386,12 @@ int ecx_build_diag(void) { return ECX_DIAG ? 1 : 0; }
 
 int ecx_host_exec_isa(void) { return host_exec_isa(); }
 
+int ecx_stripe_range(int64_t nstripes, int parts, int j, int64_t *begin, int64_t *end) {
+    if (nstripes < 0 || parts <= 0 || j < 0 || j >= parts || !begin || !end) return ECX_E_ILLEGAL_ARGUMENT;
+    stripe_range(nstripes, parts, j, begin, end);
+    return ECX_OK;
+}
+
 int ecx_map_layout_choice(const ecx_map *map, int64_t slot_pitch, float *median_ms, int n) {
     return guarded(__func__, [&]() -> int {
         if (!map) throw Error(ECX_E_NULL, "null map");

@@ -461,6 +461,9 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
                     uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                     int64_t nbytes);
 
+// Part j of `parts` contiguous stripe ranges of nstripes, the remainder on the first parts (the
+// rule of shard_stripes, __init__.py; run_host_batch_devices' split).
+void stripe_range(int64_t nstripes, int parts, int j, int64_t *begin, int64_t *end);
 // run_host_batch over several devices (host_pipe.cpp): device j of `devices` takes the
 // contiguous stripe range j of ndev (remainder on the first), on a worker thread of its own
 // with that device's pipe.  Refuses bad device ids before any copy; joins every worker, then

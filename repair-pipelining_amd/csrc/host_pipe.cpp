@@ -163,6 +163,13 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     }
 }
 
+void stripe_range(int64_t nstripes, int parts, int j, int64_t *begin, int64_t *end) {
+    // contiguous ranges, the remainder on the first ones (shard_stripes, __init__.py)
+    const int64_t base = nstripes / parts, extra = nstripes % parts;
+    *begin = j * base + std::min<int64_t>(j, extra);
+    *end = *begin + base + (j < extra ? 1 : 0);
+}
+
 void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                             uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                             int64_t nbytes, const int *devices, int ndev) {
@@ -180,10 +187,10 @@ void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_strip
         std::string what;
     };
     std::vector<Result> res((size_t)ndev);
-    // Device j's range: contiguous, the remainder on the first ranges (shard_stripes, __init__.py).
-    const int64_t base = nstripes / ndev, extra = nstripes % ndev;
     auto work = [&](int j) {
-        const int64_t lo = j * base + std::min<int64_t>(j, extra), n = base + (j < extra ? 1 : 0);
+        int64_t lo = 0, hi = 0;
+        stripe_range(nstripes, ndev, j, &lo, &hi);
+        const int64_t n = hi - lo;
         if (n <= 0) return;
         try {
             check_hip(hipSetDevice(devices[j]), "hipSetDevice (host batch worker)");

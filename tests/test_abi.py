@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(ecx):
     assert headers == ["ecx.h", "ecx_tune.h"]
     missing = [s for h in headers for s in declared_symbols(h) if not hasattr(lib, s)]
     assert not missing, missing
-    assert len(declared_symbols("ecx_tune.h")) == 15
+    assert len(declared_symbols("ecx_tune.h")) == 16
 
 
 def test_binding_table_matches_header(ecx):
@@ -307,3 +307,25 @@ print(out)
         got = eval(r.stdout.strip().splitlines()[-1])
         for k, st in got.items():
             assert st == (0 if (k in deploy or opt_in) else -1), (opt_in, k, st)
+
+
+def test_multi_gpu_host_batch_split_matches_shard_stripes(ecx):
+    """The multi-GPU host batches split a batch exactly as shard_stripes partitions stripes
+    across ranks (ecx_stripe_range, the split run_host_batch_devices uses): contiguous, covering,
+    the remainder on the first entries; bad requests are refused."""
+    f = ecx.lib().ecx_stripe_range
+    f.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                  ctypes.POINTER(ctypes.c_int64)]
+    f.restype = ctypes.c_int
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    for n in (0, 1, 5, 7, 8, 1023, 1 << 20, (1 << 33) + 3):
+        for parts in (1, 2, 3, 7, 8, 13):
+            prev = 0
+            for j in range(parts):
+                assert f(n, parts, j, ctypes.byref(b), ctypes.byref(e)) == 0
+                assert (b.value, e.value) == ecx.shard_stripes(n, parts, j)
+                assert b.value == prev
+                prev = e.value
+            assert prev == n
+    for bad in ((-1, 2, 0), (5, 0, 0), (5, 2, 2), (5, 2, -1)):
+        assert f(*bad, ctypes.byref(b), ctypes.byref(e)) == -1
