@@ -456,9 +456,10 @@ class Workload:
     def host_expect(self, hin, hout, n) -> bool:
         """The host outputs of the first n stripes equal the device run's."""
         import numpy as np
-        got = (hin if self.host_out_bytes() == 0 else hout)[:n * max(self.host_out_bytes(), 1)]
-        if self.host_out_bytes() == 0:
+        if self.host_out_bytes() == 0:  # written in place: the whole host stripes equal the device pool's
+            got = hin[:n * self.host_stripe_bytes()]
             return bool(np.array_equal(got.reshape(n, -1), self.pool[:n].reshape(n, -1).cpu().numpy()))
+        got = hout[:n * self.host_out_bytes()]
         return bool(np.array_equal(got.reshape(n, -1), self.out[:n].reshape(n, -1).cpu().numpy()))
 
     def pcie_bytes(self):

@@ -208,3 +208,25 @@ def test_round_scripts_cover_every_workload():
         for w in names.split("|"):
             pools[w] = int(pool)
     assert pools == {w: v[1] for w, v in bench.WORKLOADS.items()}
+
+
+def test_e2e_host_expect_in_place_and_separate():
+    """The end-to-end leg's verification (Workload.host_expect): written-in-place workloads
+    compare the whole host stripes with the device pool, the others the host outputs with the
+    device outputs; one differing byte is caught either way (CPU tensors stand in for HBM)."""
+    import numpy as np
+    import torch
+    pool = torch.randint(0, 256, (3, 20, 64), dtype=torch.uint8)
+    r = _bare(bench.RS173, pool=pool, L=64)
+    hin = pool.numpy().reshape(-1).copy()
+    assert r.host_out_bytes() == 0 and r.host_stripe_bytes() == 20 * 64
+    assert r.host_expect(hin, np.empty(0, np.uint8), 3)
+    hin[2 * 20 * 64 + 17 * 64 + 5] ^= 1  # a parity byte of the last stripe
+    assert not r.host_expect(hin, np.empty(0, np.uint8), 3)
+    out = torch.randint(0, 256, (3, 8, 32), dtype=torch.uint8)
+    c = _bare(bench.Clay42, pool=torch.zeros((3, 48, 32), dtype=torch.uint8), out=out)
+    hout = out.numpy().reshape(-1).copy()
+    assert c.host_expect(np.empty(0, np.uint8), hout, 3)
+    hout[-1] ^= 0x80
+    assert not c.host_expect(np.empty(0, np.uint8), hout, 3)
+    assert c.pcie_bytes() == (20 * 32768, 8 * 32768)
