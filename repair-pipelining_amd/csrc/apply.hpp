@@ -394,6 +394,10 @@ void launch_shape_t(const Shape &s, dim3 grid, size_t lds, hipStream_t stream, c
 void launch_skew(int k, int rows, int depth, bool ntl, int threads, dim3 grid, hipStream_t stream,
                  const ApplyArgs &a);
 
+// k_gf_apply_multi (apply_multi.hip): single-tile maps, `units` consecutive (stripe, chunk) units per
+// workgroup, one load ring across them; grid = ceil(ApplyArgs::multi_total / units).
+void launch_multi(int units, int depth, int threads, bool tail, dim3 grid, hipStream_t stream, const ApplyArgs &a);
+
 // k_gf_bits (apply_bits.hip): the bit-sliced kernel, 128-lane workgroups over 4 KiB
 // chunks, ring depth 2 or 4; grid = stripes x chunks x tiles, as k_gf_apply.
 void launch_bits(bool ntl, int depth, dim3 grid, hipStream_t stream, const ApplyArgs &a);

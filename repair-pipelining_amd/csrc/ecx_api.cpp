@@ -1344,6 +1344,10 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.lds_lut = value;
     }
+    else if (k == "units") {
+        if (value != 1 && value != 2 && value != 4) return ECX_E_ILLEGAL_ARGUMENT;
+        t.units = value;
+    }
     else if (k == "host_exec_kib") {
         if (value < 0 || value > (1 << 20)) return ECX_E_ILLEGAL_ARGUMENT;
         t.host_exec_max = (int64_t)value << 10;

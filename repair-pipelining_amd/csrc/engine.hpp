@@ -246,6 +246,7 @@ struct ApplyArgs {
     // runs in the same launch as the full chunks (-1: none), and its byte count (a multiple of 16)
     int64_t tail_chunk;
     int tail_bytes;
+    int64_t multi_total;  // k_gf_apply_multi: (stripe, chunk) units in the launch
 };
 
 // Launch-shape knobs (diagnostics / tuning, include/ecx_tune.h).
@@ -349,6 +350,9 @@ struct Tuning {
     // per-call host APIs: byte counts up to this run on the calling thread (host_exec.cpp) instead of
     // the device -- below the measured per-call crossover (profiles/r05_percall_threshold.jsonl); 0 = never
     int64_t host_exec_max = 8 << 10;
+    // single-tile maps: (stripe, chunk) units per workgroup with one load ring across them
+    // (k_gf_apply_multi, apply_multi.hip): 1 = one unit per workgroup (k_gf_apply), 2 or 4
+    int units = 1;
 };
 void launch_probe(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, bool nt, hipStream_t stream);
 // The process-wide tuning (include/ecx_tune.h).  tuning() returns a snapshot taken under

@@ -398,6 +398,11 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         skew = 0;
         depth = 4;
     }
+    // Several units per workgroup with one ring across them (k_gf_apply_multi, ecx_tune "units"):
+    // single-tile maps on the default NT shape, rings of 4 / 8 (and 20 on 256 threads)
+    const bool multi = tu.units > 1 && cm.n_tiles() == 1 && !waves && !wide && !bits && !lut && !planes && !skew &&
+                       rows == kTileRows && ntmode == 2 && nts == 1 && tu.lds_tables != 2 &&
+                       (depth == 4 || depth == 8 || (depth == 20 && threads == kBlockThreads));
     const DevicePlan &plan = cm.plan_for_current_device(depth);
     // Multi-tile maps can run as tile groups (one wave per tile, 1 KiB chunks); otherwise
     // one workgroup per (stripe, chunk, tile) with 4 KiB (256 threads) or 1 KiB (64) chunks.
@@ -440,6 +445,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     a.accumulate = accumulate ? 1 : 0;
     a.tail_chunk = -1;
     a.tail_bytes = 0;
+    a.multi_total = 0;
 
     bool tail_launch = false;  // the next non-safe run covers the partial last chunk (k_gf_apply_tail)
     auto run = [&](bool safe, int64_t chunk_begin, int64_t n_chunks) {
@@ -486,6 +492,12 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                     if (ntl) hipLaunchKernelGGL((k_gf_apply_wide<false, true, 1, 4>), grid, blk, 0, stream, a);
                     else hipLaunchKernelGGL((k_gf_apply_wide<false, false, 1, 4>), grid, blk, 0, stream, a);
                 }
+                continue;
+            }
+            if (multi && !safe) {
+                a.multi_total = ns * per_stripe;
+                launch_multi(tu.units, depth, threads, tail_launch,
+                             dim3((unsigned)((a.multi_total + tu.units - 1) / tu.units)), stream, a);
                 continue;
             }
             Shape s;

@@ -2204,3 +2204,73 @@ def test_layout_selection_two_streams(ecx, torch_dev):
                 ref[i][:] = 0
             O.ReedSolomon(k, m).encode_parity(ref, 0, L)
             assert all((ref[i] == host[i]).all() for i in range(k, 16)), s
+
+
+@pytest.mark.parametrize("units", [2, 4])
+def test_multi_unit_workgroups_match(ecx, torch_dev, units):
+    """k_gf_apply_multi (ecx_tune "units": several (stripe, chunk) units per workgroup, one load
+    ring across them) writes the same bytes as k_gf_apply on every single-tile shape it serves --
+    the 20-deep headline ring (Clay(4,2) repair), the RS(17,3) encode with its fused partial last
+    chunk, one-wave RS(12,4) decode, accumulate mode -- with stripe counts that leave the last
+    workgroup short, and the oracle agrees on a sampled stripe."""
+    import oracle as O
+    torch = torch_dev
+
+    def run(fn, out):
+        ecx.tune("units", 1)
+        ecx.tune("layout_select", 0)
+        try:
+            ref = out.clone()
+            fn(ref)
+            ecx.tune("units", units)
+            got = out.clone()
+            fn(got)
+            torch.cuda.synchronize()
+            return ref, got, ecx.last_kernel()
+        finally:
+            ecx.tune("units", 1)
+            ecx.tune("layout_select", 1)
+
+    # Clay(4,2) repair, 32 KiB, 7 stripes (odd)
+    S, B = 7, 32768
+    pool = torch.empty((S, 48, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 71)
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    out = torch.zeros((S, 8, B), dtype=torch.uint8, device="cuda")
+    ref, got, kern = run(lambda o: step.performCodingBatch(pool, 48 * B, B, o, 8 * B, B, S, B), out)
+    assert kern.startswith("k_gf_apply_multi<20"), kern
+    assert torch.equal(ref, got)
+    host = pool[S - 1].cpu().numpy()
+    oref = [np.zeros(B, np.uint8) for _ in range(8)]
+    O.Clay(4, 2, [1]).perform_coding([None if i % 6 == 1 else host[i].copy() for i in range(48)], oref, B)
+    assert all((got[S - 1, z].cpu().numpy() == oref[z]).all() for z in range(8))
+    # RS(17,3) encode in place on the published shape (fused partial chunk), 5 stripes
+    S, L = 5, 200000
+    rpool = torch.empty((S, 20, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(rpool, rpool.numel(), 72)
+    rs = ecx.ReedSolomon.create(17, 3)
+    ref, got, kern = run(lambda p: rs.encodeParityBatch(p, 20 * L, L, S, 0, L), rpool)
+    assert kern.startswith("k_gf_apply_multi<8") and kern.endswith("true>"), kern
+    assert torch.equal(ref, got)
+    h = got[2].cpu().numpy()
+    sh = [h[i].copy() for i in range(20)]
+    for i in range(17, 20):
+        sh[i][:] = 0
+    O.ReedSolomon(17, 3).encode_parity(sh, 0, L)
+    assert all((sh[i] == h[i]).all() for i in range(17, 20))
+    # RS(12,4) decode {0, 1} into a separate buffer, one-wave workgroups forced; accumulate mode
+    S, L = 3, 1 << 20
+    dpool = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(dpool, dpool.numel(), 73)
+    dmap = ecx.ReedSolomon.create(12, 4).decode_map([False, False] + [True] * 14)
+    acc0 = torch.empty((S, 2, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(acc0, acc0.numel(), 74)
+    ecx.tune("block_threads", 64)
+    try:
+        ref, got, kern = run(lambda o: dmap.apply_batch(dpool, 16 * L, L, o, 2 * L, L, S, L), acc0)
+        assert ", 64, " in kern and kern.startswith("k_gf_apply_multi"), kern
+        assert torch.equal(ref, got)
+        ref, got, kern = run(lambda o: dmap.accumulate_batch(dpool, 16 * L, L, o, 2 * L, L, S, L), acc0)
+        assert torch.equal(ref, got) and not torch.equal(got, acc0)
+    finally:
+        ecx.tune("block_threads", 0)
