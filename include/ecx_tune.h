@@ -43,10 +43,6 @@
  *   "small_tiles"      single-tile maps of <= 2 or <= 4 rows: 1 = kernel variants with that many
  *                      accumulator rows (fewer VGPRs); 0 = the 8-row kernel; 2 = auto (default):
  *                      the small variant for maps of <= 2 rows over <= 4 inputs (LRC block repair)
- *   "units"            single-tile maps on the default non-temporal shape: (stripe, chunk) units per
- *                      workgroup with one load ring running across them, so a unit's stores leave
- *                      while the next unit's loads are in flight (k_gf_apply_multi): 1 = one unit per
- *                      workgroup (default), 2 or 4
  *   "plan_cache"       per-call entry points that receive or derive their coefficients per call
  *                      (ecx_code_some_shards, ecx_check_some_shards, ecx_code_single,
  *                      ecx_rs_encode_parity_single, ecx_rs_decode_missing_single): compiled plans
@@ -163,6 +159,11 @@
  *   [DIAG] "rtc_units"        the plane-group kernel's 512-B slices per workgroup: 1 (default), or 2 with the
  *                      second slice's first two rows loaded while the first slice finishes (software
  *                      pipelining across the exchange barrier; no persistent grid)
+ *   [DIAG] "units"            single-tile maps on the default non-temporal shape: (stripe, chunk) units per
+ *                      workgroup with one load ring running across them, so a unit's stores leave
+ *                      while the next unit's loads are in flight (k_gf_apply_multi): 1 = one unit per
+ *                      workgroup (default), 2 or 4; measured 3-16 % slower on every single-tile map
+ *                      (profiles/r05_units_ab.jsonl)
  *   [DIAG] "rtc_persist"      the plane-group kernel's grid: 0 = one workgroup per unit (default), 1..8 =
  *                      a persistent grid of that many workgroups per CU walking the units
  */

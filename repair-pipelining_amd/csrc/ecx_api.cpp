@@ -1177,7 +1177,7 @@ bool diagnostic_builds_allowed() {
 // the diagnostic library only (`make DIAG=1`, libecx_diag.so).
 bool lab_key(const std::string &k) {
     return k == "bitslice" || k == "lds_lut" || k == "wave_groups" || k == "rtc_units" || k == "rtc_persist" ||
-           k == "rtc_diag" || k == "occ_lds";
+           k == "rtc_diag" || k == "occ_lds" || k == "units";
 }
 
 // Deployment knobs (host pipeline, per-call plan cache, markers, the layout selection's on/off):

@@ -400,7 +400,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     }
     // Several units per workgroup with one ring across them (k_gf_apply_multi, ecx_tune "units"):
     // single-tile maps on the default NT shape, rings of 4 / 8 (and 20 on 256 threads)
-    const bool multi = tu.units > 1 && cm.n_tiles() == 1 && !waves && !wide && !bits && !lut && !planes && !skew &&
+    [[maybe_unused]] const bool multi = ECX_DIAG && tu.units > 1 && cm.n_tiles() == 1 && !waves && !wide && !bits && !lut && !planes && !skew &&
                        rows == kTileRows && ntmode == 2 && nts == 1 && tu.lds_tables != 2 &&
                        (depth == 4 || depth == 8 || (depth == 20 && threads == kBlockThreads));
     const DevicePlan &plan = cm.plan_for_current_device(depth);
@@ -494,12 +494,14 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
                 }
                 continue;
             }
-            if (multi && !safe) {
+#if ECX_DIAG
+            if (multi && !safe) {  // measured slower on every single-tile map: DESIGN.md section 4.5
                 a.multi_total = ns * per_stripe;
                 launch_multi(tu.units, depth, threads, tail_launch,
                              dim3((unsigned)((a.multi_total + tu.units - 1) / tu.units)), stream, a);
                 continue;
             }
+#endif
             Shape s;
             s.safe = safe;
             s.ntl = ntmode == 2;

@@ -21,7 +21,7 @@ if has diag; then
   # the measured-and-rejected kernels, in the diagnostic library (make DIAG=1): the tests marked
   # `diag` and the lab variants of the mixed tests
   ECX_LIB_PATH="$ROOT/repair-pipelining_amd/libecx_diag.so" timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf \
-      --timeout 120 --timeout-method thread -k "diag or bitslice or lds_lut or multitile_launch or random_maps or clay_rtc_kernel or two_slice or skew_chunks or stagger_unit" \
+      --timeout 120 --timeout-method thread -k "diag or bitslice or lds_lut or multitile_launch or random_maps or clay_rtc_kernel or two_slice or skew_chunks or stagger_unit or multi_unit" \
       > "$OUT/pytest_gpu_diag.log" 2>&1
   rc=$?; echo "pytest gpu diag rc=$rc"; tail -3 "$OUT/pytest_gpu_diag.log"; [ $rc -ne 0 ] && stop pytest_diag $rc
 fi

@@ -153,21 +153,21 @@ def test_tuning_keys(ecx):
     header = (ROOT / "include" / "ecx_tune.h").read_text()
     documented = re.findall(r'^ \*\s+"([a-z_]+)"', header, flags=re.M)
     lab = re.findall(r'^ \*\s+\[DIAG\] "([a-z_]+)"', header, flags=re.M)
-    assert sorted(lab) == sorted(["wave_groups", "occ_lds", "bitslice", "lds_lut", "rtc_diag", "rtc_units", "rtc_persist"])
+    assert sorted(lab) == sorted(["wave_groups", "occ_lds", "bitslice", "lds_lut", "rtc_diag", "rtc_units", "rtc_persist",
+                                  "units"])
     for key in lab:  # the product library refuses them; the diagnostic one takes its defaults
-        assert tune(key.encode(), 1 if key == "rtc_units" else 0) == (0 if ecx.is_diag() else -1), key
+        assert tune(key.encode(), 1 if key in ("rtc_units", "units") else 0) == (0 if ecx.is_diag() else -1), key
     defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0,
                 "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_sched": 2, "rtc_nt": 5, "xcd_run": 8, "xcd_misaligned": 1,
                 "map_planes": 1, "planes_lookahead": 12, "planes_waves": 2,
-                "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512, "host_exec_kib": 8,
-                "units": 1}
+                "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512, "host_exec_kib": 8}
     assert sorted(documented) == sorted(defaults)
     integration = (ROOT / "INTEGRATION.md").read_text()
     assert all("`%s`" % k in integration for k in documented), "INTEGRATION.md must list every tuning key"
     for key, val in defaults.items():
         assert tune(key.encode(), val) == 0, key
     assert tune(b"no_such_knob", 1) == -1
-    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("xcd_misaligned", 2), ("stagger", -1), ("stagger", 65), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("layout_select", 2), ("plan_cache", -1), ("bitslice", 3), ("lds_lut", 3), ("lds_lut", -1), ("roctx", 2), ("host_contexts", 2), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("rtc_units", 0), ("rtc_units", 3), ("rtc_sched", 3), ("rtc_nt", -1), ("rtc_nt", 16), ("occ_lds", -2), ("occ_lds", 65537), ("rtc_diag", 1), ("rtc_diag", 32), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5), ("host_exec_kib", -1), ("units", 3), ("units", 0)):
+    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("xcd_misaligned", 2), ("stagger", -1), ("stagger", 65), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("layout_select", 2), ("plan_cache", -1), ("bitslice", 3), ("lds_lut", 3), ("lds_lut", -1), ("roctx", 2), ("host_contexts", 2), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("rtc_units", 0), ("rtc_units", 3), ("rtc_sched", 3), ("rtc_nt", -1), ("rtc_nt", 16), ("occ_lds", -2), ("occ_lds", 65537), ("rtc_diag", 1), ("rtc_diag", 32), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5), ("host_exec_kib", -1)):
         assert tune(key.encode(), bad) == -1, key
     for key, val in defaults.items():  # restore
         tune(key.encode(), val)

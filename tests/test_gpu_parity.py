@@ -2206,6 +2206,7 @@ def test_layout_selection_two_streams(ecx, torch_dev):
             assert all((ref[i] == host[i]).all() for i in range(k, 16)), s
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("units", [2, 4])
 def test_multi_unit_workgroups_match(ecx, torch_dev, units):
     """k_gf_apply_multi (ecx_tune "units": several (stripe, chunk) units per workgroup, one load
