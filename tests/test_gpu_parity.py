@@ -2275,3 +2275,33 @@ def test_multi_unit_workgroups_match(ecx, torch_dev, units):
         assert torch.equal(ref, got) and not torch.equal(got, acc0)
     finally:
         ecx.tune("block_threads", 0)
+
+
+def test_layout_selection_revalidates_once(ecx, torch_dev):
+    """A layout's kept shape is re-validated once, after 512 further launches (kLayoutRevalidate):
+    the state goes exploring -> chosen -> re-validated (3) with nothing dropped on one stream, the
+    choice is still a candidate, and every launch wrote the oracle's bytes."""
+    import oracle as O
+    torch = torch_dev
+    k, m, L, S = 12, 4, 1 << 20, 24  # 288 MiB of input per launch: selected per layout
+    rs = ecx.ReedSolomon.create(k, m)
+    pool = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 401)
+    rs.encode_map().apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L)
+    dmap = rs.decode_map([True] * 5 + [False] + [True] * 10)
+    out = torch.empty((S, 1, L), dtype=torch.uint8, device="cuda")
+    states = set()
+    for i in range(640):
+        dmap.apply_batch(pool, 16 * L, L, out, L, L, S, L)
+        torch.cuda.synchronize()
+        if i % 16 == 0:
+            states.add(dmap.layout_state(L)[0])
+    state, dropped = dmap.layout_state(L)
+    assert state == 3 and dropped == 0, (state, dropped, states)
+    assert 1 in states or 2 in states, states
+    assert dmap.layout_choice(L) != -1
+    assert torch.equal(out[:, 0], pool[:, 5])
+    host = pool[S - 1].cpu().numpy()
+    shards = [host[i].copy() if i != 5 else np.zeros(L, np.uint8) for i in range(16)]
+    O.ReedSolomon(k, m).decode_missing(shards, [i != 5 for i in range(16)], 0, L)
+    assert (shards[5] == out[S - 1, 0].cpu().numpy()).all()
