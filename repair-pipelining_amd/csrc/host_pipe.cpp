@@ -129,10 +129,16 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     const std::vector<int> &ins = cm.used_in_slots(), &outs = cm.used_out_slots();
     const int64_t in_per = (int64_t)ins.size() * nbytes, out_per = (int64_t)outs.size() * nbytes;
     const Tuning &t = tuning();
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, t.host_chunk / std::max<int64_t>(1, in_per)));
+    const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes), rout = runs_of(outs, out_slot_stride, nbytes);
+    // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a stripe's used
+    // slots fall into many runs (shortened Clay(10,4): 128 runs of 3-10 sub-chunks), so each strided
+    // copy moves whole rows of many stripes instead of a few KiB per call -- within 8x host_chunk.
+    constexpr int64_t kMinRows = 64;
+    int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
+    if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
+    chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
     const int64_t nchunks = (nstripes + chunk - 1) / chunk;
     const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
-    const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes), rout = runs_of(outs, out_slot_stride, nbytes);
 
     HostPipe &p = HostPipe::current();
     std::lock_guard<std::mutex> lk(p.mu);

@@ -746,7 +746,7 @@ def test_map_host_batch_devices_and_refusals(ecx, small_host_chunks):
 
 @pytest.mark.parametrize("k,m,L,off,S", [(17, 3, 200000, 0, 6), (4, 2, 104449, 0, 5), (4, 2, 4096 * 3, 16, 4),
                                          (10, 10, 8192 + 48, 0, 3), (5, 5, 1001, 3, 4), (17, 3, 4096, 0, 3),
-                                         (2, 1, 16, 0, 2)])
+                                         (2, 1, 16, 0, 2), (64, 64, 4096 + 16, 0, 2), (12, 4, 3 * 4096, 0, 9)])
 def test_is_parity_correct_batch_vs_oracle(ecx, torch_dev, k, m, L, off, S):
     """isParityCorrectBatch (k_gf_check, read-only): valid stripes pass; one flipped byte --
     in a data shard at byte 0, in a parity shard inside the partial last chunk, at the last
