@@ -646,8 +646,9 @@ def test_partial_sum_batches(ecx, torch_dev):
 # ---------------------------------------------------------------- host-memory batches
 @pytest.fixture
 def small_host_chunks(ecx):
-    """Force many pipelined chunks and ring reuse; restore the defaults afterwards."""
-    ecx.tune("host_chunk_kib", 96)
+    """Force many pipelined chunks and ring reuse (one stripe per chunk on these layouts, even with
+    the many-run rule of host_pipe.cpp); restore the defaults afterwards."""
+    ecx.tune("host_chunk_kib", 16)
     ecx.tune("host_buffers", 3)
     yield
     ecx.tune("host_chunk_kib", 65536)
