@@ -2290,10 +2290,10 @@ def test_layout_selection_revalidates_once(ecx, torch_dev):
     ecx.fill_random(pool, pool.numel(), 401)
     rs.encode_map().apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L)
     dmap = rs.decode_map([True] * 5 + [False] + [True] * 10)
-    out = torch.empty((S, 1, L), dtype=torch.uint8, device="cuda")
+    out = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")  # the map writes output slot 5
     states = set()
     for i in range(640):
-        dmap.apply_batch(pool, 16 * L, L, out, L, L, S, L)
+        dmap.apply_batch(pool, 16 * L, L, out, 16 * L, L, S, L)
         torch.cuda.synchronize()
         if i % 16 == 0:
             states.add(dmap.layout_state(L)[0])
@@ -2301,8 +2301,8 @@ def test_layout_selection_revalidates_once(ecx, torch_dev):
     assert state == 3 and dropped == 0, (state, dropped, states)
     assert 1 in states or 2 in states, states
     assert dmap.layout_choice(L) != -1
-    assert torch.equal(out[:, 0], pool[:, 5])
+    assert torch.equal(out[:, 5], pool[:, 5])
     host = pool[S - 1].cpu().numpy()
     shards = [host[i].copy() if i != 5 else np.zeros(L, np.uint8) for i in range(16)]
     O.ReedSolomon(k, m).decode_missing(shards, [i != 5 for i in range(16)], 0, L)
-    assert (shards[5] == out[S - 1, 0].cpu().numpy()).all()
+    assert (shards[5] == out[S - 1, 5].cpu().numpy()).all()
