@@ -39,7 +39,7 @@ contract (same launch, timing and JSON line; the default is the headline):
   rs173check the same benchmark's other half (ReedSolomonBenchmark.java:73-87,126-149): RS(17,3)
            isParityCorrect over the encoded pool, read-only, one verdict byte per stripe; MB/s of
            data bytes checked (no published figure)
-Every workload carries a cpu_baseline (rank 0, after the timed region, at any N): the
+Every workload's N=1 line carries a cpu_baseline (rank 0, after the timed region): the
 oracle's restatement of the reference path for that workload on this host's cores.
 """
 import argparse
@@ -1182,13 +1182,13 @@ def main():
                        per_rank_GiBps=[round(r, 3) for r in rates])
 
     sample = units = None
-    if rank == 0 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the contract: rank 0 at N=1 only
         sample = wl.sample()  # one pool unit for the oracle check
         units = wl.host_units(8 if wl.unit_bytes < (64 << 20) else 2)  # the GPU run's own stripes
     probes = memory_probes(ecx, torch, wl.region, wl.reads, wl.writes) if not args.no_probes else None
 
     cpu = None
-    if sample is not None:  # rank 0 only, after the timed region (at any N)
+    if sample is not None:  # rank 0 at N=1 only, after the timed region
         cpu = cpu_baseline(wl, args.cpu_seconds, sample, units=units, protocol=args.cpu_protocol)
         if wl.metric_unit != "GiB/s":  # the line's own unit: metric bytes per metric_scale
             f = 2**30 / wl.metric_scale * metric_bytes / wl.unit_bytes
