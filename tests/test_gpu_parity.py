@@ -2306,3 +2306,142 @@ def test_layout_selection_revalidates_once(ecx, torch_dev):
     shards = [host[i].copy() if i != 5 else np.zeros(L, np.uint8) for i in range(16)]
     O.ReedSolomon(k, m).decode_missing(shards, [i != 5 for i in range(16)], 0, L)
     assert (shards[5] == out[S - 1, 5].cpu().numpy()).all()
+
+
+@pytest.mark.host_exec
+def test_every_entry_kind_at_once(ecx, torch_dev):
+    """Every kind of entry point from its own host thread at the same time, as one JVM's pub/sub
+    threads would drive them: per-call calls on both sides of the host-executor threshold
+    (2,174-B and 4 KiB calls on the calling thread, 32 KiB calls on the device), device batches on
+    their own streams (RS(17,3) encodeParity then isParityCorrect on the published shape, LRC
+    encode), and a host-memory Clay(4,2) batch split over the device list [0, 0].  Each thread
+    checks its own results (the oracle's, or the verdicts the encode implies) on every iteration."""
+    import threading
+    torch = torch_dev
+    ecx.tune("host_exec_kib", 8)
+    rng = np.random.default_rng(2024)
+    errors = []
+
+    # per-call RS(4,2): 2,174 B and 4 KiB on the host executor, 32 KiB on the device
+    rs_cases = {}
+    for L in (2174, 4096, 32768):
+        base = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(6)]
+        ref = [b.copy() for b in base]
+        O.ReedSolomon(4, 2).encode_parity(ref, 0, L)
+        rs_cases[L] = (base, ref)
+    # per-call Clay(4,2) repair of node 1, 4 KiB sub-chunks (host executor) and 32 KiB (device)
+    clay_cases = {}
+    for B in (4096, 32768):
+        inputs = [None if i % 6 == 1 else rng.integers(0, 256, B, dtype=np.uint8) for i in range(48)]
+        ref = [np.zeros(B, np.uint8) for _ in range(8)]
+        O.Clay(4, 2, [1]).perform_coding(inputs, ref, B)
+        clay_cases[B] = (inputs, ref)
+    # host-memory Clay(4,2) batch, 37 stripes of 8 KiB sub-chunks, split over [0, 0]
+    S_h, B_h = 37, 8192
+    hin = rng.integers(0, 256, (S_h, 48, B_h), dtype=np.uint8)
+    step_h = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    href = np.zeros((S_h, 8, B_h), np.uint8)
+    step_h.performCodingBatchHost(hin, 48 * B_h, B_h, href, 8 * B_h, B_h, S_h, B_h)  # one device, before the threads
+    for s in (0, S_h - 1):
+        o = [np.zeros(B_h, np.uint8) for _ in range(8)]
+        O.Clay(4, 2, [1]).perform_coding([None if i % 6 == 1 else hin[s, i].copy() for i in range(48)], o, B_h)
+        assert all((href[s, z] == o[z]).all() for z in range(8))
+
+    def guarded(fn):
+        def run():
+            try:
+                fn()
+            except Exception as exc:  # noqa: BLE001 -- reported below
+                errors.append((fn.__name__, repr(exc)))
+        return run
+
+    def per_call_rs():
+        rs = ecx.ReedSolomon.create(4, 2)
+        for it in range(24):
+            L = (2174, 4096, 32768)[it % 3]
+            base, ref = rs_cases[L]
+            sh = [b.copy() for b in base]
+            rs.encodeParity(sh, 0, L)
+            if not all((sh[i] == ref[i]).all() for i in range(6)):
+                errors.append(("rs encode", it, L))
+            present = [True] * 6
+            present[it % 4] = False
+            sh[it % 4][:] = 0
+            rs.decodeMissing(sh, present, 0, L)
+            if not (sh[it % 4] == ref[it % 4]).all():
+                errors.append(("rs decode", it, L))
+
+    def per_call_clay():
+        step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+        for it in range(16):
+            B = (4096, 32768)[it % 2]
+            inputs, ref = clay_cases[B]
+            got = [np.zeros(B, np.uint8) for _ in range(8)]
+            step.performCoding(inputs, got, B)
+            if not all((got[z] == ref[z]).all() for z in range(8)):
+                errors.append(("clay", it, B))
+
+    def rs173_batches():
+        S, L = 96, 200000
+        st = torch.cuda.Stream()
+        rs = ecx.ReedSolomon.create(17, 3)
+        with torch.cuda.stream(st):
+            pool = torch.empty((S, 20, L), dtype=torch.uint8, device="cuda")
+            verdict = torch.empty(S, dtype=torch.uint8, device="cuda")
+        ecx.fill_random(pool, pool.numel(), 77, stream=st)
+        for it in range(12):
+            rs.encodeParityBatch(pool, 20 * L, L, S, 0, L, stream=st)
+            rs.isParityCorrectBatch(pool, 20 * L, L, S, 0, L, verdict, stream=st)
+            st.synchronize()
+            if int(verdict.sum()) != S:
+                errors.append(("rs173 verdict after encode", it, int(verdict.sum())))
+            s = it % S
+            with torch.cuda.stream(st):
+                pool[s, it % 20, (it * 7919) % L] ^= 0x5A  # one flipped byte: exactly that stripe fails
+            rs.isParityCorrectBatch(pool, 20 * L, L, S, 0, L, verdict, stream=st)
+            st.synchronize()
+            bad = torch.nonzero(verdict == 0).flatten().tolist()
+            if bad != [s]:
+                errors.append(("rs173 flipped", it, bad[:4]))
+        h = pool[S - 1].cpu().numpy()
+        sh = [h[i].copy() for i in range(20)]
+        for i in range(17, 20):
+            sh[i][:] = 0
+        O.ReedSolomon(17, 3).encode_parity(sh, 0, L)
+        if not all((sh[i] == h[i]).all() for i in range(17, 20)):
+            errors.append(("rs173 oracle",))
+
+    def lrc_batches():
+        S, B = 64, 65536
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            pool = torch.empty((S, 16, B), dtype=torch.uint8, device="cuda")
+        ecx.fill_random(pool, pool.numel(), 78, stream=st)
+        for it in range(12):
+            ecx.LRCErasureCode.encodeBatch(pool, 16 * B, B, S, B, stream=st)
+        st.synchronize()
+        h = pool[S // 2].cpu().numpy()
+        for g in range(4):  # group g: blocks 4g..4g+2 and their XOR parity 4g+3
+            want = h[4 * g] ^ h[4 * g + 1] ^ h[4 * g + 2]
+            if not (h[4 * g + 3] == want).all():
+                errors.append(("lrc group", g))
+
+    def host_devices():
+        step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+        for it in range(6):
+            out = np.zeros((S_h, 8, B_h), np.uint8)
+            step.performCodingBatchHostDevices(hin, 48 * B_h, B_h, out, 8 * B_h, B_h, S_h, B_h, [0, 0])
+            if not (out == href).all():
+                errors.append(("host devices", it))
+
+    threads = [threading.Thread(target=guarded(f))
+               for f in (per_call_rs, per_call_rs, per_call_clay, rs173_batches, lrc_batches, host_devices)]
+    try:
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=100)
+    finally:
+        ecx.tune("host_exec_kib", 0)
+    assert not any(t.is_alive() for t in threads), "a worker thread hung"
+    assert not errors, errors[:6]
