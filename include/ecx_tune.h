@@ -124,7 +124,8 @@
  *   "host_exec_kib"    per-call host entry points (the CodingLoop / ReedSolomon / Clay byte[][] calls):
  *                      byte counts up to this many KiB run on the calling thread (host_exec.cpp:
  *                      AVX-512 GFNI affine multiplies, else AVX2 nibble tables) instead of a device
- *                      round trip -- below the measured per-call crossover (default 8; 0 = every
+ *                      round trip (default 8, a policy: on one core the executor beat the device at
+ *                      every size measured, profiles/r05_percall_threshold.jsonl; 0 = every
  *                      call on the device).  Never a fallback: without a HIP device these calls
  *                      fail with ECX_E_DEVICE like the device path
  *   "host_zero_copy"   per-call host entry points on the gather path: 1 = the kernel reads and

@@ -1,13 +1,13 @@
-// host_exec.cpp -- the per-call executor below the CPU/GPU crossover (SURVEY.md 8(b) group 1).
+// host_exec.cpp -- the per-call executor below the CPU/GPU size threshold (SURVEY.md 8(b) group 1).
 //
 // The reference's drop-in sites call the codec at fine grain: one encodeParitySingle per 34-B
 // word (NodeHelper.kt:89, 1,024 calls per block), one RS(2,2) decodeMissing per Clay sub-chunk
 // pair of 2,174 B (ClayCodeNode.kt:125-132, ClayCodeHelper.kt:90).  A call that small is all
 // latency on the GPU -- staging, a launch and a synchronise, 19-52 us -- against well under a
-// microsecond of arithmetic, so per-call entry points whose byte count is at most the measured
-// crossover (ecx_tune "host_exec_kib", profiles/r05_percall_threshold.jsonl) apply the map
-// here, on the calling thread; everything at or above it, and every batch entry point, runs
-// the HIP kernels.  It is not a fallback: with no HIP device the call fails (ECX_E_DEVICE) as
+// microsecond of arithmetic, so per-call entry points whose byte count is at most the
+// threshold (ecx_tune "host_exec_kib", default 8 KiB; profiles/r05_percall_threshold.jsonl)
+// apply the map here, on the calling thread; everything above it, and every batch entry
+// point, runs the HIP kernels.  It is not a fallback: with no HIP device the call fails (ECX_E_DEVICE) as
 // the GPU path would, and "host_exec_kib" 0 sends every call to the device.
 //
 // Arithmetic: c * x over GF(2^8) (0x11D) is linear over GF(2), so it is one GF2P8AFFINEQB with
