@@ -30,8 +30,7 @@
  *                      and row); 1 = the low dword of each 8-entry table staged per workgroup
  *                      in LDS, for multi-tile maps (default); 2 = for every map
  *   "store_scope"      0 = non-temporal output stores (`nt`, default); 1 = `nt sc0 sc1`
- *                      (system scope: written through, dropped from L2); [DIAG] 2 = write-back
- *                      stores behind non-temporal loads (single-tile maps, depth 8 / 20)
+ *                      (system scope: written through, dropped from L2)
  *   "chunk_major"      block order of the one-workgroup-per-tile kernel: 0 = stripe-major
  *                      (default), 1 = chunk-major (chunk c of every stripe, then chunk c + 1)
  *   "stagger"          unit order of the single-tile kernels (k_gf_apply, k_gf_apply_skew): 0 = none

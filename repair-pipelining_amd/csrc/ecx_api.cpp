@@ -1228,7 +1228,7 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.wave_groups = value;
     }
-    else if (k == "store_scope") t.store_scope = ECX_DIAG && value == 2 ? 2 : value != 0;
+    else if (k == "store_scope") t.store_scope = value != 0;
     else if (k == "occ_lds") {
         if (value < -1 || value > 65536) return ECX_E_ILLEGAL_ARGUMENT;
         t.occ_lds = value;

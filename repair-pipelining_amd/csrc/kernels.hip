@@ -278,10 +278,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     const bool waves = ECX_DIAG && cm.n_tiles() > 1 && cm.n_groups() > 0 && tu.wave_groups;
     // Non-temporal policy: 0 never; 1 auto (NT stores, NT loads for single-tile maps); 2 always.
     const int ntmode = tu.nontemporal == 2 ? 2 : (tu.nontemporal == 1 ? (cm.n_tiles() == 1 ? 2 : 1) : 0);
-    // store_scope 2 (diagnostic build): write-back stores behind non-temporal loads
-    const bool wb_stores = ECX_DIAG && tu.store_scope == 2 && ntmode == 2;
-    const int nts = ntmode == 0 || wb_stores ? 0 : (tu.store_scope ? 2 : 1);
-    const int nts_ok = wb_stores ? 0 : 1;  // the store policy the deep-ring and tail instances exist for
+    const int nts = ntmode == 0 ? 0 : (tu.store_scope ? 2 : 1);
     // Launch shapes that exist (apply_launch.inc); anything else is clamped here.
     // Workgroup size: 256 threads over 4 KiB chunks; one wave over 1 KiB chunks when forced
     // (64) or, in auto (0), for single-tile maps of <= 2 rows over >= 8 inputs whose slot
@@ -304,7 +301,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     // profiles/r02_small_tiles_ab.jsonl).
     const bool small = tu.small_tiles == 1 ||
                        (tu.small_tiles == 2 && cm.max_tile_rows() <= 2 && cm.map().n_in <= 4 && cm.n_tiles() == 1);
-    if (small && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1 && !wb_stores)
+    if (small && !waves && threads == kBlockThreads && ntmode == 2 && nts == 1)
         rows = cm.max_tile_rows() <= 2 ? 2 : (cm.max_tile_rows() <= 4 ? 4 : kTileRows);
     int depth = tu.depth ? tu.depth : cm.preferred_depth();
     if (rows < kTileRows) {
@@ -313,7 +310,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
         if (depth == 2 && (waves || threads != kBlockThreads || nts != 1)) depth = 4;
         // deep rings (10-24) exist for single-tile maps with NT loads and stores and SGPR tables
         if (depth > 8 && (cm.n_tiles() != 1 || threads != kBlockThreads || ntmode != 2 ||
-                          (nts != nts_ok && !(nts == 2 && depth == 20)) ||
+                          (nts != 1 && !(nts == 2 && depth == 20)) ||
                           tu.lds_tables == 2))
             depth = 8;
     }
@@ -570,7 +567,7 @@ void launch_apply_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_str
     // launch of its own.
     const int64_t tail_len = nbytes - full * chunk;
     const bool fuse_tail = aligned && full >= 1 && tail_len > 0 && tail_len % 16 == 0 && (depth == 4 || depth == 8) &&
-                           cm.n_tiles() == 1 && rows == kTileRows && ntmode == 2 && nts == nts_ok && tu.lds_tables != 2 &&
+                           cm.n_tiles() == 1 && rows == kTileRows && ntmode == 2 && nts == 1 && tu.lds_tables != 2 &&
                            !waves && !wide && !bits && !lut && outputs_never_read(cm.map(), in, in_stripe_stride, in_slot_stride, out,
                                                       out_stripe_stride, out_slot_stride, nstripes, nbytes);
     if (fuse_tail) {
