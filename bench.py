@@ -89,7 +89,7 @@ PUBLISHED = {"rs173": 525.7}  # MB/s, RS(17,3) encodeParity, InputOutputByteTabl
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=8)  # 8 x 32 headline launches: >= 1 s timed
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="clay42", choices=list(WORKLOADS))
     ap.add_argument("--stripes-per-step", type=int, default=None, help="default: per workload (2^20 for clay42)")
