@@ -808,7 +808,18 @@ class RS173Check(RS173):
     def selected_map(self):
         return None
 
-    host_ok = False  # the check's host form is the per-call isParityCorrect (ecx_rs_is_parity_correct)
+    def host_out_bytes(self):
+        return 1  # one verdict byte per stripe comes back
+
+    def host_call(self, hin, hout, n):  # pipelined H2D of the 20 shards, the check, the verdicts D2H
+        self.rs.isParityCorrectBatchHost(hin, 20 * self.L, self.L, n, 0, self.L, hout)
+
+    def host_expect(self, hin, hout, n):
+        """Every host stripe (a copy of the valid pool) passes, as the device check says."""
+        return bool((hout[:n] == 1).all()) and bool((self.verdict[:n] == 1).all())
+
+    def pcie_bytes(self):
+        return 20 * self.L, 1
 
     def verify(self):
         """Every stripe passes; a flipped byte in a data shard (stripe 1, byte 0), in a parity

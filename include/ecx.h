@@ -273,6 +273,19 @@ int ecx_clay_perform_coding_batch_host_devices(ecx_clay *clay, const uint8_t *in
                                                int64_t in_sub_stride, uint8_t *out, int64_t out_stripe_stride,
                                                int64_t out_sub_stride, int64_t nstripes, int64_t buf_size,
                                                const int *devices, int ndev);
+/* ReedSolomon.isParityCorrect (ReedSolomon.java:129-178) over nstripes HOST-memory stripes
+ * (the layout of ecx_rs_is_parity_correct_batch, host pointers): each chunk of stripes goes
+ * H2D and through the read-only check kernel, and only the verdict bytes come back --
+ * verdict[s] (a host byte array of nstripes) = 1 when stripe s's parity is correct over bytes
+ * [offset, offset + byte_count), else 0.  Synchronous; the _devices form splits the stripes
+ * over a device list exactly as ecx_map_apply_batch_host_devices does. */
+int ecx_rs_is_parity_correct_batch_host(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride,
+                                        int64_t shard_stride, int64_t nstripes, int64_t offset,
+                                        int64_t byte_count, uint8_t *verdict);
+int ecx_rs_is_parity_correct_batch_host_devices(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride,
+                                                int64_t shard_stride, int64_t nstripes, int64_t offset,
+                                                int64_t byte_count, uint8_t *verdict, const int *devices,
+                                                int ndev);
 /* Page-locked host memory for the calls above (e.g. backing direct ByteBuffers). */
 int ecx_host_alloc(int64_t nbytes, void **out);
 int ecx_host_free(void *ptr);

@@ -153,6 +153,7 @@ RULES = {
     "ecx_lrc_decode_batch": ((), [A("block_present", "16")]),
     "ecx_map_apply_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
     "ecx_clay_perform_coding_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
+    "ecx_rs_is_parity_correct_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
 }
 
 
@@ -170,9 +171,16 @@ BUFFER_VARIANTS = {
                                            "        if (st == ECX_OK) st = ecx_map_slot_extent(cm, &max_in, &max_out);\n"
                                            "    }", "cl_ne > 0"),
 }
+# The host check batch: the stripes (every shard read, max slot n - 1, bytes up to offset +
+# byte_count) and a verdict buffer of one byte per stripe.
+BUFFER_VARIANTS["ecx_rs_is_parity_correct_batch_host"] = ("rs", "    max_in = rs_k + rs_m - 1;", None)
 # the multi-GPU forms take the same buffers, extents and conditions
 BUFFER_VARIANTS["ecx_map_apply_batch_host_devices"] = BUFFER_VARIANTS["ecx_map_apply_batch_host"]
 BUFFER_VARIANTS["ecx_clay_perform_coding_batch_host_devices"] = BUFFER_VARIANTS["ecx_clay_perform_coding_batch_host"]
+BUFFER_VARIANTS["ecx_rs_is_parity_correct_batch_host_devices"] = BUFFER_VARIANTS["ecx_rs_is_parity_correct_batch_host"]
+# buffers laid out other than (stripe stride, slot stride) after the address: param -> (stripe
+# stride, slot stride, max slot, bytes per slot), as C expressions
+BUFFER_SHAPES = {"verdict": ("1", "0", "0", "1")}
 
 
 def host_address_native(name):
@@ -188,6 +196,10 @@ def buffer_variant(ret, name, params):
     names = [p for _, p in params]
     handle = names[0]
     length = next(p for p in reversed(names) if p in ("byte_count", "buf_size"))
+    negative = "nstripes < 0 || %s < 0" % length
+    if "offset" in names:  # a window [offset, offset + byte_count) of every slot
+        negative += " || offset < 0"
+        length = "(int64_t)offset + %s" % length
     jparams, cparams, args, bufs, ints = [], ["JNIEnv *env", "jclass cls"], [], [], []
     for i, (t, p) in enumerate(params):
         kind = classify(name, t, p)[0]
@@ -203,7 +215,10 @@ def buffer_variant(ret, name, params):
         elif kind == "addr":
             jparams.append("ByteBuffer %s" % camel("ecx_" + p))
             cparams.append("jobject %s" % p)
-            bufs.append((p, names[i + 1], names[i + 2]))
+            if p in BUFFER_SHAPES:
+                bufs.append((p,) + BUFFER_SHAPES[p])
+            else:  # (stripe stride, slot stride) follow; the map's slots; the batch's bytes per slot
+                bufs.append((p, names[i + 1], names[i + 2], "max_in" if p in ("in", "base") else "max_out", length))
             args.append("(%s)%s_p" % (t.strip(), p))
         elif kind == "handle":
             jparams.append("long %s" % camel("ecx_" + p))
@@ -214,14 +229,14 @@ def buffer_variant(ret, name, params):
             cparams.append("jlong %s" % p)
             args.append("(int64_t)%s" % p)
     body = ["    (void)cls;", "    jint st = ECX_OK;", "    if (!%s) st = ECX_E_NULL;" % handle,
-            "    if (st == ECX_OK && (nstripes < 0 || %s < 0)) st = ECX_E_ILLEGAL_ARGUMENT;" % length,
-            QUERIES[query], "    int max_in = -1, max_out = -1;", extent]
-    for p, _, _ in bufs:
-        body.append("    uint8_t *%s_p = NULL;" % p)
+            "    if (st == ECX_OK && (%s)) st = ECX_E_ILLEGAL_ARGUMENT;" % negative,
+            QUERIES[query], "    int max_in = -1, max_out = -1;", extent, "    (void)max_in;", "    (void)max_out;"]
+    for b in bufs:
+        body.append("    uint8_t *%s_p = NULL;" % b[0])
     cond = "st == ECX_OK" + (" && (%s)" % when if when else "")
-    for p, ss, sl in bufs:
+    for p, ss, sl, ms, nb in bufs:
         body.append("    if (%s) st = direct_check(env, %s, %s, %s, %s, nstripes, %s, &%s_p);"
-                    % (cond, p, ss, sl, "max_in" if p == "in" else "max_out", length, p))
+                    % (cond, p, ss, sl, ms, nb, p))
     for p, cnt in ints:
         body.append("    int *%s_c = NULL;" % p)
         body.append("    if (st == ECX_OK && %s < 0) st = ECX_E_ILLEGAL_ARGUMENT;" % cnt)
@@ -238,7 +253,7 @@ def buffer_variant(ret, name, params):
          "JNIEXPORT jint JNICALL Java_%s_%s(%s) {\n%s\n}\n"
          % (name, JCLASS, jname, ", ".join(cparams), "\n".join(body)))
     java = ("\n    /** %s over direct ByteBuffers: the forwarder checks each buffer's capacity against the\n"
-            "     *  batch extent (ecx_map_slot_extent) and refuses heap buffers (NullPointerException). */\n"
+            "     *  batch extent and refuses heap buffers (NullPointerException). */\n"
             "    public static native int %s(%s);\n" % (name, jname, ", ".join(jparams)))
     return c, java
 

@@ -600,6 +600,31 @@ class ReedSolomon:
         check(lib().ecx_rs_is_parity_correct_batch(self._h, _dev_ptr(shards), stripe_stride, shard_stride, nstripes,
                                                    firstByte, byteCount, _dev_ptr(verdict), _stream(stream)))
 
+    def isParityCorrectBatchHost(self, shards, stripe_stride, shard_stride, nstripes, firstByte, byteCount,
+                                 verdict) -> None:
+        """isParityCorrectBatch over HOST-memory stripes (ecx_rs_is_parity_correct_batch_host):
+        chunks of stripes are pipelined H2D through the read-only check kernel and only the
+        verdict bytes come back into the host uint8 array ``verdict`` (nstripes bytes)."""
+        _check_layout(shards, stripe_stride, shard_stride, self.getTotalShardCount() - 1, nstripes,
+                      firstByte + byteCount, "shards")
+        _check_layout(verdict, 1, 0, 0, nstripes, 1, "verdict")
+        check(lib().ecx_rs_is_parity_correct_batch_host(self._h, _host_ptr(shards), stripe_stride, shard_stride,
+                                                        nstripes, firstByte, byteCount, _host_ptr(verdict)))
+
+    def isParityCorrectBatchHostDevices(self, shards, stripe_stride, shard_stride, nstripes, firstByte, byteCount,
+                                        verdict, devices) -> None:
+        """isParityCorrectBatchHost split over several GPUs of this process
+        (ecx_rs_is_parity_correct_batch_host_devices): contiguous stripe ranges, one worker
+        thread and pipe per device entry."""
+        _check_layout(shards, stripe_stride, shard_stride, self.getTotalShardCount() - 1, nstripes,
+                      firstByte + byteCount, "shards")
+        _check_layout(verdict, 1, 0, 0, nstripes, 1, "verdict")
+        devs = list(devices)
+        arr = np.ascontiguousarray(devs + [0], np.int32)  # never a null list: an empty one is ndev 0
+        check(lib().ecx_rs_is_parity_correct_batch_host_devices(self._h, _host_ptr(shards), stripe_stride,
+                                                                shard_stride, nstripes, firstByte, byteCount,
+                                                                _host_ptr(verdict), arr.ctypes.data, len(devs)))
+
     def decodeMissingBatch(self, shards, shardPresent, stripe_stride, shard_stride, nstripes, offset, byteCount,
                            stream=None):
         """decodeMissing over nstripes device-resident stripes, in place (ecx_rs_decode_missing_batch)."""

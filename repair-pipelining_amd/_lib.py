@@ -126,6 +126,8 @@ SIGNATURES = {
     "ecx_clay_perform_coding_batch_host": (I, [P, P, I64, I64, P, I64, I64, I64, I64]),
     "ecx_map_apply_batch_host_devices": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P, I]),
     "ecx_clay_perform_coding_batch_host_devices": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P, I]),
+    "ecx_rs_is_parity_correct_batch_host": (I, [P, P, I64, I64, I64, I64, I64, P]),
+    "ecx_rs_is_parity_correct_batch_host_devices": (I, [P, P, I64, I64, I64, I64, I64, P, P, I]),
     "ecx_host_alloc": (I, [I64, ctypes.POINTER(P)]),
     "ecx_host_free": (I, [P]),
     "ecx_host_register": (I, [P, I64]),

@@ -16,6 +16,7 @@
 #include "clay_rtc.hpp"
 #include "map_rtc.hpp"
 #include "engine.hpp"
+#include "host_pipe.hpp"
 
 using namespace ecx;
 
@@ -1130,6 +1131,40 @@ int ecx_clay_perform_coding_batch_host_devices(ecx_clay *clay, const uint8_t *in
                                out_stripe_stride, out_sub_stride, nstripes, buf_size, devices, ndev);
         return ECX_OK;
     });
+}
+
+namespace {
+int rs_check_host(const char *fn, ecx_rs *rs, const uint8_t *base, int64_t stripe_stride, int64_t shard_stride,
+                  int64_t nstripes, int64_t offset, int64_t byte_count, uint8_t *verdict, const int *devices,
+                  int ndev, bool multi) {
+    return guarded(fn, [&]() -> int {
+        if (!rs) throw Error(ECX_E_NULL, "null codec");
+        if (nstripes < 0 || offset < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (stripe_stride < 0 || shard_stride < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative stride");
+        if (nstripes > 0 && (!base || !verdict)) throw Error(ECX_E_NULL, "null host pointer");
+        CompiledMap &cm = rs_check_map(rs)->cm;
+        const uint8_t *in = nstripes > 0 ? base + offset : base;
+        if (multi) run_host_check_batch_devices(cm, in, stripe_stride, shard_stride, nstripes, byte_count, verdict,
+                                                devices, ndev);
+        else run_host_check_batch(cm, in, stripe_stride, shard_stride, nstripes, byte_count, verdict);
+        return ECX_OK;
+    });
+}
+}  // namespace
+
+int ecx_rs_is_parity_correct_batch_host(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride,
+                                        int64_t shard_stride, int64_t nstripes, int64_t offset,
+                                        int64_t byte_count, uint8_t *verdict) {
+    return rs_check_host(__func__, rs, base, stripe_stride, shard_stride, nstripes, offset, byte_count, verdict,
+                         nullptr, 0, false);
+}
+
+int ecx_rs_is_parity_correct_batch_host_devices(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride,
+                                                int64_t shard_stride, int64_t nstripes, int64_t offset,
+                                                int64_t byte_count, uint8_t *verdict, const int *devices,
+                                                int ndev) {
+    return rs_check_host(__func__, rs, base, stripe_stride, shard_stride, nstripes, offset, byte_count, verdict,
+                         devices, ndev, true);
 }
 
 int ecx_host_alloc(int64_t nbytes, void **out) {

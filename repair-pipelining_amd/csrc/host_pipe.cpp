@@ -16,9 +16,10 @@
 // that are also consecutive in host memory are merged into one strided (2D)
 // copy per chunk.
 #include <algorithm>
+#include <cstring>
 #include <thread>
 
-#include "engine.hpp"
+#include "host_pipe.hpp"
 
 namespace ecx {
 namespace {
@@ -169,6 +170,57 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     }
 }
 
+void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                          int64_t nstripes, int64_t nbytes, uint8_t *verdict) {
+    if (nstripes <= 0) return;
+    if (!verdict) throw Error(ECX_E_NULL, "verdict buffer is null");
+    if (nbytes <= 0 || cm.map().n_out == 0) {  // nothing to compare: every stripe passes (as launch_check)
+        std::memset(verdict, 1, (size_t)nstripes);
+        return;
+    }
+    // The read-only twin of run_host_batch: the check map's used slots cross PCIe into a set's
+    // compact buffer, k_gf_check writes one verdict byte per stripe of the chunk into the set's
+    // output area, and only those bytes come back.
+    CompiledMap &cc = cm.compact();
+    const std::vector<int> &ins = cm.used_in_slots();
+    const int64_t in_per = (int64_t)ins.size() * nbytes;
+    const Tuning &t = tuning();
+    const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes);
+    constexpr int64_t kMinRows = 64;
+    int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
+    if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
+    chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
+    const int64_t nchunks = (nstripes + chunk - 1) / chunk;
+    const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
+
+    HostPipe &p = HostPipe::current();
+    std::lock_guard<std::mutex> lk(p.mu);
+    try {
+        p.ensure(nb, (size_t)(chunk * in_per), (size_t)chunk);
+        for (int64_t i = 0; i < nchunks; ++i) {
+            HostPipe::Set &b = p.sets[(size_t)(i % nb)];
+            const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
+            if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
+            for (const Run &r : rin)
+                copy_rows(b.in + r.compact0 * nbytes, in_per, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
+                          in_stripe_stride, r.len * nbytes, n, hipMemcpyHostToDevice, p.h2d);
+            check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
+            if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");
+            launch_check(cc, b.in, in_per, nbytes, b.out, n, nbytes, p.cmp);
+            check_hip(hipEventRecord(b.computed, p.cmp), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(p.d2h, b.computed, 0), "hipStreamWaitEvent");
+            check_hip(hipMemcpyAsync(verdict + lo, b.out, (size_t)n, hipMemcpyDeviceToHost, p.d2h),
+                      "hipMemcpyAsync (verdicts)");
+            check_hip(hipEventRecord(b.drained, p.d2h), "hipEventRecord");
+        }
+        check_hip(hipStreamSynchronize(p.d2h), "hipStreamSynchronize (host check batch)");
+    } catch (...) {
+        p.drain();
+        throw;
+    }
+}
+
 void stripe_range(int64_t nstripes, int parts, int j, int64_t *begin, int64_t *end) {
     // contiguous ranges, the remainder on the first ones (shard_stripes, __init__.py)
     const int64_t base = nstripes / parts, extra = nstripes % parts;
@@ -176,9 +228,13 @@ void stripe_range(int64_t nstripes, int parts, int j, int64_t *begin, int64_t *e
     *end = *begin + base + (j < extra ? 1 : 0);
 }
 
-void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
-                            uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
-                            int64_t nbytes, const int *devices, int ndev) {
+namespace {
+
+// One worker thread per device entry over contiguous stripe ranges; `range(lo, n)` runs on the
+// worker with its device current.  Bad ids are refused before any worker starts; the first
+// failing device's status is thrown after every worker has joined (each drains its own pipe).
+template <typename F>
+void on_devices(const int *devices, int ndev, int64_t nstripes, F &&range) {
     if (!devices) throw Error(ECX_E_NULL, "null device list");
     if (ndev <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "empty device list");
     int count = 0;
@@ -187,7 +243,7 @@ void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_strip
         if (devices[j] < 0 || devices[j] >= count)
             throw Error(ECX_E_ILLEGAL_ARGUMENT, "device " + std::to_string(devices[j]) + " of " +
                                                     std::to_string(count) + " visible");
-    if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
+    if (nstripes <= 0) return;
     struct Result {
         int code = ECX_OK;
         std::string what;
@@ -196,12 +252,10 @@ void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_strip
     auto work = [&](int j) {
         int64_t lo = 0, hi = 0;
         stripe_range(nstripes, ndev, j, &lo, &hi);
-        const int64_t n = hi - lo;
-        if (n <= 0) return;
+        if (hi <= lo) return;
         try {
             check_hip(hipSetDevice(devices[j]), "hipSetDevice (host batch worker)");
-            run_host_batch(cm, in + lo * in_stripe_stride, in_stripe_stride, in_slot_stride,
-                           out + lo * out_stripe_stride, out_stripe_stride, out_slot_stride, n, nbytes);
+            range(lo, hi - lo);
         } catch (const Error &e) {
             res[(size_t)j] = {e.code, e.what()};
         } catch (const std::bad_alloc &) {
@@ -210,7 +264,7 @@ void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_strip
             res[(size_t)j] = {ECX_E_ILLEGAL_ARGUMENT, e.what()};
         }
     };
-    // one worker thread per device entry; the caller's thread (and its current device) only waits
+    // the caller's thread (and its current device) only waits
     std::vector<std::thread> th;
     th.reserve((size_t)ndev);
     try {
@@ -223,6 +277,28 @@ void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_strip
     for (int j = 0; j < ndev; ++j)
         if (res[(size_t)j].code != ECX_OK)
             throw Error(res[(size_t)j].code, "device " + std::to_string(devices[j]) + ": " + res[(size_t)j].what);
+}
+
+}  // namespace
+
+void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                            uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
+                            int64_t nbytes, const int *devices, int ndev) {
+    if (nbytes <= 0 || cm.map().n_out == 0) nstripes = 0;  // validate the list, touch nothing
+    on_devices(devices, ndev, nstripes, [&](int64_t lo, int64_t n) {
+        run_host_batch(cm, in + lo * in_stripe_stride, in_stripe_stride, in_slot_stride, out + lo * out_stripe_stride,
+                       out_stripe_stride, out_slot_stride, n, nbytes);
+    });
+}
+
+void run_host_check_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride,
+                                  int64_t in_slot_stride, int64_t nstripes, int64_t nbytes, uint8_t *verdict,
+                                  const int *devices, int ndev) {
+    if (nstripes > 0 && !verdict) throw Error(ECX_E_NULL, "verdict buffer is null");
+    on_devices(devices, ndev, nstripes, [&](int64_t lo, int64_t n) {
+        run_host_check_batch(cm, in + lo * in_stripe_stride, in_stripe_stride, in_slot_stride, n, nbytes,
+                             verdict + lo);
+    });
 }
 
 }  // namespace ecx

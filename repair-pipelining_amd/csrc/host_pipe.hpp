@@ -1,0 +1,19 @@
+// host_pipe.hpp -- the read-only host-memory batches of host_pipe.cpp (the check; the
+// map batches are declared with the engine, engine.hpp).
+#pragma once
+
+#include "engine.hpp"
+
+namespace ecx {
+
+// launch_check over host-memory stripes: the check map's used slots of each chunk of stripes
+// go H2D, k_gf_check writes the chunk's verdict bytes on the device and only those come back
+// into the host array `verdict` (one byte per stripe).  Synchronous, on the current device.
+void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                          int64_t nstripes, int64_t nbytes, uint8_t *verdict);
+// run_host_check_batch split over a device list, as run_host_batch_devices (engine.hpp).
+void run_host_check_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride,
+                                  int64_t in_slot_stride, int64_t nstripes, int64_t nbytes, uint8_t *verdict,
+                                  const int *devices, int ndev);
+
+}  // namespace ecx

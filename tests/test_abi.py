@@ -211,10 +211,11 @@ def test_codec_registry_refcounts_and_bounds_idle(ecx):
     destroy(a)
     assert counts()[:2] == [live0 + 1, idle0]        # one reference left
     destroy(b)
-    assert counts()[:2] == [live0, idle0 + 1]        # parked idle, not freed
+    parked = min(idle0 + 1, 64)  # (an idle cache already full evicts its oldest entry instead)
+    assert counts()[:2] == [live0, parked]           # parked idle, not freed
     destroy(b)                                        # a second destroy holds no reference: ignored
-    assert counts()[:2] == [live0, idle0 + 1]
-    assert rs(29, 3) == a and counts()[:2] == [live0 + 1, idle0]  # revived: same object
+    assert counts()[:2] == [live0, parked]
+    assert rs(29, 3) == a and counts()[:2] == [live0 + 1, parked - 1]  # revived: same object
     destroy(a)
     # many distinct codecs created and released: the idle cache stays bounded
     for k in range(100):
@@ -271,6 +272,36 @@ def test_is_parity_correct_batch_argument_checks(ecx):
     assert lib.ecx_rs_is_parity_correct_batch(rs._h, None, 20 * 64, 64, 0, 0, 64, None, None) == 0
     if not _has_device(ecx):
         assert lib.ecx_rs_is_parity_correct_batch(rs._h, 16, 20 * 64, 64, 1, 0, 64, 16, None) == -10
+
+
+def test_host_check_batch_argument_checks(ecx):
+    """ecx_rs_is_parity_correct_batch_host(_devices): negative counts or strides are
+    IllegalArgumentException, a null codec, stripe or verdict pointer NullPointerException, an
+    empty or null device list is refused before any device is touched; an empty batch is a
+    no-op; with bytes to check and no device the call fails loudly (ECX_E_DEVICE) -- no CPU path."""
+    import numpy as np
+    lib = ecx.lib()
+    rs = ecx.ReedSolomon.create(17, 3)
+    shards, verdict = np.zeros((2, 20, 64), np.uint8), np.full(2, 7, np.uint8)
+    base, v = shards.ctypes.data, verdict.ctypes.data
+    f = lib.ecx_rs_is_parity_correct_batch_host
+    assert f(rs._h, base, 20 * 64, 64, -1, 0, 64, v) == -1
+    assert f(rs._h, base, 20 * 64, 64, 2, -1, 64, v) == -1
+    assert f(rs._h, base, 20 * 64, 64, 2, 0, -64, v) == -1
+    assert f(rs._h, base, -1, 64, 2, 0, 64, v) == -1
+    assert f(None, base, 20 * 64, 64, 2, 0, 64, v) == -6
+    assert f(rs._h, None, 20 * 64, 64, 2, 0, 64, v) == -6
+    assert f(rs._h, base, 20 * 64, 64, 2, 0, 64, None) == -6
+    assert f(rs._h, None, 20 * 64, 64, 0, 0, 64, None) == 0
+    g = lib.ecx_rs_is_parity_correct_batch_host_devices
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert g(rs._h, base, 20 * 64, 64, 2, 0, 64, v, None, 1) == -6
+    assert g(rs._h, base, 20 * 64, 64, 2, 0, 64, v, devs, 0) == -1
+    assert g(rs._h, base, 20 * 64, 64, -2, 0, 64, v, devs, 2) == -1
+    if not _has_device(ecx):
+        assert f(rs._h, base, 20 * 64, 64, 2, 0, 64, v) == -10
+        assert g(rs._h, base, 20 * 64, 64, 2, 0, 64, v, devs, 2) == -10
+        assert (verdict == 7).all()  # nothing was decided on the host
 
 
 def test_shape_knobs_need_the_opt_in():

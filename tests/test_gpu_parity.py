@@ -786,6 +786,22 @@ def test_is_parity_correct_batch_vs_oracle(ecx, torch_dev, k, m, L, off, S):
     for s in range(S):
         sh = [host[s, i].copy() for i in range(n)]
         assert O.ReedSolomon(k, m).is_parity_correct(sh, off, L) == bool(want[s])
+    # the same stripes from host memory (isParityCorrectBatchHost: chunks pipelined H2D through
+    # k_gf_check, only the verdict bytes D2H), one device and the list [0, 0], in 16 KiB chunks
+    ecx.tune("host_chunk_kib", 16)
+    try:
+        for devs in (None, [0, 0]):
+            for win in (L, L - 1, 0):
+                # a stripe fails when one of its flipped bytes lies in [off, off + win)
+                expect = [0 if s in flips and flips[s][1] < off + win else 1 for s in range(S)]
+                hv = np.full(S, 7, np.uint8)
+                if devs is None:
+                    rs.isParityCorrectBatchHost(host, n * pitch, pitch, S, off, win, hv)
+                else:
+                    rs.isParityCorrectBatchHostDevices(host, n * pitch, pitch, S, off, win, hv, devs)
+                assert hv.tolist() == expect, (devs, win, hv.tolist())
+    finally:
+        ecx.tune("host_chunk_kib", 65536)
     # the window: a check that ends before the last flipped byte passes that stripe
     if L > 1:
         rs.isParityCorrectBatch(pool, n * pitch, pitch, S, off, L - 1, verdict)

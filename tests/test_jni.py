@@ -112,13 +112,19 @@ def test_no_public_native_takes_a_raw_host_address():
     direct ByteBuffers whose capacity the forwarder reads itself (ClayCoordinator.kt:378-390)."""
     public = dict(re.findall(r"public static native [\w\[\]]+ (\w+)\(([^)]*)\);", JAVA_SRC))
     for name in ("directAddress", "wrapAddress", "mapApplyBatchHost", "clayPerformCodingBatchHost",
-                 "mapApplyBatchHostDevices", "clayPerformCodingBatchHostDevices"):
+                 "mapApplyBatchHostDevices", "clayPerformCodingBatchHostDevices", "rsIsParityCorrectBatchHost",
+                 "rsIsParityCorrectBatchHostDevices"):
         assert name not in public, name
         assert re.search(r"\n    static native [\w\[\]]+ %s\(" % name, JAVA_SRC), name
     host_batch = {n: p for n, p in public.items() if "BatchHost" in n}
     assert set(host_batch) == {"mapApplyBatchHostBuffer", "clayPerformCodingBatchHostBuffer",
-                               "mapApplyBatchHostDevicesBuffer", "clayPerformCodingBatchHostDevicesBuffer"}
+                               "mapApplyBatchHostDevicesBuffer", "clayPerformCodingBatchHostDevicesBuffer",
+                               "rsIsParityCorrectBatchHostBuffer", "rsIsParityCorrectBatchHostDevicesBuffer"}
     for n, params in host_batch.items():
+        if n.startswith("rsIsParityCorrect"):  # the stripes and one verdict byte per stripe
+            assert "ByteBuffer base" in params and "ByteBuffer verdict" in params, n
+            assert "long base," not in params and "long verdict," not in params, n
+            continue
         assert "ByteBuffer in" in params and "ByteBuffer out" in params, n
         assert "long in," not in params and "long out," not in params, n
     # the generated C forwarder reads the capacity of every ByteBuffer it is given

@@ -331,6 +331,36 @@ def test_clay_batch_host_devices_buffer_checks(J):
         J.call("clayDestroy", clay)
 
 
+def test_rs_check_batch_host_buffer_checks(J):
+    """rsIsParityCorrectBatchHost(Devices)Buffer: the stripes' ByteBuffer must hold every shard
+    of every stripe up to offset + byteCount, the verdict ByteBuffer one byte per stripe; short,
+    heap or null buffers and a bad device list are refused before anything is read or written."""
+    rs = handle(J, "rsCreate", 17, 3)
+    try:
+        S, L = 3, 512
+        ss, sl = 20 * L, L
+        shards, verdict = rnd(S * ss, 21), np.full(S, 7, np.uint8)
+        need = (S - 1) * ss + 19 * sl + L
+        J.reset()
+        call = lambda b, v, **kw: J.call("rsIsParityCorrectBatchHostBuffer", rs, b, ss, sl, kw.get("S", S),  # noqa: E731
+                                         kw.get("off", 0), kw.get("L", L), v)
+        assert call(J.direct(shards, need - 1), J.direct(verdict)) == IDX     # stripes one byte short
+        assert call(J.direct(shards), J.direct(verdict, S - 1)) == IDX         # verdict one byte short
+        assert call(J.direct(shards), J.direct(verdict), off=1) == IDX         # window past the shard pitch end
+        assert call(J.direct(shards), J.direct(verdict), off=-1) == ILL
+        assert call(J.direct(shards), J.direct(verdict), S=-1) == ILL
+        assert call(J.array(shards), J.direct(verdict)) == NUL                 # heap buffer
+        assert call(J.direct(shards), None) == NUL
+        dcall = lambda devs, nd: J.call("rsIsParityCorrectBatchHostDevicesBuffer", rs, J.direct(shards), ss, sl,  # noqa: E731
+                                        S, 0, L, J.direct(verdict), devs, nd)
+        assert dcall(J.ints([0]), 2) == ILL and dcall(None, 1) == NUL and dcall(J.ints([0]), -1) == ILL
+        assert J.counters()["pins"] == 0 and (verdict == 7).all()
+        st = call(J.direct(shards, need), J.direct(verdict, S))
+        assert st == (OK if has_device(J) else DEV), st
+    finally:
+        J.call("rsDestroy", rs)
+
+
 def test_codec_reference_survives_other_releases(J):
     """The registry side of ADVICE r04 (EcxPartialSums / EcxClayCodeErasureDecodingStep close):
     two handles of one (k, m) codec are one shared object; releasing one and then more than
@@ -494,6 +524,40 @@ def test_clay_batch_host_devices_buffer_via_jni_vs_oracle(J):
                 assert (out[s_ * oss + z * B:s_ * oss + (z + 1) * B] == ref[z]).all(), (s_, z)
     finally:
         J.call("clayDestroy", clay)
+
+
+@pytest.mark.gpu
+def test_rs_check_batch_host_buffer_via_jni_vs_oracle(J):
+    """RS(17,3) isParityCorrect over 7 host stripes through the checked ByteBuffer forwarders,
+    one device and the list [0, 0]: stripes encoded by the oracle pass, a stripe with one byte
+    flipped (a data shard, a parity shard's last byte) fails, as the oracle's isParityCorrect says."""
+    rs = handle(J, "rsCreate", 17, 3)
+    try:
+        S, L = 7, 3000
+        ss, sl = 20 * L, L
+        shards = rnd(S * ss, 31)
+        for s_ in range(S):
+            sh = [shards[s_ * ss + i * L:s_ * ss + (i + 1) * L].copy() for i in range(20)]
+            O.ReedSolomon(17, 3).encode_parity(sh, 0, L)
+            shards[s_ * ss:(s_ + 1) * ss] = np.concatenate(sh)
+        shards[2 * ss + 5 * L + 17] ^= 1         # stripe 2: data shard 5
+        shards[6 * ss + 19 * L + L - 1] ^= 0x80  # stripe 6: parity shard 19's last byte
+        want = []
+        for s_ in range(S):
+            sh = [shards[s_ * ss + i * L:s_ * ss + (i + 1) * L].copy() for i in range(20)]
+            want.append(1 if O.ReedSolomon(17, 3).is_parity_correct(sh, 0, L) else 0)
+        assert want == [1, 1, 0, 1, 1, 1, 0]
+        for devs in (None, [0, 0]):
+            verdict = np.full(S, 7, np.uint8)
+            if devs is None:
+                st = J.call("rsIsParityCorrectBatchHostBuffer", rs, J.direct(shards), ss, sl, S, 0, L, J.direct(verdict))
+            else:
+                st = J.call("rsIsParityCorrectBatchHostDevicesBuffer", rs, J.direct(shards), ss, sl, S, 0, L,
+                            J.direct(verdict), J.ints(devs), len(devs))
+            assert st == OK, st
+            assert verdict.tolist() == want, (devs, verdict.tolist())
+    finally:
+        J.call("rsDestroy", rs)
 
 
 @pytest.mark.gpu
