@@ -345,7 +345,7 @@ const char *ecx_status_string(int s) {
 }
 
 const char *ecx_last_error(void) { return g_last_error.c_str(); }
-int ecx_version(void) { return 105; }  // 1.05: round-5 ABI (check batch, multi-GPU host batches, per-call executor)
+int ecx_version(void) { return 106; }  // 1.06: round-5 ABI (check batches device and host, multi-GPU host batches, per-call executor)
 
 // ---------------------------------------------------------------- device
 int ecx_device_count(int *count) {
