@@ -1159,7 +1159,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    launch_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    launch_times = [a.elapsed_time(b) for a, b in evs]
+    launch_ms = sum(launch_times) / len(launch_times)
+    # the spread of the timed launches, first and last step apart: a memory system still busy
+    # with something else early in the run (e.g. the driver clearing VRAM a previous process
+    # freed) shows as a slower first step
+    per_step = [sum(launch_times[i * passes:(i + 1) * passes]) / passes for i in range(args.steps)]
+    launch_spread = {"min": round(min(launch_times), 4), "max": round(max(launch_times), 4),
+                     "first_step": round(per_step[0], 4), "last_step": round(per_step[-1], 4)}
     per_launch_bytes = P * wl.unit_bytes
     achieved = per_launch_bytes / (launch_ms * 1e-3) / 1e9
     total_stripes = stripes_per_step * args.steps * world
@@ -1243,7 +1250,7 @@ def main():
                 "traffic_note": traffic_note,
                 "kernel": kernel,
                 "kernel_source_hash": kernel_source_hash(kernel),
-                "avg_launch_ms": round(launch_ms, 4),
+                "avg_launch_ms": round(launch_ms, 4), "launch_ms_spread": launch_spread,
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "measured_ceilings": probes,
                 "launch_shape": dict(launch_shape or {}, name=shape),
