@@ -15,6 +15,8 @@ null one is refused before anything is pinned or read.
 GPU: codeSomeShards (RS(4,2) parity rows), the RS codec calls, decodeMissingSingle,
 clayPerformCoding (Clay(4,2), e = 1) and the two ByteBuffer host batches through the
 binding equal the oracle, with array positions (ByteBuffer.arrayOffset + position) applied."""
+import re
+
 import numpy as np
 import pytest
 
@@ -382,12 +384,24 @@ def test_codec_reference_survives_other_releases(J):
     from pathlib import Path
     root = Path(__file__).resolve().parents[1] / "jni"
     for f, field in (("com/backblaze/erasure/ecx/EcxPartialSums.java", "rs"),
+                     ("com/backblaze/erasure/ecx/EcxParityCheck.java", "rs"),
                      ("distributed/erasure/coding/clay/EcxClayCodeErasureDecodingStep.java", "clay")):
         src = (root / f).read_text()
         close = src[src.index("public synchronized void close()"):]
         close = close[:close.index("\n    }\n")]
         assert "if (%s == 0)" % field in close and "%s = 0;" % field in close, f
         assert "private long %s;" % field in src and "IllegalStateException" in src, f
+
+
+def test_parity_check_wrapper_uses_the_checked_variants():
+    """EcxParityCheck (the batch isParityCorrect for JVM callers) reaches libecx only through
+    the capacity-checked ByteBuffer natives, and checks the same extents in Java first."""
+    from pathlib import Path
+    src = (Path(__file__).resolve().parents[1] / "jni" / "com" / "backblaze" / "erasure" / "ecx" /
+           "EcxParityCheck.java").read_text()
+    used = set(re.findall(r"EcxNative\.(\w+)\(", src))
+    assert used == {"rsIsParityCorrectBatchHostBuffer", "rsIsParityCorrectBatchHostDevicesBuffer", "rsDestroy"}
+    assert src.count("checkExtent(stripes") == 2 and "ArrayIndexOutOfBoundsException" in src
 
 
 def test_java_wrapper_uses_the_checked_variant():
