@@ -20,6 +20,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 
 #include "host_exec.hpp"
@@ -44,10 +45,11 @@ uint64_t affine_of(uint8_t c) {
     return a;
 }
 
-int g_force_isa = -1;  // host_exec_force_isa (tests)
+std::atomic<int> g_force_isa{-1};  // host_exec_force_isa (tests); read by every calling thread
 
 int isa_level() {  // 2: AVX-512BW + GFNI, 1: AVX2, 0: scalar
-    if (g_force_isa >= 0) return g_force_isa;
+    const int forced = g_force_isa.load(std::memory_order_relaxed);
+    if (forced >= 0) return forced;
     static const int v = [] {
         __builtin_cpu_init();
         if (__builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("gfni")) return 2;
@@ -229,10 +231,10 @@ void host_exec_scale(uint8_t c, const uint8_t *in, uint8_t *out, int64_t n, bool
 int host_exec_isa() { return isa_level(); }
 
 int host_exec_force_isa(int level) {
-    g_force_isa = -1;
+    g_force_isa.store(-1);
     const int have = isa_level();
     if (level > have) return -1;
-    g_force_isa = level;
+    g_force_isa.store(level);
     return level;
 }
 
