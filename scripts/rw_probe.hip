@@ -9,7 +9,7 @@
 // Full 4 KiB chunks only (the partial last chunk of a 200,000-B shard is left out of both the
 // launch and the bytes).  Interleaved rounds, median launch, algorithmic GB/s over ~16 GB.
 //
-//   hipcc --offload-arch=gfx950 -O3 scripts/rw_probe.hip -o scripts/rw_probe && ./scripts/rw_probe [pitch]
+//   hipcc --offload-arch=gfx950 -O3 scripts/rw_probe.hip -o scripts/rw_probe && ./scripts/rw_probe [pitch | rs124]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -91,7 +91,7 @@ float launch(const uint8_t *pool, uint8_t *out, const Layout &l, int64_t stripes
 float dispatch(int r, int w, const uint8_t *pool, uint8_t *out, const Layout &l, int64_t stripes) {
 #define RW(R_, W_) \
     if (r == R_ && w == W_) return launch<R_, W_>(pool, out, l, stripes);
-    RW(20, 0) RW(17, 3) RW(17, 0) RW(14, 6) RW(10, 10) RW(8, 2) RW(12, 2) RW(20, 8) RW(12, 4) RW(3, 17)
+    RW(20, 0) RW(17, 3) RW(17, 0) RW(14, 6) RW(10, 10) RW(8, 2) RW(12, 2) RW(20, 8) RW(12, 4) RW(3, 17) RW(12, 0)
 #undef RW
     return -1.f;
 }
@@ -99,6 +99,14 @@ float dispatch(int r, int w, const uint8_t *pool, uint8_t *out, const Layout &l,
 int main(int argc, char **argv) {
     // "pitch": 17:3 in place over a sweep of shard pitches (and a few separate-output points)
     const bool pitch_sweep = argc > 1 && std::string(argv[1]) == "pitch";
+    // "rs124": RS(12,4)'s 2-erasure decode pattern (12 read, 2 written in place) over shard pitches
+    const bool rs124 = argc > 1 && std::string(argv[1]) == "rs124";
+    const Case rs124_cases[] = {
+        {"12r2w_4m", 12, 2, 4194304, true},      {"12r2w_4m4k", 12, 2, 4194304 + 4096, true},
+        {"12r2w_4m64k", 12, 2, 4194304 + 65536, true}, {"12r2w_2m", 12, 2, 2097152, true},
+        {"12r2w_1m", 12, 2, 1048576, true},      {"12r2w_256k", 12, 2, 262144, true},
+        {"12r0w_4m", 12, 0, 4194304, true},      {"12r2w_4m_sep", 12, 2, 4194304, false},
+    };
     const Case sweep[] = {
         {"17r3w_32k", 17, 3, 32768, true},    {"17r3w_64k", 17, 3, 65536, true},    {"17r3w_128k", 17, 3, 131072, true},
         {"17r3w_192k", 17, 3, 196608, true},  {"17r3w_200000", 17, 3, 200000, true}, {"17r3w_256k", 17, 3, 262144, true},
@@ -121,8 +129,9 @@ int main(int argc, char **argv) {
     hipMemset(pool, 0x5A, pool_bytes);
     hipMemset(sep, 0, sep_bytes);
     hipDeviceSynchronize();
-    const Case *cases = pitch_sweep ? sweep : base;
-    const size_t ncases = pitch_sweep ? sizeof(sweep) / sizeof(sweep[0]) : sizeof(base) / sizeof(base[0]);
+    const Case *cases = rs124 ? rs124_cases : pitch_sweep ? sweep : base;
+    const size_t ncases = rs124 ? sizeof(rs124_cases) / sizeof(rs124_cases[0])
+                          : pitch_sweep ? sizeof(sweep) / sizeof(sweep[0]) : sizeof(base) / sizeof(base[0]);
     for (int round = 0; round < 2; ++round) {
         for (size_t ci = 0; ci < ncases; ++ci) {
             const Case &c = cases[ci];
