@@ -2461,3 +2461,39 @@ def test_every_entry_kind_at_once(ecx, torch_dev):
         ecx.tune("host_exec_kib", 0)
     assert not any(t.is_alive() for t in threads), "a worker thread hung"
     assert not errors, errors[:6]
+
+
+def test_host_check_batch_random_layouts(ecx):
+    """isParityCorrectBatchHost(Devices) over 24 random layouts -- RS(k, m) with k + m <= 24,
+    shard lengths 1 .. 20,000 B, byte windows at random offsets, padded pitches, 1 .. 9 stripes,
+    one device or [0, 0], 16 KiB host chunks -- with a random half of the stripes given one
+    flipped byte inside or outside the window: every verdict equals the oracle's isParityCorrect."""
+    rng = np.random.default_rng(20261018)
+    ecx.tune("host_chunk_kib", 16)
+    try:
+        for case in range(24):
+            k = int(rng.integers(1, 18))
+            m = int(rng.integers(1, min(8, 25 - k)))
+            n = k + m
+            L = int(rng.integers(1, 20001))
+            off = int(rng.integers(0, 64))
+            win = int(rng.integers(0, L + 1)) if rng.random() < 0.3 else L
+            pitch = off + L + int(rng.integers(0, 3)) * 16
+            S = int(rng.integers(1, 10))
+            host = rng.integers(0, 256, (S, n, pitch), dtype=np.uint8)
+            for s in range(S):
+                O.ReedSolomon(k, m).encode_parity([host[s, i] for i in range(n)], off, L)
+            for s in range(S):
+                if rng.random() < 0.5:
+                    host[s, int(rng.integers(0, n)), off + int(rng.integers(0, L))] ^= int(rng.integers(1, 256))
+            want = [1 if O.ReedSolomon(k, m).is_parity_correct([host[s, i].copy() for i in range(n)], off, win) else 0
+                    for s in range(S)]
+            rs = ecx.ReedSolomon.create(k, m)
+            verdict = np.full(S, 7, np.uint8)
+            if case % 2:
+                rs.isParityCorrectBatchHostDevices(host, n * pitch, pitch, S, off, win, verdict, [0, 0])
+            else:
+                rs.isParityCorrectBatchHost(host, n * pitch, pitch, S, off, win, verdict)
+            assert verdict.tolist() == want, (case, k, m, L, off, win, pitch, S)
+    finally:
+        ecx.tune("host_chunk_kib", 65536)
