@@ -88,6 +88,32 @@ int main() {
     rs("rs173 200,000-B shards, separate outputs", P173, false);
     rs("rs173 256 KiB shards in place", P256, true);
     rs("rs173 256 KiB shards, separate outputs", P256, false);
+    // LRC(12 data, 4 XOR local parities), 64 KiB blocks [d d d p] x 4: the encode reads the twelve
+    // data blocks and writes the four parities in place; the block-2 repair reads blocks 0, 1, 3
+    // of its group and writes one block to a separate buffer
+    const int64_t P64 = 65536;
+    {
+        Case c{"lrc encode 64 KiB blocks in place", {}, 1 << 15, true};
+        c.s.n_in = 12;
+        c.s.n_out = 4;
+        for (int i = 0; i < 12; ++i) c.s.in_slot[i] = (int64_t)((i / 3) * 4 + i % 3) * P64;
+        for (int r = 0; r < 4; ++r) c.s.out_slot[r] = (int64_t)(r * 4 + 3) * P64;
+        c.s.stripe_bytes = c.s.out_stripe_bytes = 16 * P64;
+        c.s.chunks = 16;
+        cases.push_back(c);
+    }
+    {
+        Case c{"lrc repair of block 2, 64 KiB blocks", {}, 1 << 15, false};
+        c.s.n_in = 3;
+        c.s.n_out = 1;
+        const int slots[3] = {0, 1, 3};
+        for (int i = 0; i < 3; ++i) c.s.in_slot[i] = slots[i] * P64;
+        c.s.out_slot[0] = 0;
+        c.s.stripe_bytes = 16 * P64;
+        c.s.out_stripe_bytes = P64;
+        c.s.chunks = 16;
+        cases.push_back(c);
+    }
 
     int64_t pool_bytes = 0, out_bytes = 0;
     for (auto &c : cases) {
@@ -108,6 +134,8 @@ int main() {
         const dim3 grid((unsigned)(c.stripes * c.s.chunks));
         uint8_t *dst = c.inplace ? pool : out;
         if (c.s.n_in == 20) hipLaunchKernelGGL((k_slots<20, 8>), grid, dim3(256), 0, 0, pool, dst, c.s);
+        else if (c.s.n_in == 12) hipLaunchKernelGGL((k_slots<12, 4>), grid, dim3(256), 0, 0, pool, dst, c.s);
+        else if (c.s.n_in == 3) hipLaunchKernelGGL((k_slots<3, 1>), grid, dim3(256), 0, 0, pool, dst, c.s);
         else hipLaunchKernelGGL((k_slots<17, 3>), grid, dim3(256), 0, 0, pool, dst, c.s);
     };
     for (int round = 0; round < 5; ++round)
