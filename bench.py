@@ -333,25 +333,94 @@ def pmc_traffic(workload: str, pool: int, kernel: str, shape: str = None):
         return None, "unreadable PMC profile: %s" % e
 
 
-E2E_HOST_BYTES = 3 << 30  # pinned host input per rank for the end-to-end leg (at least one stripe)
+# Pinned host input per rank for the end-to-end leg.  One rank alone gets E2E_HOST_BYTES; the
+# ranks of one node share E2E_NODE_BYTES (they run the leg at once on one host), and all of them
+# together take at most E2E_MEM_FRACTION of the host memory the lease has free (the smaller of
+# MemAvailable and the cgroup's memory.max - memory.current), read before the leg starts.
+E2E_HOST_BYTES = 3 << 30
+E2E_NODE_BYTES = 6 << 30
+E2E_MEM_FRACTION = 0.25
+E2E_COPY_CHUNK = 256 << 20  # device <-> host copies of the leg's fill and check, per step
 
 
-def e2e_rate(ecx, torch, wl, seconds: float):
+def host_memory_free() -> dict:
+    """Host memory this process may still take: /proc/meminfo MemAvailable and the cgroup
+    (v2 memory.max - memory.current, or v1 memory.limit_in_bytes - usage_in_bytes) limit."""
+    out = {"mem_available": None, "cgroup_limit": None, "cgroup_used": None}
+    try:
+        for ln in open("/proc/meminfo"):
+            if ln.startswith("MemAvailable:"):
+                out["mem_available"] = int(ln.split()[1]) * 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    for lim, cur in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
+                     ("/sys/fs/cgroup/memory/memory.limit_in_bytes", "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+        try:
+            text = open(lim).read().strip()
+            used = int(open(cur).read().strip())
+        except (OSError, ValueError):
+            continue
+        if text != "max" and int(text) < (1 << 60):  # v1 reports "no limit" as a huge number
+            out["cgroup_limit"], out["cgroup_used"] = int(text), used
+        break
+    frees = [v for v in (out["mem_available"],
+                         out["cgroup_limit"] - out["cgroup_used"] if out["cgroup_limit"] else None) if v is not None]
+    out["free"] = max(0, min(frees)) if frees else None
+    return out
+
+
+def e2e_host_budget(world: int, free_bytes=None) -> int:
+    """Pinned host input bytes one rank may use for the end-to-end leg: E2E_HOST_BYTES alone,
+    an equal share of E2E_NODE_BYTES when `world` ranks run it at once, and never more than
+    its share of E2E_MEM_FRACTION of the free host memory."""
+    world = max(1, int(world))
+    budget = min(E2E_HOST_BYTES, E2E_NODE_BYTES // world)
+    if free_bytes is not None:
+        budget = min(budget, int(free_bytes * E2E_MEM_FRACTION) // world)
+    return max(0, budget)
+
+
+def _copy_chunked(dst, src, chunk=None):
+    """dst.copy_(src) for two flat uint8 tensors (one on the device, one a host view), at most
+    `chunk` bytes per step, so no full-size host intermediate exists at any time."""
+    chunk = chunk or E2E_COPY_CHUNK
+    for a in range(0, src.numel(), chunk):
+        dst[a:a + chunk].copy_(src[a:a + chunk])
+
+
+def _peak_rss_bytes() -> int:
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024  # Linux reports KiB
+
+
+def e2e_rate(ecx, torch, wl, seconds: float, world: int = 1):
     """End-to-end rate of this workload's map on this rank's GPU with the data starting and
     ending in host memory, as the reference's path does (sub-chunks arrive and leave on
     sockets, ClayCoordinator.kt:372-395, ClayCodeNode.kt:330-347): pinned host stripes ->
     pipelined H2D -> the same kernel -> D2H (ecx_*_batch_host, host_pipe.cpp), repeated for
-    >= `seconds`.  The host input holds the first stripes of the GPU run's own (valid) pool;
-    the host outputs are compared with the device run's.  GiBps counts the workload's
-    algorithmic bytes per stripe (as `value`); h2d/d2h_GBps the bytes that crossed PCIe."""
+    >= `seconds`.  The host input holds the first stripes of the GPU run's own (valid) pool,
+    copied into the pinned buffer straight from HBM in E2E_COPY_CHUNK steps (no pageable copy
+    of the pool); the host outputs are compared with the device run's the same way.  The
+    pinned input is bounded per rank by e2e_host_budget(world, free host memory).  GiBps
+    counts the workload's algorithmic bytes per stripe (as `value`); h2d/d2h_GBps the bytes
+    that crossed PCIe."""
     import numpy as np
     if not wl.host_ok:
         return None
     sb, ob = wl.host_stripe_bytes(), wl.host_out_bytes()
-    n = max(1, min(wl.P, E2E_HOST_BYTES // sb))
+    mem = host_memory_free()
+    budget = e2e_host_budget(world, mem["free"])
+    n = min(wl.P, budget // sb)
+    cap = {"budget_bytes_per_rank": budget, "world": world, "host_free_bytes": mem["free"],
+           "mem_available": mem["mem_available"], "cgroup_limit": mem["cgroup_limit"]}
+    if n == 0:  # one stripe alone is larger than this rank's share
+        if world == 1 and (mem["free"] is None or sb + ob <= mem["free"] * E2E_MEM_FRACTION):
+            n = 1  # a single rank may still take one (large) stripe within its memory fraction
+        else:
+            return {"skipped": "one %d-B stripe exceeds this rank's host budget" % sb, "host_cap": cap}
     hin = ecx.HostBuffer(n * sb)
     hout = ecx.HostBuffer(n * ob) if ob else None
-    hin.array.reshape(n, sb)[:] = wl.pool[:n].reshape(n, sb).cpu().numpy()
+    _copy_chunked(torch.from_numpy(hin.array), wl.pool[:n].reshape(-1))
     ha, ho = hin.array, (hout.array if hout else None)
     wl.host_call(ha, ho, n)  # warm-up: plans, pipe buffers
     ok = wl.host_expect(ha, ho if ho is not None else np.empty(0, np.uint8), n)
@@ -367,6 +436,7 @@ def e2e_rate(ecx, torch, wl, seconds: float):
     out = {"GiBps": round(units * wl.unit_bytes / el / 2**30, 3),
            "h2d_GBps": round(units * h2d / el / 1e9, 2), "d2h_GBps": round(units * d2h / el / 1e9, 2),
            "stripes_per_call": n, "calls": calls, "seconds": round(el, 3), "verified": ok,
+           "host_bytes": n * (sb + ob), "host_cap": cap, "peak_rss_bytes": _peak_rss_bytes(),
            "path": "pinned host -> H2D -> kernel -> D2H, pipelined (ecx host batch, host_pipe.cpp)"}
     if wl.metric_unit != "GiB/s":
         out["value"] = round(units * (wl.metric_bytes or wl.unit_bytes) / el / wl.metric_scale, 1)
@@ -454,13 +524,19 @@ class Workload:
         raise NotImplementedError
 
     def host_expect(self, hin, hout, n) -> bool:
-        """The host outputs of the first n stripes equal the device run's."""
+        """The host outputs of the first n stripes equal the device run's (compared in
+        E2E_COPY_CHUNK steps: no full-size host copy of the device side)."""
         import numpy as np
         if self.host_out_bytes() == 0:  # written in place: the whole host stripes equal the device pool's
-            got = hin[:n * self.host_stripe_bytes()]
-            return bool(np.array_equal(got.reshape(n, -1), self.pool[:n].reshape(n, -1).cpu().numpy()))
-        got = hout[:n * self.host_out_bytes()]
-        return bool(np.array_equal(got.reshape(n, -1), self.out[:n].reshape(n, -1).cpu().numpy()))
+            got, want = hin[:n * self.host_stripe_bytes()], self.pool[:n].reshape(-1)
+        else:
+            got, want = hout[:n * self.host_out_bytes()], self.out[:n].reshape(-1)
+        if got.size != want.numel():
+            return False
+        for a in range(0, got.size, E2E_COPY_CHUNK):
+            if not np.array_equal(got[a:a + E2E_COPY_CHUNK], want[a:a + E2E_COPY_CHUNK].cpu().numpy()):
+                return False
+        return True
 
     def pcie_bytes(self):
         """(H2D, D2H) bytes per stripe: only the map's used input / output slots cross PCIe."""
@@ -1188,16 +1264,26 @@ def main():
     if args.e2e_seconds > 0:
         if grouped:
             dist.barrier()
-        mine = e2e_rate(ecx, torch, wl, args.e2e_seconds)
+        rss_before = _peak_rss_bytes()  # the process before the leg: torch + HIP runtime, the bench's own state
+        mine = e2e_rate(ecx, torch, wl, args.e2e_seconds, world)
         if mine is not None:
-            rates = [mine["GiBps"]]
+            # (rate, peak host RSS before / after the leg) of every rank; a rank that skipped
+            # the leg reports rate -1
+            own = [mine.get("GiBps", -1.0), float(rss_before), float(_peak_rss_bytes())]
+            rows = [own]
             if grouped:
-                g = [torch.zeros(1, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+                g = [torch.zeros(3, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
                      for _ in range(world)]
-                dist.all_gather(g, torch.tensor([mine["GiBps"]], dtype=torch.float64, device=g[0].device))
-                rates = [float(x.item()) for x in g]
-            e2e = dict(mine, rank0_GiBps=mine["GiBps"], GiBps=round(sum(rates), 3),
-                       per_rank_GiBps=[round(r, 3) for r in rates])
+                dist.all_gather(g, torch.tensor(own, dtype=torch.float64, device=g[0].device))
+                rows = [[float(v) for v in x.tolist()] for x in g]
+            rates = [r[0] for r in rows]
+            rss = {"per_rank_MiB": [round(r[2] / 2**20) for r in rows], "max_MiB": round(max(r[2] for r in rows) / 2**20),
+                   "before_leg_per_rank_MiB": [round(r[1] / 2**20) for r in rows]}
+            if "skipped" in mine:
+                e2e = dict(mine, peak_rss=rss)
+            else:
+                e2e = dict(mine, rank0_GiBps=mine["GiBps"], GiBps=round(sum(r for r in rates if r >= 0), 3),
+                           per_rank_GiBps=[round(r, 3) for r in rates], peak_rss=rss)
 
     sample = units = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the contract: rank 0 at N=1 only

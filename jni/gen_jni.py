@@ -491,7 +491,7 @@ public final class EcxNative {
             java.append("\n    /** Raw host addresses: package-private (use %sBuffer). */" % jname)
         java.append("\n    %sstatic native %s %s(%s);\n" % (vis, jret, jname, ", ".join(jparams)))
         body = []
-        pre, pin, unpin, post, args = [], [], [], [], []
+        pre, copies, pin, unpin, post, args = [], [], [], [], [], []
         pnames = {p: kind for (kind, _, _), t, p in kinds}
         needs_rule = [p for p, k in pnames.items() if k in ("bytes", "ints", "shorts", "buflist")]
         if needs_rule and name not in RULES:
@@ -541,6 +541,18 @@ public final class EcxNative {
                 args.append("&%s_h" % p)
                 post.append("    if (st >= 0 && %s) { jlong v = (jlong)(intptr_t)%s_h; (*env)->SetLongArrayRegion(env, %s, 0, 1, &v); }"
                             % (p, p, p))
+            elif kind == "ints" and t.startswith("const"):
+                # read-only int[] (device lists, slots, erased indices): copied out of the Java
+                # array before any critical region opens, never pinned, so a long export (a
+                # multi-GPU host batch) holds no GC-blocking pin ("pinning")
+                need = next(r[2] for r in rules if r[0] == "array" and r[1] == p)
+                pre.append("    int *%s_p = NULL;" % p)
+                copies.append("    if (st == ECX_OK && %s && !(%s_p = (int *)malloc(sizeof(int) * ((size_t)(%s) + 1))))"
+                              " st = ECX_E_NOMEM;" % (p, p, need))
+                copies.append("    if (st == ECX_OK && %s) (*env)->GetIntArrayRegion(env, %s, 0, (jsize)(%s), (jint *)%s_p);"
+                              % (p, p, need, p))
+                post.append("    free(%s_p);" % p)
+                args.append("%s_p" % p)
             elif kind in ("bytes", "ints", "shorts"):
                 cty = {"bytes": "uint8_t", "ints": "int", "shorts": "int16_t"}[kind]
                 mode = "JNI_ABORT" if t.startswith("const") else "0"
@@ -572,11 +584,13 @@ public final class EcxNative {
             body.extend(checks)
             body.extend(pre)
             body.extend(late)
+            body.extend(copies)
             body.extend(pin)
             pinned = [ln for ln in pin]
             if pinned:
                 # every PIN that returned NULL for a non-null array is an allocation failure
-                checks = ["(%s && !%s_p)" % (p, p) for (kind, _, _), t, p in kinds if kind in ("bytes", "ints", "shorts")]
+                checks = ["(%s && !%s_p)" % (p, p) for (kind, _, _), t, p in kinds
+                          if kind in ("bytes", "ints", "shorts") and not (kind == "ints" and t.startswith("const"))]
                 if checks:
                     body.append("    if (st == ECX_OK && (%s)) st = ECX_E_NOMEM;" % " || ".join(checks))
             body.append("    if (st == ECX_OK) st = %s;" % call)

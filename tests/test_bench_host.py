@@ -230,3 +230,63 @@ def test_e2e_host_expect_in_place_and_separate():
     hout[-1] ^= 0x80
     assert not c.host_expect(np.empty(0, np.uint8), hout, 3)
     assert c.pcie_bytes() == (20 * 32768, 8 * 32768)
+
+
+def test_e2e_host_budget_shrinks_with_world():
+    """The end-to-end leg's pinned host input per rank: E2E_HOST_BYTES for
+    one rank, a share of E2E_NODE_BYTES when the ranks of a node run it at once, and within
+    E2E_MEM_FRACTION of the free host memory in every case."""
+    per = [bench.e2e_host_budget(w) for w in (1, 2, 4, 8)]
+    assert per[0] == bench.E2E_HOST_BYTES
+    assert all(a >= b for a, b in zip(per, per[1:])) and per[3] < per[2] < per[1]
+    assert all(p * w <= max(bench.E2E_NODE_BYTES, bench.E2E_HOST_BYTES) for p, w in zip(per, (1, 2, 4, 8)))
+    free = 16 << 30  # a tight lease: 16 GiB free -> 4 GiB for all ranks together
+    capped = [bench.e2e_host_budget(w, free) for w in (1, 2, 4, 8)]
+    assert all(c * w <= free * bench.E2E_MEM_FRACTION for c, w in zip(capped, (1, 2, 4, 8)))
+    assert capped[3] == (4 << 30) // 8
+    mem = bench.host_memory_free()  # this container: MemAvailable is readable
+    assert mem["mem_available"] and mem["free"] and mem["free"] <= mem["mem_available"]
+
+
+class _FakeHostBuffer:
+    def __init__(self, nbytes):
+        import numpy as np
+        self.array = np.zeros(nbytes, np.uint8)
+
+
+def test_e2e_leg_fills_in_chunks_within_the_budget(monkeypatch):
+    """e2e_rate fills the pinned input from the pool in E2E_COPY_CHUNK steps (no full-size
+    .cpu() of the pool), takes at most the per-rank budget, verifies, and reports the cap
+    and the peak RSS (CPU tensors and a numpy HostBuffer stand in for HBM and pinned memory)."""
+    import numpy as np
+    import torch
+    monkeypatch.setattr(bench, "E2E_COPY_CHUNK", 1000)  # several steps per stripe
+    pool = torch.randint(0, 256, (40, 20, 64), dtype=torch.uint8)
+    wl = _bare(bench.RS173, pool=pool, L=64, P=40)
+    calls = []
+    wl.host_call = lambda ha, ho, n: calls.append(n)  # in place, so the host copy is already "encoded"
+    full = pool.numel()
+
+    class Ecx:
+        HostBuffer = _FakeHostBuffer
+    stripe = 20 * 64
+    monkeypatch.setattr(bench, "E2E_HOST_BYTES", 25 * stripe)
+    monkeypatch.setattr(bench, "E2E_NODE_BYTES", 50 * stripe)
+    r1 = bench.e2e_rate(Ecx, torch, wl, 0.01, world=1)
+    assert r1["verified"] and r1["stripes_per_call"] == 25 and r1["host_bytes"] == 25 * stripe < full
+    assert r1["host_cap"]["budget_bytes_per_rank"] == 25 * stripe and r1["peak_rss_bytes"] > 0
+    r8 = bench.e2e_rate(Ecx, torch, wl, 0.01, world=8)
+    assert r8["verified"] and r8["stripes_per_call"] == 50 // 8 and r8["host_bytes"] < r1["host_bytes"]
+    assert set(calls) == {25, 6}
+    # a stripe larger than a rank's share at N > 1 is skipped, with the reason and the cap
+    monkeypatch.setattr(bench, "E2E_NODE_BYTES", stripe)
+    r = bench.e2e_rate(Ecx, torch, wl, 0.01, world=8)
+    assert "skipped" in r and r["host_cap"]["world"] == 8
+
+
+def test_copy_chunked_round_trip():
+    import torch
+    src = torch.randint(0, 256, (12345,), dtype=torch.uint8)
+    dst = torch.zeros_like(src)
+    bench._copy_chunked(dst, src, chunk=1000)
+    assert torch.equal(dst, src)

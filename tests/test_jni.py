@@ -131,3 +131,25 @@ def test_no_public_native_takes_a_raw_host_address():
     for n in host_batch:
         body = re.search(r"JNICALL Java_%s_%s\(.*?\n\}" % (gen_jni.JCLASS, n), C_SRC, flags=re.S).group(0)
         assert body.count("direct_check(") == 2, n
+
+
+def test_no_read_only_int_array_is_pinned():
+    """a critical pin stalls the JVM's GC for as long as it is held, and
+    the multi-GPU host batches run for seconds.  Every read-only int[] (the device lists,
+    slot lists, erased indices) is copied with GetIntArrayRegion before any pin opens, and no
+    host-batch forwarder pins anything across its export call (its buffers are raw addresses
+    or direct ByteBuffers)."""
+    const_ints = {(name, p) for _ret, name, params in gen_jni.exports() for t, p in params
+                  if t.replace(" ", "") == "constint*"}
+    assert ("ecx_map_apply_batch_host_devices", "devices") in const_ints and len(const_ints) >= 7
+    fw = forwarders()
+    for name, p in const_ints:
+        body = fw["Java_%s_%s" % (gen_jni.JCLASS, gen_jni.camel(name))][1]
+        assert "PIN(%s)" % p not in body, (name, p)
+        copy = body.index("GetIntArrayRegion(env, %s, " % p)
+        first_pin = min([body.index(x) for x in ("PIN(", "buflist_pin(") if x in body] or [len(body)])
+        assert copy < first_pin < len(body) or first_pin == len(body), (name, p)
+        assert "free(%s_p);" % p in body
+    for jname, (_n, body) in fw.items():
+        if "BatchHost" in jname:
+            assert "PIN(" not in body and "buflist_pin(" not in body and "Critical" not in body, jname
