@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--stripes-per-step", type=int, default=None, help="default: per workload (2^20 for clay42)")
     ap.add_argument("--pool", type=int, default=None, help="resident stripes per GPU (clay42: 2^15 = 48 GiB)")
     ap.add_argument("--erased", type=int, default=None, help="erased node (clay42: 1, README '1 LP 1 pipeline')")
+    ap.add_argument("--sub-bytes", type=int, default=None,
+                    help="clay104: bytes per sub-chunk (CLAY_BLOCK_SIZE). Default 4096: 1 MiB node blocks of 256 "
+                         "sub-chunks; 1048576 is config 4's other reading, 1 MiB sub-chunks (256 MiB node blocks)")
     ap.add_argument("--pitch-pad", type=int, default=0,
                     help="rs124: bytes of padding per 4 MiB shard (default 0: the natural contiguous [S][16][4 MiB] layout)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -114,6 +117,14 @@ def parse():
                                                  "kernel-source hash) as JSON here (scripts/pmc.sh)")
     args = ap.parse_args()
     _metric, pool, per_step = WORKLOADS[args.workload]
+    if args.sub_bytes is not None and args.workload != "clay104":
+        ap.error("--sub-bytes applies to --workload clay104 only")
+    if args.workload == "clay104" and args.sub_bytes and args.sub_bytes != Clay104.b:
+        # the same 2^15 x 1,088 x 4 KiB of algorithmic bytes per step, over a pool of 16 stripes
+        # (56 GiB at 1 MiB sub-chunks) instead of 2,048
+        scale = args.sub_bytes / Clay104.b
+        pool = max(1, min(16, int(2 * pool / scale)))
+        per_step = max(pool, int(per_step / scale))
     args.pool = args.pool or pool
     args.stripes_per_step = args.stripes_per_step or per_step
     if args.erased is None:
@@ -174,6 +185,7 @@ def host_cpu_info() -> dict:
             "l3_bytes_machine": l3_all or None, "l3_bytes_affinity": l3_aff or None}
 
 
+CPU_ARENA_BYTES = 8 << 30  # host bytes of unit copies the CPU baseline may allocate (see cpu_baseline)
 # BASELINE.md section 4's measurement protocol (ReedSolomonBenchmark.java:104-124)
 REF_WARMUPS, REF_MEASUREMENTS, REF_SECONDS = 2, 10, 2.0
 
@@ -221,12 +233,23 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
     # unit has its own memory (the cache sees the whole working set).
     distinct = list(units) if units else spec["make"](np.random.default_rng(0))
     data_kind = "GPU-pool" if units else spec["data_kind"]
-    arena = np.empty((n_units,) + distinct[0].shape, np.uint8)
-    for u in range(n_units):
-        arena[u] = distinct[u % len(distinct)]
-    slot_bytes = arena.shape[-1]
+    # Units far larger than the L3 (Clay(10,4) at 1 MiB sub-chunks: 3.5 GiB) are not copied
+    # per unit: when n_units copies would exceed CPU_ARENA_BYTES, the units the oracle only
+    # reads (read_only_units) alias the distinct ones, each still >> L3 (the DRAM-streaming
+    # premise of ReedSolomonBenchmark.java:25-33 holds per unit).
+    n_arena = n_units
+    if n_units * distinct[0].nbytes > CPU_ARENA_BYTES and spec.get("read_only_units"):
+        n_arena = max(1, min(len(distinct), CPU_ARENA_BYTES // distinct[0].nbytes))
+    if n_arena < n_units:
+        arena_units = [np.ascontiguousarray(d) for d in distinct[:n_arena]]
+    else:
+        arena = np.empty((n_units,) + distinct[0].shape, np.uint8)
+        for u in range(n_units):
+            arena[u] = distinct[u % len(distinct)]
+        arena_units = list(arena)
+    slot_bytes = distinct[0].shape[-1]
     zero = np.zeros(slot_bytes, np.uint8)  # a shared zero-filled node (shortened Clay's virtual nodes)
-    rows = np.arange(n_units, dtype=np.int64)[:, None] * arena[0].nbytes + arena.ctypes.data
+    rows = np.array([arena_units[u % n_arena].ctypes.data for u in range(n_units)], np.int64)[:, None]
     addrs = np.where(spec["present"][None, :] == 1, rows + spec["arena_slot"][None, :] * slot_bytes,
                      np.where(spec["present"][None, :] == 2, zero.ctypes.data, 0)).astype(np.int64)
     op, data, parity, erased = spec["op"], spec["data"], spec["parity"], spec["erased"]
@@ -255,6 +278,9 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
                   f"{n_units} units in {el1:.1f} s")
         measurements = None
     ws = n_units * unit_bytes
+    alias = ("" if n_arena == n_units else
+             "; the %d units alias %d distinct %.1f GiB host units (read-only, each >> L3)"
+             % (n_units, n_arena, distinct[0].nbytes / 2**30))
     out = {
         "value": round(allv, 3),
         "unit": "GiB/s",
@@ -268,7 +294,7 @@ def cpu_baseline(wl, seconds: float, sample=None, max_units=None, units=None, pr
         "sample": f"{spec['what']}, stage-by-stage C restatement of the reference JVM path (oracle/), "
                   f"lease quota {info['cgroup_quota_cpus']} of {info['cpus_present']} CPUs (affinity "
                   f"{info['affinity_cpus']}), {per_thread} host-resident {data_kind} units per thread, "
-                  f"{ws / 2**20:.0f} MiB of algorithmic bytes touched (>= 2x the {l3 / 2**20:.0f} MiB L3): {timing}; "
+                  f"{ws / 2**20:.0f} MiB of algorithmic bytes touched (>= 2x the {l3 / 2**20:.0f} MiB L3){alias}: {timing}; "
                   f"{info['model']}",
     }
     if measurements:
@@ -647,10 +673,15 @@ class Clay42x2(Clay42):
 
 class Clay104(Workload):
     """Config 4: shortened Clay(10,4) (Clay(12,4) with 2 virtual zero data nodes),
-    1 MiB node blocks = 256 planes x 4 KiB sub-chunks, single-node repair."""
+    single-node repair.  Its "1 MiB blocks" is read two ways: 1 MiB
+    node blocks = 256 planes x 4 KiB sub-chunks (the default, b = 4096), or 1 MiB
+    sub-chunks, CLAY_BLOCK_SIZE in the sense of PipelineUtil.kt:13-28 (b = 1 MiB, a
+    256 MiB node block, --sub-bytes 1048576)."""
     k, m, v, b, alpha = 10, 4, 2, 4096, 256
 
-    def __init__(self, ecx, torch, dev, P, erased, seed):
+    def __init__(self, ecx, torch, dev, P, erased, seed, sub_bytes=None):
+        if sub_bytes:
+            self.b = sub_bytes
         k, m, v, b, a = self.k, self.m, self.v, self.b, self.alpha
         n = k + m
         self.P, self.erased, self.torch, self.n = P, erased, torch, n
@@ -668,8 +699,10 @@ class Clay104(Workload):
         self.write_bytes = info["n_out"] * b
         self.reads, self.writes = info["n_in"], info["n_out"]
         self.region = self.pool
+        blocks = ("1 MiB node blocks = 256 x 4096-B sub-chunks" if b == 4096 else
+                  "CLAY_BLOCK_SIZE=%d: %d-B sub-chunks, %d MiB node blocks" % (b, b, a * b >> 20))
         self.description = ("Clay(10,4) (shortened Clay(12,4), 2 virtual nodes) single-node repair (erased node %d), "
-                            "1 MiB node blocks = 256 x 4096-B sub-chunks" % erased)
+                            "%s" % (erased, blocks))
 
     def launch(self):
         n, a, b = self.n, self.alpha, self.b
@@ -713,13 +746,14 @@ class Clay104(Workload):
                 present.append(2 if virtual else (0 if u == e_u else 1))
 
         def make(rng):  # random bytes: the oracle's work does not depend on the data
-            return [rng.integers(0, 256, (n_r * a, self.b), dtype=np.uint8) for _ in range(2)]
+            return [rng.integers(0, 256, (n_r * a, self.b), dtype=np.uint8)
+                    for _ in range(1 if n_r * a * self.b > CPU_ARENA_BYTES // 2 else 2)]
         return {"op": O.BENCH_CLAY, "data": k + v, "parity": m, "erased": [e_u], "make": make,
                 "arena_slot": np.array(arena_slot, np.int64), "present": np.array(present, np.int64),
                 "data_kind": "random-byte",
                 "what": "Clay(10,4) repairs of node %d as the reference runs them: Clay(12,4) with the 2 virtual "
-                        "data nodes zero-filled, 256 x 4 KiB sub-chunks; GiB/s over the shortened map's "
-                        "algorithmic bytes" % self.erased}
+                        "data nodes zero-filled, 256 x %d-B sub-chunks; GiB/s over the shortened map's "
+                        "algorithmic bytes" % (self.erased, self.b), "read_only_units": True}
 
 
 class RS124(Workload):
@@ -1158,7 +1192,7 @@ def main():
     if args.workload == "clay42":
         wl = Clay42(ecx, torch, dev, P, args.erased, seed)
     elif args.workload == "clay104":
-        wl = Clay104(ecx, torch, dev, P, args.erased, seed)
+        wl = Clay104(ecx, torch, dev, P, args.erased, seed, args.sub_bytes)
     elif args.workload == "clay42x2":
         wl = Clay42x2(ecx, torch, dev, P, args.erased, seed)
     elif args.workload == "rs124":
@@ -1288,7 +1322,7 @@ def main():
     sample = units = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the contract: rank 0 at N=1 only
         sample = wl.sample()  # one pool unit for the oracle check
-        units = wl.host_units(8 if wl.unit_bytes < (64 << 20) else 2)  # the GPU run's own stripes
+        units = wl.host_units(8 if wl.unit_bytes < (64 << 20) else (2 if wl.unit_bytes < (1 << 30) else 1))
     probes = memory_probes(ecx, torch, wl.region, wl.reads, wl.writes) if not args.no_probes else None
 
     cpu = None

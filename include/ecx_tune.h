@@ -58,7 +58,9 @@
  *                      rules' shape, 4 KiB and one-wave workgroups, skewed chunks, staggered stripes,
  *                      5 timings each, events read without blocking on later calls -- and the fastest
  *                      median is kept (default; every candidate computes the same bytes, nothing extra
- *                      is launched); 0 = the static rules only (skew on 4 MiB-multiple pitches, one
+ *                      is launched).  Any kept shape is re-validated once, 512 launches later, against
+ *                      its alternative: the static rules for a non-static choice, the runner-up for a
+ *                      static one.  0 = the static rules only (skew on 4 MiB-multiple pitches, one
  *                      wave for <= 2-row maps over >= 8 inputs)
  *   "wide_tiles"       multi-tile maps: pairs of 8-row tiles that share inputs in one workgroup
  *                      (16 accumulator rows, each shared input loaded once).  1 = when pairing
@@ -90,6 +92,9 @@
  *                      after every node -- 119 VGPRs and 4 waves per SIMD instead of 154 and 3; 2 =
  *                      every load of a unit issued up front, the accumulators pinned (151 VGPRs;
  *                      default)
+ *   "rtc_wide"         the plane-group kernel's load addresses: 0 = 32-bit buffer offsets, and 64-bit
+ *                      flat addresses only where a stripe's slot offsets exceed 31 bits (1 MiB sub-chunks
+ *                      of Clay(10,4), default); 1 = 64-bit on every layout (A/B, tests)
  *   "rtc_nt"           non-temporal loads in the generated Clay kernels, bits: plane-group kernel --
  *                      1 the sub-chunks read once (rows ya and yb, the column mates), 2 the row-yc
  *                      own sub-chunks (re-read as partners by the neighbouring plane groups), 4 the
@@ -175,6 +180,9 @@
 extern "C" {
 #endif
 int ecx_tune(const char *key, int value); /* 0, or ECX_E_ILLEGAL_ARGUMENT for an unknown key */
+/* The current value of a DEPLOYMENT key (in ecx_tune's units, e.g. "host_exec_kib" in KiB) into
+ * *value: 0, or ECX_E_ILLEGAL_ARGUMENT for a shape key, an unknown key or a null pointer. */
+int ecx_tune_value(const char *key, int *value);
 /* 1 in the diagnostic library (make DIAG=1, libecx_diag.so), 0 in the product library. */
 int ecx_build_diag(void);
 /* The per-call host executor's instruction set ("host_exec_kib"): 2 AVX-512BW + GFNI, 1 AVX2,
@@ -205,7 +213,8 @@ int ecx_map_layout_choice(const struct ecx_map *map, int64_t slot_pitch, float *
 /* State of that layout's selection: -1 none yet, 0 exploring, 1 chosen, 2 re-validating, 3
  * re-validated (final), 4 contended (probes kept overlapping other streams' launches: the static
  * rules, untimed); `dropped` = timing probes discarded because another stream of the device
- * launched while they were in flight.  Either pointer may be NULL. */
+ * launched between the probing stream's previous launch and the probe's end (a launch that
+ * finds the probe already finished does not count).  Either pointer may be NULL. */
 int ecx_map_layout_state(const struct ecx_map *map, int64_t slot_pitch, int *state, int *dropped);
 /* The kernel instance of the last full-chunk launch this thread enqueued, named as
  * rocprofv3 names it (e.g. "k_gf_apply<false, true, 1, 20, false, 256, 8>"), copied

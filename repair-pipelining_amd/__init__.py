@@ -211,6 +211,15 @@ def tune(key: str, value: int) -> None:
     check(f(key.encode(), int(value)))
 
 
+def tune_value(key: str) -> int:
+    """The current value of a deployment knob (ecx_tune_value, include/ecx_tune.h)."""
+    f = lib().ecx_tune_value
+    f.argtypes, f.restype = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], ctypes.c_int
+    v = ctypes.c_int()
+    check(f(key.encode(), ctypes.byref(v)))
+    return v.value
+
+
 def is_diag() -> bool:
     """True for the diagnostic library (make DIAG=1, libecx_diag.so): it also holds the
     measured-and-rejected kernels, whose ecx_tune keys the product library refuses."""

@@ -85,13 +85,11 @@ void launch_check_k(dim3 grid, hipStream_t stream, const ApplyArgs &a) {
 }
 }  // namespace
 
-// verdict[s] = 1 when every parity shard of stripe s equals the parity of its
-// data over bytes [0, nbytes) of each slot, else 0.  `cm` is a check map (rows = syndromes).
-void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
-                  uint8_t *verdict, int64_t nstripes, int64_t nbytes, hipStream_t stream) {
-    if (nstripes <= 0) return;
-    check_hip(hipMemsetAsync(verdict, 1, (size_t)nstripes, stream), "hipMemsetAsync (verdicts)");
-    if (nbytes <= 0 || cm.map().n_out == 0) return;
+namespace {
+// Clears verdict[s] when a syndrome byte of stripe s over bytes [0, nbytes) is non-zero (the
+// verdicts were set to 1 by launch_check).
+void launch_check_core(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                       uint8_t *verdict, int64_t nstripes, int64_t nbytes, hipStream_t stream) {
     // Ring depth 4 (forced 8 / 20 with ecx_tune "depth"): on RS(17,3) 200,000-B shards depth 4 reads
     // 0.83 of HBM, depth 8 and 20 0.80 -- the short ring leaves registers for more resident waves
     // (profiles/r05_check_sweep.jsonl).  Accumulator rows: 4 when every tile has at most 4 (RS with
@@ -161,9 +159,29 @@ void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         set_last_shape_order("stagger=" + std::to_string(a.stagger) + " xcd_group=" + std::to_string(a.xcd_group) +
                              " xcd_run=" + std::to_string(a.xcd_group == 3 ? a.xcd_run : 0));
     check_hip(hipGetLastError(), "k_gf_check launch");
+}
+}  // namespace
+
+// verdict[s] = 1 when every parity shard of stripe s equals the parity of its
+// data over bytes [0, nbytes) of each slot, else 0.  `cm` is a check map (rows = syndromes).
+// A start that is not 16-B aligned (isParityCorrect's firstByte may be anything) on 16-B
+// strides: the bytes up to the first 16-B boundary go to the byte-safe kernel, the rest to the
+// vectorised one, so only the head (< 16 B per slot) pays the byte-safe rate.
+void launch_check(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
+                  uint8_t *verdict, int64_t nstripes, int64_t nbytes, hipStream_t stream) {
+    if (nstripes <= 0) return;
+    check_hip(hipMemsetAsync(verdict, 1, (size_t)nstripes, stream), "hipMemsetAsync (verdicts)");
+    if (nbytes <= 0 || cm.map().n_out == 0) return;
+    const int64_t head = (int64_t)((16 - (uintptr_t)in % 16) % 16);
+    if (head > 0 && head < nbytes && in_stripe_stride % 16 == 0 && in_slot_stride % 16 == 0) {
+        launch_check_core(cm, in, in_stripe_stride, in_slot_stride, verdict, nstripes, head, stream);
+        launch_check_core(cm, in + head, in_stripe_stride, in_slot_stride, verdict, nstripes, nbytes - head, stream);
+    } else {
+        launch_check_core(cm, in, in_stripe_stride, in_slot_stride, verdict, nstripes, nbytes, stream);
+    }
     int dev = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
-    note_device_launch(dev, stream);
+    note_device_launch(dev, stream, nstripes * nbytes * cm.map().n_in);
 }
 
 }  // namespace ecx

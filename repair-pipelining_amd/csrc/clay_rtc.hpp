@@ -51,6 +51,10 @@ struct RtcShape {
     // by the neighbouring plane groups), 4 the row-yc partner loads; per-plane kernel -- 8: every
     // load (its own sub-chunks are re-read as partners, from L2)
     int nt = 5;
+    // plane-group kernel: 64-bit load addresses (flat global loads) instead of 32-bit buffer
+    // offsets, for layouts whose input slot offsets exceed 31 bits (1 MiB sub-chunks: a 3.5 GiB
+    // Clay(10,4) stripe).  Set by the launcher from the layout, not a tuning knob.
+    int wide = 0;
 };
 
 // HIP source of the kernel `k_clay_repair` for this program (exposed for tests).

@@ -957,8 +957,12 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
             if (ClayRtc *r = clay_rtc(clay)) {
                 // auto: a generated kernel that cannot be compiled or loaded here (no
                 // hiprtc, another target) falls back to the composed map; forced (2) throws
-                const RtcShape sh = rtc_current_shape();
-                if ((int64_t)r->program().max_in_slot * in_sub_stride + kChunkBytes <= 0x7FFFFFFF &&
+                RtcShape sh = rtc_current_shape();
+                // slot offsets beyond 31 bits (1 MiB sub-chunks of Clay(10,4)): the plane-group
+                // kernel with 64-bit load addresses; the per-plane kernel has no such form
+                const bool narrow = (int64_t)r->program().max_in_slot * in_sub_stride + kChunkBytes <= 0x7FFFFFFF;
+                if (!narrow) sh.wide = 1;
+                if ((narrow || (clay_grp_supported(r->program()) && sh.group)) &&
                     (rtc_mode == 2 || r->available(sh, (hipStream_t)stream))) {
                     done = buf_size / kChunkBytes * kChunkBytes;
                     r->launch(sh, in, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride,
@@ -966,7 +970,7 @@ int ecx_clay_perform_coding_batch(ecx_clay *clay, const uint8_t *in, int64_t in_
                     rtc_kernel = r->kernel_name(sh);
                     int dev = 0;
                     check_hip(hipGetDevice(&dev), "hipGetDevice");
-                    note_device_launch(dev, (hipStream_t)stream);
+                    note_device_launch(dev, (hipStream_t)stream, nstripes * done * (int64_t)(r->program().max_in_slot + 1));
                 }
             }
         }
@@ -1335,6 +1339,10 @@ int set_tune(Tuning &t, const std::string &k, int value) {
         if (value < 0 || value > 2) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_sched = value;
     }
+    else if (k == "rtc_wide") {
+        if (value < 0 || value > 1) return ECX_E_ILLEGAL_ARGUMENT;
+        t.rtc_wide = value;
+    }
     else if (k == "rtc_nt") {
         if (value < 0 || value > 15) return ECX_E_ILLEGAL_ARGUMENT;
         t.rtc_nt = value;
@@ -1401,6 +1409,22 @@ int ecx_tune(const char *key, int value) {
     int rc = ECX_OK;
     update_tuning([&](Tuning &t) { rc = set_tune(t, k, value); });
     return rc;
+}
+
+int ecx_tune_value(const char *key, int *value) {
+    const std::string k = key ? key : "";
+    if (!value || !deployment_key(k)) return ECX_E_ILLEGAL_ARGUMENT;
+    const Tuning t = tuning();
+    if (k == "host_chunk_kib") *value = (int)(t.host_chunk >> 10);
+    else if (k == "host_buffers") *value = t.host_buffers;
+    else if (k == "host_gather_kib") *value = (int)(t.host_gather_max >> 10);
+    else if (k == "host_zero_copy") *value = t.host_zero_copy;
+    else if (k == "host_contexts") *value = t.host_contexts;
+    else if (k == "host_exec_kib") *value = (int)(t.host_exec_max >> 10);
+    else if (k == "roctx") *value = g_roctx.load();
+    else if (k == "plan_cache") *value = t.plan_cache;
+    else *value = t.layout_select;  // deployment_key: the only one left
+    return ECX_OK;
 }
 
 int ecx_probe_bandwidth(int kind, const uint8_t *src, uint8_t *dst, int64_t nbytes, int nontemporal, void *stream) {

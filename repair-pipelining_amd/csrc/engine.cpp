@@ -420,11 +420,13 @@ const uint8_t *zero_page_for_current_device() {
 }
 
 CompiledMap::~CompiledMap() {
-    for (auto &kv : layout_sel_)
+    for (auto &kv : layout_sel_) {
         for (auto &p : kv.second.pending) {
+            if (p.e1) close_probe(p.dev, p.e1);
             if (p.e0) (void)hipEventDestroy(p.e0);
             if (p.e1) (void)hipEventDestroy(p.e1);
         }
+    }
     for (auto &kv : dev_) {
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) continue;
@@ -695,18 +697,72 @@ float median_of(std::vector<float> v) {
     return v.empty() ? -1.f : v[v.size() / 2];
 }
 
+// A filled layout probe still open to contamination: until a launch on another stream of its
+// device finds its end event done, such a launch may share the GPU with it (`dirty`).
+struct OpenProbe {
+    hipStream_t stream;
+    hipEvent_t e1;
+    std::shared_ptr<std::atomic<bool>> dirty;
+};
+// A stream's launches: the latest one's serial, and an event recorded behind its latest LARGE
+// launch (>= kMarkBytes of input), so a probe can tell whether one may still run.  A smaller
+// launch runs for microseconds, negligible against a multi-millisecond probe, and is not marked.
+struct StreamMark {
+    uint64_t serial = 0;
+    hipEvent_t done = nullptr;
+    bool marked = false;  // `done` was recorded behind a large launch of this stream
+};
+constexpr int64_t kMarkBytes = 64 << 20;
+constexpr uint64_t kUnmarkedLarge = 1ull << 63;  // serial flag: a large launch whose event failed
 struct DevLaunches {
     uint64_t serial = 0;
-    std::map<hipStream_t, uint64_t> last;  // stream -> serial of its latest launch
+    std::map<hipStream_t, StreamMark> last;  // aged out, below
+    std::vector<OpenProbe> open;
 };
+constexpr uint64_t kStreamAge = 4096;  // a stream silent for this many launches leaves `last`
 std::mutex g_launch_mu;
 std::map<int, DevLaunches> g_launches;
 }  // namespace
 
-uint64_t note_device_launch(int dev, hipStream_t s) {
+uint64_t note_device_launch(int dev, hipStream_t s, int64_t bytes) {
     std::lock_guard<std::mutex> lk(g_launch_mu);
     DevLaunches &d = g_launches[dev];
-    d.last[s] = ++d.serial;
+    StreamMark &mk = d.last[s];
+    mk.serial = ++d.serial;
+    if (bytes >= kMarkBytes) {
+        if (!mk.done && hipEventCreateWithFlags(&mk.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            mk.done = nullptr;
+        }
+        // unmarked when the record fails: this large launch then counts as possibly running
+        mk.marked = mk.done && hipEventRecord(mk.done, s) == hipSuccess;
+        if (!mk.marked) {
+            (void)hipGetLastError();
+            mk.serial |= kUnmarkedLarge;
+        }
+    }
+    // An open probe on another stream, at a large launch: still running -> this launch may
+    // overlap it (dirty); finished -> no later launch can, so its window closes here.  Either way
+    // it leaves the list.
+    for (auto it = d.open.begin(); bytes >= kMarkBytes && it != d.open.end();) {
+        if (it->stream == s) {  // same stream: queued behind the probe
+            ++it;
+            continue;
+        }
+        const hipError_t q = hipEventQuery(it->e1);
+        if (q == hipErrorNotReady) it->dirty->store(true);
+        else if (q != hipSuccess) (void)hipGetLastError();
+        it = d.open.erase(it);
+    }
+    if (d.serial % 256 == 0)  // bounded: streams not seen for kStreamAge launches are forgotten
+        for (auto it = d.last.begin(); it != d.last.end();) {
+            if ((it->second.serial & ~kUnmarkedLarge) + kStreamAge >= d.serial) {
+                ++it;
+                continue;
+            }
+            if (it->second.done) (void)hipEventDestroy(it->second.done);
+            it = d.last.erase(it);
+        }
     return d.serial;
 }
 
@@ -715,16 +771,44 @@ uint64_t stream_last_launch(int dev, hipStream_t s) {
     auto it = g_launches.find(dev);
     if (it == g_launches.end()) return 0;
     auto jt = it->second.last.find(s);
-    return jt == it->second.last.end() ? 0 : jt->second;
+    return jt == it->second.last.end() ? 0 : jt->second.serial & ~kUnmarkedLarge;
 }
 
-bool other_stream_launched_since(int dev, hipStream_t s, uint64_t since) {
+bool other_stream_may_run(int dev, hipStream_t s, uint64_t since) {
     std::lock_guard<std::mutex> lk(g_launch_mu);
     auto it = g_launches.find(dev);
     if (it == g_launches.end()) return false;
-    for (const auto &kv : it->second.last)
-        if (kv.first != s && kv.second > since) return true;
+    for (const auto &kv : it->second.last) {
+        if (kv.first == s) continue;
+        const StreamMark &mk = kv.second;
+        if (mk.serial & kUnmarkedLarge) {  // a large launch without an event: assume it may run
+            if ((mk.serial & ~kUnmarkedLarge) > since) return true;
+        } else if (mk.marked) {  // its latest large launch: running iff the event is not done
+            const hipError_t q = hipEventQuery(mk.done);
+            if (q == hipErrorNotReady) return true;
+            if (q != hipSuccess) (void)hipGetLastError();
+        }
+    }
     return false;
+}
+
+std::shared_ptr<std::atomic<bool>> open_probe(int dev, hipStream_t s, hipEvent_t e1, bool dirty) {
+    auto flag = std::make_shared<std::atomic<bool>>(dirty);
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    if (!dirty) g_launches[dev].open.push_back({s, e1, flag});
+    return flag;
+}
+
+void close_probe(int dev, hipEvent_t e1) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    auto it = g_launches.find(dev);
+    if (it == g_launches.end()) return;
+    auto &v = it->second.open;
+    for (auto jt = v.begin(); jt != v.end(); ++jt)
+        if (jt->e1 == e1) {
+            v.erase(jt);
+            return;
+        }
 }
 
 // Reads the finished probes of `s` (non-blocking): clean timings go to the exploration's
@@ -742,8 +826,9 @@ void CompiledMap::harvest(LayoutSel &s, int n_cand) {
         }
         float ms = 0.f;
         const bool timed = q == hipSuccess && hipEventElapsedTime(&ms, it->e0, it->e1) == hipSuccess && ms > 0.f;
+        close_probe(it->dev, it->e1);  // before its events go
         if (!timed) (void)hipGetLastError();  // a failed probe is dropped; its candidate is timed again
-        else if (other_stream_launched_since(it->dev, it->stream, it->since)) ++s.dropped;
+        else if (it->dirty && it->dirty->load()) ++s.dropped;
         else if (s.state == kLayoutRevalidating) {
             if (it->cand == s.reval_alt) s.reval_ms[0].push_back(ms);
             else if (it->cand == s.chosen) s.reval_ms[1].push_back(ms);
@@ -760,13 +845,14 @@ int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand,
                                   hipStream_t stream, uint64_t *ticket) {
     std::lock_guard<std::mutex> lk(mu_);
     *ticket = 0;
-    if (!layout_sel_.count(key) && layout_sel_.size() >= kMaxLayouts) return 0;  // bounded: the static rules
+    const bool fresh = !layout_sel_.count(key);
+    if (fresh && layout_sel_.size() >= kMaxLayouts) return 0;  // bounded: the static rules
     LayoutSel &s = layout_sel_[key];
     if ((int)s.ms.size() != n_cand) s.ms.assign(n_cand, {});
     harvest(s, n_cand);  // also after the choice, so late probes free their events
     auto reserve = [&](int cand) {
         *ticket = ++ticket_serial_;
-        s.pending.push_back({cand, nullptr, nullptr, *ticket, dev, stream, stream_last_launch(dev, stream)});
+        s.pending.push_back({cand, nullptr, nullptr, *ticket, dev, stream, stream_last_launch(dev, stream), nullptr});
         return cand;
     };
     auto in_flight = [&](int cand) {
@@ -797,7 +883,7 @@ int CompiledMap::next_layout_pick(const std::array<int64_t, 8> &key, int n_cand,
             if (!keep) s.chosen = s.reval_alt;
             s.state = kLayoutRevalidated;
             s.serial = ++layout_serial_;
-            return s.chosen;
+                return s.chosen;
         }
         if (have[0] >= samples && have[1] >= samples) return s.chosen;  // all in flight: untimed
         return reserve(have[0] <= have[1] ? s.reval_alt : s.chosen);
@@ -844,6 +930,9 @@ void CompiledMap::fill_layout_probe(const std::array<int64_t, 8> &key, uint64_t 
         if (p.ticket == ticket) {
             p.e0 = e0;
             p.e1 = e1;
+            // contaminated already if another stream's latest launch may still run as the probe
+            // is enqueued; later launches are judged by note_device_launch while it is open
+            p.dirty = open_probe(p.dev, p.stream, e1, other_stream_may_run(p.dev, p.stream, p.since));
             return;
         }
     (void)hipEventDestroy(e0);  // not reserved (cannot happen): drop the events

@@ -23,6 +23,7 @@
 #endif
 
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -155,15 +156,18 @@ public:
     // Per-layout launch-shape selection (kernels.hip launch_apply, ecx_tune "layout_select"):
     // the candidate to run for this call of the batch layout `key` on `stream` of device `dev`.
     // Finished timing probes are harvested first (non-blocking).  A probe is DROPPED, not
-    // counted, when another stream of the same device enqueued a libecx launch between this
-    // stream's previous launch and the harvest (note_device_launch): its kernel may have shared
-    // the GPU with the probe.  Once every one of the n_cand candidates has `samples` clean
+    // counted, when another stream of the same device had a large libecx launch that may still
+    // run when the probe was enqueued, or enqueued one while the probe was still running (the
+    // first such launch that finds the probe's end event done closes its window;
+    // note_device_launch): that kernel may have shared the GPU with the probe.  Once every
+    // one of the n_cand candidates has `samples` clean
     // timings the fastest median is kept (candidate 0 -- the static rules -- unless another is
     // faster by kLayoutMargin); after kLayoutMaxDropped dropped probes the layout is CONTENDED
-    // and keeps candidate 0 untimed.  A kept shape other than the static rules is re-validated
-    // once, after kLayoutRevalidate further launches: `samples` clean timings each of it and
-    // of the static rules, and the static rules return unless the kept shape still wins by the
-    // margin.  At most kMaxLayouts layouts are selected per map (later ones get candidate 0,
+    // and keeps candidate 0 untimed.  Any kept shape is re-validated once, after
+    // kLayoutRevalidate further launches, against its alternative -- the static rules for a
+    // non-static choice, the runner-up for a static one: `samples` clean timings of each, and
+    // the alternative takes over if it wins by the margin (a non-static choice must keep
+    // beating the static rules by it).  At most kMaxLayouts layouts are selected per map (later ones get candidate 0,
     // untimed).  When the call is to be timed, *ticket is set to a non-zero probe slot
     // reserved in the layout's pending list (so concurrent callers are never handed the same
     // probe twice): the caller brackets its launch with two events on `stream` and hands them
@@ -189,6 +193,7 @@ private:
             int dev;
             hipStream_t stream;
             uint64_t since;      // the stream's last launch serial before this probe (note_device_launch)
+            std::shared_ptr<std::atomic<bool>> dirty;  // set when another stream's launch may overlap it
         };
         std::vector<std::vector<float>> ms;  // per candidate: clean launch times of its probes
         std::vector<Probe> pending;          // reserved or unfinished probes
@@ -327,6 +332,8 @@ struct Tuning {
     int rtc_sched = 2;      // plane-group kernel load schedule: 0 = rtc_lookahead's, 1 = lean, 2 = all loads
                             // up front with pinned accumulators (+0.8-2.4 % over 0 on two boxes,
                             // profiles/r03_clay104_final.jsonl, r03_clay104_lean_run2.jsonl)
+    int rtc_wide = 0;       // plane-group kernel: 1 = 64-bit load addresses on every layout (auto, 0: only
+                            // where slot offsets exceed 31 bits, RtcShape::wide)
     int rtc_nt = 5;         // non-temporal loads in the generated Clay kernels (RtcShape::nt bits):
                             // 5 = the plane-group kernel's read-once rows and row-yc partner loads,
                             // +3-6 % on Clay(10,4) over cached loads (profiles/r03_clay104_nt.jsonl)
@@ -386,12 +393,20 @@ void note_kernel(const char *name, P... params) {
 
 // Per-device launch registry (engine.cpp), read by the layout selection's contamination check:
 // every batch launch of the library (launch_apply, launch_check, the generated Clay kernels)
-// records its stream here.  note_device_launch returns the launch's serial; stream_last_launch
-// the serial of a stream's latest launch (0 = none); other_stream_launched_since whether a
-// stream other than `s` on device `dev` launched after serial `since`.
-uint64_t note_device_launch(int dev, hipStream_t s);
+// records its stream and input bytes here.  note_device_launch returns the launch's serial and,
+// for a launch of >= 64 MiB, records an event behind it (smaller launches run for microseconds
+// and never count as overlapping a probe); stream_last_launch is the serial of a stream's latest
+// launch (0 = none); other_stream_may_run whether a stream other than `s` on device `dev` has a
+// large launch that may still run (its event is not done; or no event could be recorded and it
+// came after `since`).  Streams unseen for 4,096 launches age out of the registry.
+uint64_t note_device_launch(int dev, hipStream_t s, int64_t bytes);
 uint64_t stream_last_launch(int dev, hipStream_t s);
-bool other_stream_launched_since(int dev, hipStream_t s, uint64_t since);
+bool other_stream_may_run(int dev, hipStream_t s, uint64_t since);
+// A layout probe whose end event `e1` is recorded on `s`: registered (unless already `dirty`)
+// so that note_device_launch on another stream of `dev` flags it while it runs; close_probe
+// unregisters it before its events are destroyed.
+std::shared_ptr<std::atomic<bool>> open_probe(int dev, hipStream_t s, hipEvent_t e1, bool dirty);
+void close_probe(int dev, hipEvent_t e1);
 
 // Enqueue out = M * in over nstripes stripes (kernels.hip).
 // The launch_apply_core pick of per-layout candidate `cand` (kernels.hip kLayoutCand):

@@ -199,11 +199,46 @@ bool apply_rows(const LinearMap &m, const uint8_t *const *inputs, uint8_t *const
 
 }  // namespace
 
+namespace {
+// [a, a + n) and [b, b + n) share a byte but start at different addresses
+bool shifted_overlap(const uint8_t *a, const uint8_t *b, int64_t n) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return x != y && x < y + (uintptr_t)n && y < x + (uintptr_t)n;
+}
+}  // namespace
+
 void host_exec_apply(const LinearMap &m, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
                      int64_t byte_count) {
     for (int slot : m.out_slot)
         if (!outputs[slot]) throw Error(ECX_E_NULL, "output buffer is null");
-    (void)apply_rows(m, inputs, outputs, offset, byte_count, false);
+    // Block by block every row is computed before any is stored, so an output may BE an input
+    // (the same address).  An output that overlaps an input at a shifted address would overwrite
+    // input bytes a later block still reads: such inputs are read from a copy taken first, as the
+    // device path stages every input before it writes anything.
+    int max_in = 0;
+    for (int slot : m.in_slot) max_in = std::max(max_in, slot);
+    thread_local std::vector<const uint8_t *> ins;
+    thread_local std::vector<uint8_t> copies;
+    ins.assign(inputs, inputs + max_in + 1);
+    std::vector<int> shifted;
+    for (int j = 0; j < m.n_in; ++j) {
+        const int slot = m.in_slot[j];
+        if (!inputs[slot]) continue;
+        for (int slot_o : m.out_slot)
+            if (shifted_overlap(inputs[slot] + offset, outputs[slot_o] + offset, byte_count)) {
+                if (std::find(shifted.begin(), shifted.end(), slot) == shifted.end()) shifted.push_back(slot);
+                break;
+            }
+    }
+    if (!shifted.empty()) {
+        copies.resize(shifted.size() * (size_t)byte_count);
+        for (size_t i = 0; i < shifted.size(); ++i) {
+            uint8_t *c = copies.data() + i * (size_t)byte_count;
+            std::memcpy(c, inputs[shifted[i]] + offset, (size_t)byte_count);
+            ins[(size_t)shifted[i]] = c - offset;  // read back at + offset
+        }
+    }
+    (void)apply_rows(m, ins.data(), outputs, offset, byte_count, false);
 }
 
 bool host_exec_all_zero(const LinearMap &m, const uint8_t *const *inputs, int64_t offset, int64_t byte_count) {
@@ -213,7 +248,13 @@ bool host_exec_all_zero(const LinearMap &m, const uint8_t *const *inputs, int64_
 void host_exec_scale(uint8_t c, const uint8_t *in, uint8_t *out, int64_t n, bool accumulate) {
     const CoefTables &t = tables();
     const int level = isa_level();
-    // out (=|^=) c * in, in blocks through a small stack buffer (out may alias in)
+    // out (=|^=) c * in, in blocks through a small stack buffer: out may be in (the same
+    // address); an input overlapping out at a shifted address is copied first
+    thread_local std::vector<uint8_t> copy;
+    if (shifted_overlap(in, out, n)) {
+        copy.assign(in, in + n);
+        in = copy.data();
+    }
     uint8_t acc[1024];
     Coef k[2] = {{in, c, t.affine[c], t.lo[c], t.hi[c]}, {out, 1, t.affine[1], t.lo[1], t.hi[1]}};
     const int terms = accumulate ? 2 : 1;

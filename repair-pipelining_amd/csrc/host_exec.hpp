@@ -7,13 +7,15 @@
 #include "codes.hpp"
 
 namespace ecx {
-// outputs[out_slot[o]][offset..+byte_count) = sum_j M[o][j] * inputs[in_slot[j]][...]; outputs may
-// alias inputs (each 4 KiB block of every row is computed before any is stored)
+// outputs[out_slot[o]][offset..+byte_count) = sum_j M[o][j] * inputs[in_slot[j]][...]; an output
+// may be an input (each 4 KiB block of every row is computed before any is stored), and an
+// input that overlaps an output at a shifted address is read from a copy taken first
 void host_exec_apply(const LinearMap &m, const uint8_t *const *inputs, uint8_t *const *outputs, int64_t offset,
                      int64_t byte_count);
 // whether every output row of the map over the range is zero (isParityCorrect / checkSomeShards)
 bool host_exec_all_zero(const LinearMap &m, const uint8_t *const *inputs, int64_t offset, int64_t byte_count);
 // the one-coefficient call of encodeParitySingle / code_single: out (=, or ^= with accumulate) c * in
+// (in may be out, or overlap it anywhere)
 void host_exec_scale(uint8_t c, const uint8_t *in, uint8_t *out, int64_t n, bool accumulate);
 int host_exec_isa();  // 2 AVX-512BW + GFNI, 1 AVX2, 0 scalar
 // Test hook (tests/native/host_exec_check.cpp): run the given level (-1 = detect) if this CPU has it;

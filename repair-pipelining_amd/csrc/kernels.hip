@@ -638,7 +638,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
     if (!select) {
         launch_apply_core(cm, in, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
                           nbytes, stream, accumulate, -1);
-        note_device_launch(dev, stream);
+        note_device_launch(dev, stream, nstripes * in_bytes);
         return;
     }
     // A layout is its strides, the size class of the shard (log2 of the byte count) and of the
@@ -671,7 +671,7 @@ void launch_apply(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, 
         }
         throw;
     }
-    note_device_launch(dev, stream);
+    note_device_launch(dev, stream, nstripes * in_bytes);
     if (ticket) {
         if (hipEventRecord(e1, stream) == hipSuccess) {
             cm.fill_layout_probe(key, ticket, e0, e1);

@@ -6,7 +6,8 @@
 //   * random maps (1..20 inputs, 1..8 outputs, zero and one coefficients included) over byte
 //     counts around every vector and block boundary (1, 34, 63..65, 2174, 4095..4097, 10000) at
 //     odd offsets equal a dense table-row application, and bytes outside the range are untouched;
-//   * outputs aliasing inputs (x ^= c * y, decodeMissing in place) give the pre-update result;
+//   * outputs aliasing inputs (x ^= c * y, decodeMissing in place) give the pre-update result,
+//     and so do outputs overlapping an input at a shifted address;
 //   * host_exec_all_zero is true exactly when every output row is zero over the range.
 // Exit status 0 = all good.
 #include <cstdio>
@@ -140,6 +141,38 @@ void check_level(int level) {
         uint8_t *outs[2] = {nullptr, x.data()};
         host_exec_apply(m, ins, outs, 0, len);
         expect(x == want, "output aliasing an input", level);
+    }
+    // shifted overlap (round-5 advice): the output starts d bytes after (or before) an input
+    // inside one buffer, across 4 KiB blocks; the result is the map of the ORIGINAL input bytes
+    for (int64_t len : {100, 4096, 9000}) {
+        for (int64_t d : {-4097, -1, 1, 17, 4096, 5000}) {
+            if (d >= len || -d >= len) continue;
+            LinearMap m;
+            m.n_out = 1;
+            m.n_in = 2;
+            m.a = {0x53, 0xC1};
+            m.in_slot = {0, 1};
+            m.out_slot = {2};
+            std::vector<uint8_t> arena((size_t)(3 * len + 8192)), other((size_t)len);
+            for (auto &v : arena) v = (uint8_t)rng();
+            for (auto &v : other) v = (uint8_t)rng();
+            uint8_t *in0 = arena.data() + len + 4096, *out = in0 + d;
+            const std::vector<uint8_t> orig(in0, in0 + len);
+            std::vector<uint8_t> want((size_t)len);
+            for (int64_t i = 0; i < len; ++i)
+                want[(size_t)i] = (uint8_t)(f.mul(0x53, orig[(size_t)i]) ^ f.mul(0xC1, other[(size_t)i]));
+            const uint8_t *ins[3] = {in0, other.data(), nullptr};
+            uint8_t *outs[3] = {nullptr, nullptr, out};
+            host_exec_apply(m, ins, outs, 0, len);
+            expect(std::memcmp(out, want.data(), (size_t)len) == 0, "output overlapping an input at a shift", level);
+            // the one-coefficient form over the same kind of overlap
+            for (auto &v : arena) v = (uint8_t)rng();
+            const std::vector<uint8_t> orig2(in0, in0 + len);
+            host_exec_scale(0x1D, in0, out, len, false);
+            bool ok = true;
+            for (int64_t i = 0; i < len; ++i) ok = ok && out[i] == f.mul(0x1D, orig2[(size_t)i]);
+            expect(ok, "host_exec_scale with a shifted overlap", level);
+        }
     }
 }
 }  // namespace

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(ecx):
     assert headers == ["ecx.h", "ecx_tune.h"]
     missing = [s for h in headers for s in declared_symbols(h) if not hasattr(lib, s)]
     assert not missing, missing
-    assert len(declared_symbols("ecx_tune.h")) == 16
+    assert len(declared_symbols("ecx_tune.h")) == 17
 
 
 def test_binding_table_matches_header(ecx):
@@ -158,7 +158,7 @@ def test_tuning_keys(ecx):
     for key in lab:  # the product library refuses them; the diagnostic one takes its defaults
         assert tune(key.encode(), 1 if key in ("rtc_units", "units") else 0) == (0 if ecx.is_diag() else -1), key
     defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0,
-                "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_sched": 2, "rtc_nt": 5, "xcd_run": 8, "xcd_misaligned": 1,
+                "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_sched": 2, "rtc_nt": 5, "rtc_wide": 0, "xcd_run": 8, "xcd_misaligned": 1,
                 "map_planes": 1, "planes_lookahead": 12, "planes_waves": 2,
                 "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512, "host_exec_kib": 8}
     assert sorted(documented) == sorted(defaults)
@@ -167,7 +167,7 @@ def test_tuning_keys(ecx):
     for key, val in defaults.items():
         assert tune(key.encode(), val) == 0, key
     assert tune(b"no_such_knob", 1) == -1
-    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("xcd_misaligned", 2), ("stagger", -1), ("stagger", 65), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("layout_select", 2), ("plan_cache", -1), ("bitslice", 3), ("lds_lut", 3), ("lds_lut", -1), ("roctx", 2), ("host_contexts", 2), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("rtc_units", 0), ("rtc_units", 3), ("rtc_sched", 3), ("rtc_nt", -1), ("rtc_nt", 16), ("occ_lds", -2), ("occ_lds", 65537), ("rtc_diag", 1), ("rtc_diag", 32), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5), ("host_exec_kib", -1)):
+    for key, bad in (("depth", 3), ("depth", 6), ("nontemporal", 3), ("xcd_group", -1), ("xcd_group", 4), ("xcd_run", 0), ("xcd_misaligned", 2), ("stagger", -1), ("stagger", 65), ("lds_tables", 3), ("host_buffers", 9), ("block_threads", 128), ("small_tiles", 3), ("wave_groups", 3), ("wide_tiles", 3), ("skew_chunks", 3), ("layout_select", 2), ("plan_cache", -1), ("bitslice", 3), ("lds_lut", 3), ("lds_lut", -1), ("roctx", 2), ("host_contexts", 2), ("clay_rtc", 3), ("rtc_lookahead", 32), ("rtc_waves", 1), ("rtc_persist", 9), ("rtc_units", 0), ("rtc_units", 3), ("rtc_sched", 3), ("rtc_nt", -1), ("rtc_nt", 16), ("rtc_wide", 2), ("occ_lds", -2), ("occ_lds", 65537), ("rtc_diag", 1), ("rtc_diag", 32), ("map_planes", 3), ("planes_lookahead", 16), ("planes_waves", 0), ("planes_waves", 5), ("host_exec_kib", -1)):
         assert tune(key.encode(), bad) == -1, key
     for key, val in defaults.items():  # restore
         tune(key.encode(), val)

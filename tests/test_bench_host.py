@@ -290,3 +290,24 @@ def test_copy_chunked_round_trip():
     dst = torch.zeros_like(src)
     bench._copy_chunked(dst, src, chunk=1000)
     assert torch.equal(dst, src)
+
+
+def test_clay104_sub_bytes_reading(monkeypatch):
+    """Config 4's other reading: --sub-bytes sets CLAY_BLOCK_SIZE for
+    clay104 and scales the pool / stripes per step to the same bytes per step; its CPU
+    baseline aliases read-only multi-GiB units instead of copying one per thread (a 64 KiB
+    stand-in with a small arena cap here)."""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "clay104", "--sub-bytes", "1048576"])
+    a = bench.parse()
+    assert a.sub_bytes == 1 << 20 and a.pool == 16 and a.stripes_per_step == 128
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "clay104"])
+    a = bench.parse()
+    assert a.pool == 2048 and a.stripes_per_step == 1 << 15
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "rs173", "--sub-bytes", "4096"])
+    with pytest.raises(SystemExit):
+        bench.parse()
+    monkeypatch.setattr(bench, "CPU_ARENA_BYTES", 300 << 20)
+    b = 65536
+    wl = _bare(bench.Clay104, erased=3, n=14, unit_bytes=1088 * b, b=b)
+    cpu = bench.cpu_baseline(wl, 0.2, None, max_units=2)
+    assert cpu["value"] > 0 and "alias 1 distinct" in cpu["sample"] and "65536-B sub-chunks" in cpu["sample"]

@@ -747,7 +747,8 @@ def test_map_host_batch_devices_and_refusals(ecx, small_host_chunks):
 
 @pytest.mark.parametrize("k,m,L,off,S", [(17, 3, 200000, 0, 6), (4, 2, 104449, 0, 5), (4, 2, 4096 * 3, 16, 4),
                                          (10, 10, 8192 + 48, 0, 3), (5, 5, 1001, 3, 4), (17, 3, 4096, 0, 3),
-                                         (2, 1, 16, 0, 2), (64, 64, 4096 + 16, 0, 2), (12, 4, 3 * 4096, 0, 9)])
+                                         (2, 1, 16, 0, 2), (64, 64, 4096 + 16, 0, 2), (12, 4, 3 * 4096, 0, 9),
+                                         (17, 3, 200000, 5, 4), (4, 2, 4096 * 2 + 7, 9, 3)])
 def test_is_parity_correct_batch_vs_oracle(ecx, torch_dev, k, m, L, off, S):
     """isParityCorrectBatch (k_gf_check, read-only): valid stripes pass; one flipped byte --
     in a data shard at byte 0, in a parity shard inside the partial last chunk, at the last
@@ -755,10 +756,14 @@ def test_is_parity_correct_batch_vs_oracle(ecx, torch_dev, k, m, L, off, S):
     not written; firstByte / byteCount windows follow ReedSolomon.java:129-178 (a flip
     outside the window passes).  Shapes: the published RS(17,3) 200,000 B (fused partial
     chunk), RS(4,2) on the LP-block shard size (ragged: byte-safe tail), an unaligned base
-    (offset 3), RS(10,10) (two 8-row tiles), a shard of one chunk and one of 16 B."""
+    (offset 3), RS(10,10) (two 8-row tiles), a shard of one chunk and one of 16 B; and a
+    firstByte off a 16-B boundary on 16-B strides (5, 9: the head up to the boundary runs
+    byte-safe, the rest vectorised; the flip at firstByte lies in the head)."""
     torch = torch_dev
     n = k + m
     pitch = off + L + 32
+    if off % 16:  # the unaligned-start cases on 16-B strides (the (5,5,1001,3) case keeps odd strides)
+        pitch = pitch if (k, m, L) == (5, 5, 1001) else -(-pitch // 16) * 16
     rng = np.random.default_rng(k * 1000 + L)
     host = np.zeros((S, n, pitch), np.uint8)
     host[:, :k] = rng.integers(0, 256, (S, k, pitch), dtype=np.uint8)
@@ -1750,6 +1755,73 @@ def test_clay104_shipped_repair_kernel_vs_shortened_oracle(ecx, torch_dev, e):
         assert not bad, (e, s, bad[:8])
 
 
+def test_clay104_wide_address_kernel_equals_narrow(ecx, torch_dev):
+    """The plane-group kernel's 64-bit-address form (forced with ecx_tune "rtc_wide" 1 on the
+    4 KiB sub-chunk layout, where the 32-bit form also runs) writes exactly the 32-bit form's
+    bytes on random non-codeword stripes, for a data node and a parity node."""
+    torch = torch_dev
+    k, m, v, B, S = 10, 4, 2, 4096, 6
+    n, a = k + m, 256
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 77)
+    for e in (3, 12):
+        step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+        outs = []
+        for wide in (0, 1):
+            ecx.tune("rtc_wide", wide)
+            try:
+                o = torch.full((S, a, B), 0xA5, dtype=torch.uint8, device="cuda")
+                step.performCodingBatch(pool, n * a * B, B, o, a * B, B, S, B)
+                torch.cuda.synchronize()
+                assert ecx.last_kernel() == "k_clay_repair_grp", ecx.last_kernel()
+                outs.append(o)
+            finally:
+                ecx.tune("rtc_wide", 0)
+        assert torch.equal(outs[0], outs[1]), e
+
+
+def test_clay104_one_mib_sub_chunks(ecx, torch_dev):
+    """Config 4's other reading: CLAY_BLOCK_SIZE = 1 MiB sub-chunks (PipelineUtil.kt:13-28,
+    ClayCodeErasureDecodingStep.java:72-73), alpha = 256, a 256 MiB node block, a 3.5 GiB
+    stripe.  Encode on the GPU, erase node 3 (and 13), repair, compare with the originals
+    (the round trip); then repair a random NON-codeword stripe and compare a 64 KiB window
+    of every one of the 256 repaired sub-chunks with the oracle Clay(12,4) (zero-filled
+    virtual nodes) run on the same window of every input sub-chunk: the map acts bytewise,
+    so a window pins it."""
+    torch = torch_dev
+    k, m, v, B, S, W = 10, 4, 2, 1 << 20, 2, 65536
+    n = k + m
+    enc = ecx.ClayCodeErasureDecodingStep(list(range(k, n)), k, m, virtualUnits=v)
+    a = enc.subPacketSize
+    pool = torch.empty((S, n * a, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 1044)
+    par = torch.empty((S, m * a, B), dtype=torch.uint8, device="cuda")
+    enc.performCodingBatch(pool, n * a * B, B, par, m * a * B, B, S, B)
+    pool.view(S, a, n, B)[:, :, k:, :] = par.view(S, a, m, B)
+    del par
+    out = torch.empty((S, a, B), dtype=torch.uint8, device="cuda")
+    for e in (3, 13):
+        out.fill_(0x5A)
+        ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v).performCodingBatch(
+            pool, n * a * B, B, out, a * B, B, S, B)
+        torch.cuda.synchronize()
+        assert torch.equal(out, pool.view(S, a, n, B)[:, :, e, :]), e
+    # a non-codeword stripe: the exact linear map, window by window
+    e = 3
+    ecx.fill_random(pool, pool[0].numel(), 1045)
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, virtualUnits=v)
+    step.performCodingBatch(pool, n * a * B, B, out, a * B, B, 1, B)
+    torch.cuda.synchronize()
+    assert ecx.last_kernel() == "k_clay_repair_grp", ecx.last_kernel()
+    for w0 in (0, B - W):
+        host = pool[0, :, w0:w0 + W].cpu().numpy()
+        got = out[0, :, w0:w0 + W].cpu().numpy()
+        inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
+        ref = shortened_clay_oracle(k, m, v, [e], inputs, W)
+        bad = [z for z in range(a) if not (got[z] == ref[z]).all()]
+        assert not bad, (w0, bad[:8])
+
+
 def test_clay_rtc_first_use_from_two_streams(ecx, torch_dev):
     """The per-helper-plane kernel's program table is uploaded synchronously before the
     loaded module is published (ClayRtc::prepare), so a second thread that launches the
@@ -2173,6 +2245,34 @@ def test_clay_rtc_nontemporal_policies_vs_oracle(ecx, torch_dev, e, B, S):
     inputs = [None if (i % n) == e else host[i].copy() for i in range(n * a)]
     ref = shortened_clay_oracle(k, m, v, [e], inputs, B)
     assert all((outs[0][S - 1, z] == ref[z]).all() for z in range(a))
+
+
+def test_layout_selection_serialized_streams_drop_nothing(ecx, torch_dev):
+    """Round-5 advice: callers on their own streams whose calls never overlap (JVM threads
+    serialised by @Synchronized, ClayCodeNode.kt:76-347) must not lose their timing probes.
+    Two streams take turns on one batch layout, each call finished before the next starts: a
+    launch of the other stream that finds a probe already done does not drop it, so the
+    selection concludes with nothing dropped, and every call's output is the oracle's parity."""
+    torch = torch_dev
+    k, m, L, S = 12, 4, 1 << 20, 24
+    rs = ecx.ReedSolomon.create(k, m)
+    emap = rs.encode_map()
+    pool = torch.empty((S, 16, L), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(pool, pool.numel(), 310)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i in range(80):
+        st = streams[i % 2]
+        emap.apply_batch(pool, 16 * L, L, pool, 16 * L, L, S, L, stream=st)
+        st.synchronize()
+    state, dropped = emap.layout_state(L)
+    assert emap.layout_choice(L) != -1 and state in (1, 2, 3) and dropped == 0, (state, dropped)
+    host = pool[S - 1].cpu().numpy()
+    ref = [host[i].copy() for i in range(16)]
+    for i in range(k, 16):
+        ref[i][:] = 0
+    O.ReedSolomon(k, m).encode_parity(ref, 0, L)
+    assert all((host[i] == ref[i]).all() for i in range(k, 16))
 
 
 def test_layout_selection_two_streams(ecx, torch_dev):

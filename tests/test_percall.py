@@ -20,6 +20,25 @@ ROOT = Path(__file__).resolve().parents[1]
 EXE = ROOT / "tests" / "native" / "_build" / "percall_threshold"
 
 
+def default_host_exec_kib() -> int:
+    """The library's compiled-in per-call threshold, read in a fresh process (ecx_tune_value:
+    no device needed), since the GPU suite sets host_exec_kib 0 in this one."""
+    code = ("import sys; sys.path.insert(0, %r); import rpamd; print(rpamd.load().tune_value('host_exec_kib'))"
+            % str(ROOT))
+    r = subprocess.run([os.environ.get("PYTHON", "python3"), "-c", code], capture_output=True, text=True,
+                       timeout=300, env={k: v for k, v in os.environ.items() if k != "ECX_SHAPE_KNOBS"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    return int(r.stdout.strip().splitlines()[-1])
+
+
+def test_default_threshold_below_the_reference_sub_chunk(ecx):
+    """The default host_exec_kib (8) keeps 32 KiB sub-chunk calls (the reference's
+    CLAY_BLOCK_SIZE) on the device path; the getter refuses shape keys."""
+    assert 0 < default_host_exec_kib() < 32
+    with pytest.raises(ecx.EcxError):
+        ecx.tune_value("depth")
+
+
 def _has_device(ecx):
     try:
         return ecx.device_count() > 0
@@ -58,8 +77,9 @@ def test_percall_crossover_vs_oracle(ecx):
     for key in (("rs31_single", 34), ("rs22_pair", 2174)):  # round-4 verdict item 4's bar
         x = by[key]
         assert x["default_us"] <= 2 * x["oracle_us"] + 0.5, x
-    # the default threshold sits below 32 KiB: those calls keep the device path
-    assert 8 * 1024 < 32768
+    # the library's default threshold (a fresh process: this suite sets 0) sits below 32 KiB, so
+    # the reference's 32 KiB sub-chunk calls keep the device path
+    assert 0 < default_host_exec_kib() < 32
 
 
 @pytest.mark.gpu

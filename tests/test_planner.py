@@ -505,3 +505,22 @@ def test_generated_kernels_without_hiprtc(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "code -10 True" in r.stdout, r.stdout
+
+
+def test_plane_group_kernel_wide_addresses_compile(ecx):
+    """The plane-group kernel's 64-bit-address form (RtcShape::wide, ecx_tune "rtc_wide"), used
+    where a stripe's slot offsets exceed 31 bits (Clay(10,4) with 1 MiB sub-chunks: 3.5 GiB per
+    stripe): flat global loads with 64-bit offsets replace the buffer-resource loads, the rest
+    of the generated source is the same, and it compiles with hiprtc for gfx950."""
+    step = ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2)
+    narrow = step.rtcSource()
+    ecx.tune("rtc_wide", 1)
+    try:
+        wide = step.rtcSource()
+        assert "make_buffer_rsrc" in narrow and "make_buffer_rsrc" not in wide
+        assert "const long long vz" in wide and "ibp + " in wide and "zero_page + voff" in wide
+        assert wide.count("tr(") == narrow.count("tr(")  # same arithmetic
+        assert step.rtcCompileCheck() > 0
+    finally:
+        ecx.tune("rtc_wide", 0)
+    assert step.rtcSource() == narrow
