@@ -98,6 +98,13 @@ def parse():
     ap.add_argument("--sub-bytes", type=int, default=None,
                     help="clay104: bytes per sub-chunk (CLAY_BLOCK_SIZE). Default 4096: 1 MiB node blocks of 256 "
                          "sub-chunks; 1048576 is config 4's other reading, 1 MiB sub-chunks (256 MiB node blocks)")
+    ap.add_argument("--layout", default="natural", choices=["natural", "blocked"],
+                    help="rs173 / rs124: natural = the shards back to back ([stripe][shard][pitch]); blocked = "
+                         "the engine's layout contract (ecx_rs_blocked_layout: 64 KiB blocks block-major, tails "
+                         "apart; DESIGN.md section 4.6)")
+    ap.add_argument("--pitch", default=None,
+                    help="rs173 / rs124 natural layout: the shard pitch in bytes, or 'recommended' "
+                         "(ecx_rs_recommended_pitch); default: the shard size (rs124: plus --pitch-pad)")
     ap.add_argument("--pitch-pad", type=int, default=0,
                     help="rs124: bytes of padding per 4 MiB shard (default 0: the natural contiguous [S][16][4 MiB] layout)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -119,6 +126,10 @@ def parse():
     _metric, pool, per_step = WORKLOADS[args.workload]
     if args.sub_bytes is not None and args.workload != "clay104":
         ap.error("--sub-bytes applies to --workload clay104 only")
+    if (args.layout != "natural" or args.pitch is not None) and args.workload not in ("rs173", "rs124"):
+        ap.error("--layout / --pitch apply to --workload rs173 and rs124 only")
+    if args.layout == "blocked" and (args.pitch is not None or args.pitch_pad):
+        ap.error("--layout blocked has no shard pitch")
     if args.workload == "clay104" and args.sub_bytes and args.sub_bytes != Clay104.b:
         # the same 2^15 x 1,088 x 4 KiB of algorithmic bytes per step, over a pool of 16 stripes
         # (56 GiB at 1 MiB sub-chunks) instead of 2,048
@@ -756,29 +767,78 @@ class Clay104(Workload):
                         "algorithmic bytes" % (self.erased, self.b), "read_only_units": True}
 
 
-class RS124(Workload):
+def _resolve_pitch(rs, args_pitch, L, pad=0):
+    """The natural layout's shard pitch: --pitch (bytes or 'recommended') or L + pad."""
+    if args_pitch is None:
+        return L + pad
+    if str(args_pitch) == "recommended":
+        return rs.recommendedPitch(L)
+    p = int(args_pitch)
+    if p < L:
+        raise SystemExit("--pitch %d is below the shard size %d" % (p, L))
+    return p
+
+
+class _RsLayout:
+    """A pool of RS stripes in the natural layout ([stripe][n][pitch], self.pool 3-D) or the
+    blocked one (ecx_rs_blocked_layout, self.pool flat), with natural read-back."""
+    layout, block = "natural", None
+
+    def stripes(self, first, count, slots=None):
+        """[count][slots][L] natural shards of stripes first.. (a device tensor)."""
+        if self.layout == "blocked":
+            return self.ecx.blocked_unpack(self.pool, self.P, self.n, self.L, self.block, slots, first, count)
+        sl = slice(None) if slots is None else list(slots)
+        return self.pool[first:first + count, sl, :self.L]
+
+    def _layout_desc(self):
+        if self.layout == "blocked":
+            full, tail = divmod(self.L, self.block)
+            return ("blocked layout: %d-B blocks block-major (%d full + a %d-B tail per shard, tails apart; "
+                    "ecx_rs_blocked_layout)" % (self.block, full, tail))
+        return "shard pitch %d B%s" % (self.pitch, "" if self.pitch != self.L else " (back to back)")
+
+    def host_units(self, k):
+        return [self.stripes(i, 1)[0].cpu().numpy() for i in range(min(k, self.P))]
+
+
+class RS124(_RsLayout, Workload):
     """Config 5: RS(12,4), 4 MiB shards, erasures {0,1} decoded in place (the first 12
     present shards, ReedSolomon.decodeMissing)."""
-    k, m, L = 12, 4, 4 << 20
+    k, m, L, n = 12, 4, 4 << 20, 16
     reads, writes = 12, 2
     unit_bytes = 14 * (4 << 20)
     write_bytes = 2 * (4 << 20)
 
-    def __init__(self, ecx, torch, dev, P, pad, seed):
-        self.P, self.torch, self.pitch = P, torch, self.L + pad
+    def __init__(self, ecx, torch, dev, P, pad, seed, layout="natural", pitch=None):
+        self.P, self.torch, self.ecx, self.layout = P, torch, ecx, layout
         rs = ecx.ReedSolomon.create(self.k, self.m)
-        p, L = self.pitch, self.L
-        self.pool = torch.empty((P, 16, p), dtype=torch.uint8, device=dev)
-        ecx.fill_random(self.pool, self.pool.numel(), seed)
-        rs.encode_map().apply_batch(self.pool, 16 * p, p, self.pool, 16 * p, p, P, L)
-        self.orig = self.pool[:, 0:2, :L].clone()
-        self.pool[:, 0:2, :L] = 0  # the erased shards
         self.rs = rs
-        self.dmap = rs.decode_map([False, False] + [True] * 14)
+        L = self.L
+        self.pitch = L if layout == "blocked" else _resolve_pitch(rs, pitch, L, pad)
+        p = self.pitch
+        nat = torch.empty((P, 16, p), dtype=torch.uint8, device=dev)
+        ecx.fill_random(nat, nat.numel(), seed)
+        rs.encode_map().apply_batch(nat, 16 * p, p, nat, 16 * p, p, P, L)
+        self.orig = nat[:, 0:2, :L].clone()
+        nat[:, 0:2, :L] = 0  # the erased shards
+        self.present = [False, False] + [True] * 14
+        self.dmap = rs.decode_map(self.present)
+        if layout == "blocked":
+            self.block = rs.blockedLayout(L)[0]
+            self.pool = ecx.blocked_pack(nat[:, :, :L], self.block)
+            del nat
+            self.pitch = self.block  # the slot pitch the decode's launches see
+            self.host_ok = False
+        else:
+            self.pool = nat
         self.region = self.pool
-        self.description = "RS(12,4) 2-erasure decode {0,1} in place, 4 MiB shards, shard pitch %d B" % p
+        self.description = "RS(12,4) 2-erasure decode {0,1} in place, 4 MiB shards, %s" % self._layout_desc()
 
     def launch(self):
+        if self.layout == "blocked":
+            self.rs.decodeMissingBlockedBatch(self.pool, self.present, self.P, self.L)
+            return
         p = self.pitch
         self.dmap.apply_batch(self.pool, 16 * p, p, self.pool, 16 * p, p, self.P, self.L)
 
@@ -796,14 +856,13 @@ class RS124(Workload):
         return self.L
 
     def verify(self):
-        return bool(self.torch.equal(self.pool[:, 0:2, :self.L], self.orig))
-
-    def host_units(self, k):
-        return [self.pool[i, :, :self.L].cpu().numpy() for i in range(min(k, self.P))]
+        return all(bool(self.torch.equal(self.stripes(s0, min(64, self.P - s0), [0, 1]), self.orig[s0:s0 + 64]))
+                   for s0 in range(0, self.P, 64))
 
     def sample(self):
         s = self.P // 2
-        return self.pool[s, :, :self.L].cpu().numpy(), self.pool[s, 0:2, :self.L].cpu().numpy()
+        st = self.stripes(s, 1)[0]
+        return st.cpu().numpy(), st[0:2].cpu().numpy()
 
     def oracle_check(self, stripe, got):
         import numpy as np
@@ -824,32 +883,47 @@ class RS124(Workload):
                         "inverted per call as ReedSolomon.java:224-244 does), 4 MiB shards"}
 
 
-class RS173(Workload):
+class RS173(_RsLayout, Workload):
     """The reference's published benchmark shape (rs/README.md:53, ReedSolomonBenchmark.java:
     25-33,104-124): RS(17,3) encodeParity over 200,000-byte shards, parity written in place.
-    Shards lie back to back (pitch 200,000 B): every other slot is 64 B off a 128-B line and
-    each shard ends in a 320-B partial chunk, as DESIGN.md section 4 measures."""
-    k, m, L = 17, 3, 200 * 1000
+    Natural layout: shards back to back (pitch 200,000 B), every other slot 64 B off a 128-B
+    line and each shard ending in a 320-B partial chunk, as DESIGN.md section 4 measures; or a
+    padded pitch (--pitch), or the blocked layout contract (--layout blocked)."""
+    k, m, L, n = 17, 3, 200 * 1000, 20
     reads, writes = 17, 3
     unit_bytes = 20 * 200 * 1000        # 17 shards read + 3 written (roofline bytes)
     write_bytes = 3 * 200 * 1000
     metric_unit, metric_scale, metric_bytes = "MB/s", 1e6, 17 * 200 * 1000  # data bytes, 10^6
     data_desc = "synthetic (device splitmix64 data shards; the timed launch is the encode itself)"
 
-    def __init__(self, ecx, torch, dev, P, seed):
-        self.P, self.torch = P, torch
+    def __init__(self, ecx, torch, dev, P, seed, layout="natural", pitch=None):
+        self.P, self.torch, self.ecx, self.layout = P, torch, ecx, layout
         L = self.L
-        self.pool = torch.empty((P, 20, L), dtype=torch.uint8, device=dev)
-        ecx.fill_random(self.pool, self.pool.numel(), seed)
         self.rs = ecx.ReedSolomon.create(self.k, self.m)
+        if layout == "blocked":
+            self.block = self.rs.blockedLayout(L)[0]
+            self.pitch = self.block
+            self.pool = torch.empty(P * 20 * L, dtype=torch.uint8, device=dev)
+            self.host_ok = False
+        else:
+            self.pitch = _resolve_pitch(self.rs, pitch, L)
+            self.pool = torch.empty((P, 20, self.pitch), dtype=torch.uint8, device=dev)
+            if self.pitch != L:
+                self.host_ok = False  # the e2e leg runs the published (natural) shape only
+        ecx.fill_random(self.pool, self.pool.numel(), seed)
         self.region = self.pool
-        self.description = "RS(17,3) encodeParity in place, 200,000-B shards back to back (the published shape)"
+        self.description = ("RS(17,3) encodeParity in place, 200,000-B shards, %s%s" %
+                            (self._layout_desc(), " (the published shape)" if self.pitch == L else ""))
 
     def launch(self):
-        self.rs.encodeParityBatch(self.pool, 20 * self.L, self.L, self.P, 0, self.L)
+        if self.layout == "blocked":
+            self.rs.encodeParityBlockedBatch(self.pool, self.P, self.L)
+            return
+        p = self.pitch
+        self.rs.encodeParityBatch(self.pool, 20 * p, p, self.P, 0, self.L)
 
     def selected_map(self):
-        return self.rs.encode_map(), self.L
+        return self.rs.encode_map(), self.pitch
 
     def host_out_bytes(self):
         return 0
@@ -859,20 +933,20 @@ class RS173(Workload):
 
     def verify(self):
         """The parity the GPU wrote equals the oracle's on two stripes, and re-encoding
-        leaves every stripe unchanged (isParityCorrect over the whole pool)."""
-        before = self.pool[:, self.k:, :].clone()
+        leaves the whole pool unchanged (isParityCorrect over every stripe)."""
+        before = self.pool.clone()
         self.launch()
         self.torch.cuda.synchronize()
-        same = bool(self.torch.equal(before, self.pool[:, self.k:, :]))
-        return same and all(self.oracle_check(self.pool[s].cpu().numpy(), self.pool[s, self.k:].cpu().numpy())
-                            for s in (0, self.P - 1))
+        same = bool(self.torch.equal(before, self.pool))
+        del before
+        return same and all(self.oracle_check(*self._stripe_and_parity(s)) for s in (0, self.P - 1))
 
-    def host_units(self, k):
-        return [self.pool[i].cpu().numpy() for i in range(min(k, self.P))]
+    def _stripe_and_parity(self, s):
+        st = self.stripes(s, 1)[0]
+        return st.cpu().numpy(), st[self.k:].cpu().numpy()
 
     def sample(self):
-        s = self.P // 2
-        return self.pool[s].cpu().numpy(), self.pool[s, self.k:].cpu().numpy()
+        return self._stripe_and_parity(self.P // 2)
 
     def oracle_check(self, stripe, got):
         import oracle as O
@@ -1196,9 +1270,9 @@ def main():
     elif args.workload == "clay42x2":
         wl = Clay42x2(ecx, torch, dev, P, args.erased, seed)
     elif args.workload == "rs124":
-        wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed)
+        wl = RS124(ecx, torch, dev, P, args.pitch_pad, seed, args.layout, args.pitch)
     elif args.workload == "rs173":
-        wl = RS173(ecx, torch, dev, P, seed)
+        wl = RS173(ecx, torch, dev, P, seed, args.layout, args.pitch)
     elif args.workload == "rs173check":
         wl = RS173Check(ecx, torch, dev, P, seed)
     elif args.workload == "lrcenc":

@@ -159,6 +159,33 @@ int ecx_rs_decode_missing_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_
                                 int64_t shard_stride, int64_t nstripes, int64_t offset, int64_t byte_count,
                                 void *stream);
 
+/* The engine's layout contract for RS batches in HBM (the reference
+ * keeps every shard in its own byte[], ReedSolomonBenchmark.java:198, so the device layout
+ * is the caller's choice).  BLOCKED layout of nstripes stripes of n = k + m shards of
+ * byte_count bytes, in block_bytes blocks (full = byte_count / block_bytes, tail = the rest):
+ *   body  [nstripes][full][n][block_bytes] at base -- a stripe block-major, the way Clay
+ *         stores its sub-chunks plane-major (ClayCodeErasureDecodingStep.java:84-97);
+ *   tails [nstripes][n][tail] at base + nstripes * full * n * block_bytes.
+ * It occupies exactly nstripes * n * byte_count bytes.  Measured against the natural
+ * back-to-back shards (scripts/rs_layout_contract.py): RS(17,3) encodeParity on 200,000-B
+ * shards 0.695 -> 0.760 of HBM (32 KiB blocks), RS(12,4) 2-erasure decode on 4 MiB shards
+ * 0.754 -> 0.816 (64 KiB blocks).
+ * ecx_rs_blocked_layout fills layout[3] = {block_bytes, full, tail} for RS(k, m) and a shard
+ * size: the largest power of two with n blocks within 1 MiB (4 KiB..1 MiB), or one block of
+ * byte_count bytes below that. */
+int ecx_rs_blocked_layout(int data_shards, int parity_shards, int64_t byte_count, int64_t *layout);
+/* The recommended shard pitch of the plain [stripe][shard][pitch] layout when the caller cannot
+ * block: the smallest odd multiple of 4 KiB >= byte_count (RS(12,4) 4 MiB: 0.754 -> 0.789;
+ * RS(17,3) 200,000 B: 0.695 -> 0.718). */
+int ecx_rs_recommended_pitch(int data_shards, int parity_shards, int64_t byte_count, int64_t *pitch);
+/* ecx_rs_encode_parity_batch over the blocked layout (block_bytes > 0; 0 = the recommended
+ * block), in place: two launches, the full blocks and the tails, on `stream`. */
+int ecx_rs_encode_parity_blocked_batch(ecx_rs *rs, uint8_t *base, int64_t nstripes, int64_t byte_count,
+                                       int64_t block_bytes, void *stream);
+/* ecx_rs_decode_missing_batch over the blocked layout, in place (the same map). */
+int ecx_rs_decode_missing_blocked_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base, int64_t nstripes,
+                                        int64_t byte_count, int64_t block_bytes, void *stream);
+
 /* As ecx_map_apply_batch, but XOR-accumulates: out ^= M * in. */
 int ecx_map_accumulate_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
                              int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride,

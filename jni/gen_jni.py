@@ -133,6 +133,9 @@ RULES = {
     "ecx_map_slot_extent": ((), [A("max_in_slot", "1"), A("max_out_slot", "1")]),
     "ecx_rs_decode_map": (("rs",), [A("shard_present", RS_N)]),
     "ecx_rs_decode_missing_batch": (("rs",), [A("shard_present", RS_N)]),
+    "ecx_rs_blocked_layout": ((), [A("layout", "3")]),
+    "ecx_rs_recommended_pitch": ((), [A("pitch", "1")]),
+    "ecx_rs_decode_missing_blocked_batch": (("rs",), [A("shard_present", RS_N)]),
     "ecx_rs_decode_partial_batch": (("rs",), [A("shard_present", RS_N)]),
     "ecx_clay_create": ((), [NN("n_erased"), A("erased", "n_erased")]),
     "ecx_clay_create_shortened": ((), [NN("n_erased"), A("erased", "n_erased")]),
@@ -309,6 +312,8 @@ def classify(fn, ctype, pname):
         return "bytes", "byte[]", "jbyteArray"
     if base == "int*":
         return "ints", "int[]", "jintArray"
+    if base == "int64_t*":
+        return "longs", "long[]", "jlongArray"
     if base == "int16_t*":
         return "shorts", "short[]", "jshortArray"
     raise SystemExit("unmapped parameter type %r of %s" % (ctype, fn))
@@ -493,7 +498,7 @@ public final class EcxNative {
         body = []
         pre, copies, pin, unpin, post, args = [], [], [], [], [], []
         pnames = {p: kind for (kind, _, _), t, p in kinds}
-        needs_rule = [p for p, k in pnames.items() if k in ("bytes", "ints", "shorts", "buflist")]
+        needs_rule = [p for p, k in pnames.items() if k in ("bytes", "ints", "shorts", "longs", "buflist")]
         if needs_rule and name not in RULES:
             raise SystemExit("no argument rule for %s (pointer parameters %s)" % (name, needs_rule))
         queries, rules = RULES.get(name, ((), []))
@@ -553,8 +558,8 @@ public final class EcxNative {
                               % (p, p, need, p))
                 post.append("    free(%s_p);" % p)
                 args.append("%s_p" % p)
-            elif kind in ("bytes", "ints", "shorts"):
-                cty = {"bytes": "uint8_t", "ints": "int", "shorts": "int16_t"}[kind]
+            elif kind in ("bytes", "ints", "shorts", "longs"):
+                cty = {"bytes": "uint8_t", "ints": "int", "shorts": "int16_t", "longs": "int64_t"}[kind]
                 mode = "JNI_ABORT" if t.startswith("const") else "0"
                 pre.append("    %s *%s_p = NULL;" % (cty, p))
                 pin.append("    if (st == ECX_OK) %s_p = (%s *)PIN(%s);" % (p, cty, p))
@@ -590,7 +595,7 @@ public final class EcxNative {
             if pinned:
                 # every PIN that returned NULL for a non-null array is an allocation failure
                 checks = ["(%s && !%s_p)" % (p, p) for (kind, _, _), t, p in kinds
-                          if kind in ("bytes", "ints", "shorts") and not (kind == "ints" and t.startswith("const"))]
+                          if kind in ("bytes", "ints", "shorts", "longs") and not (kind == "ints" and t.startswith("const"))]
                 if checks:
                     body.append("    if (st == ECX_OK && (%s)) st = ECX_E_NOMEM;" % " || ".join(checks))
             body.append("    if (st == ECX_OK) st = %s;" % call)

@@ -179,6 +179,48 @@ def _check_layout(buf, stripe_stride, slot_stride, max_slot, nstripes, nbytes, w
         raise EcxError(-5, f"{what}: the batch layout addresses {need} bytes but the buffer holds {avail}")
 
 
+def _check_extent(buf, nbytes, what):
+    avail = _avail_bytes(buf)
+    if nbytes > 0 and avail is not None and nbytes > avail:
+        raise EcxError(-5, f"{what}: the batch addresses {nbytes} bytes but the buffer holds {avail}")
+
+
+def blocked_pack(shards, block_bytes: int, out=None):
+    """The blocked layout (include/ecx.h ecx_rs_blocked_layout) of a [stripes][n][L] uint8
+    tensor, as a flat tensor of stripes * n * L bytes: body [stripe][block][shard][block_bytes],
+    then tails [stripe][shard][L % block_bytes] (torch copies on the tensor's device)."""
+    S, n, L = shards.shape
+    full, tail = divmod(L, block_bytes)
+    if out is None:
+        out = shards.new_empty(S * n * L)
+    body = full * n * block_bytes
+    if full:
+        out[:S * body].view(S, full, n, block_bytes).copy_(
+            shards[:, :, :full * block_bytes].reshape(S, n, full, block_bytes).permute(0, 2, 1, 3))
+    if tail:
+        out[S * body:].view(S, n, tail).copy_(shards[:, :, full * block_bytes:])
+    return out
+
+
+def blocked_unpack(flat, stripes: int, n: int, byte_count: int, block_bytes: int, slots=None, first: int = 0,
+                   count: int = None):
+    """The natural [count][len(slots)][byte_count] shards (default: every stripe, every slot) of
+    stripes first..first+count-1 of a blocked-layout buffer of `stripes` stripes (a copy)."""
+    import torch
+    count = stripes - first if count is None else count
+    slots = list(range(n)) if slots is None else list(slots)
+    full, tail = divmod(byte_count, block_bytes)
+    body = full * n * block_bytes
+    parts = []
+    if full:
+        b = flat[:stripes * body].view(stripes, full, n, block_bytes)[first:first + count][:, :, slots, :]
+        parts.append(b.permute(0, 2, 1, 3).reshape(count, len(slots), full * block_bytes))
+    if tail:
+        t = flat[stripes * body:stripes * n * byte_count].view(stripes, n, tail)[first:first + count]
+        parts.append(t[:, slots, :])
+    return torch.cat(parts, dim=2) if len(parts) > 1 else parts[0].clone()
+
+
 class HostBuffer:
     """Page-locked host memory from ecx_host_alloc, viewed as a numpy uint8 array."""
 
@@ -596,6 +638,38 @@ class ReedSolomon:
                       "shards")
         check(lib().ecx_rs_encode_parity_batch(self._h, _dev_ptr(shards), stripe_stride, shard_stride, nstripes,
                                                offset, byteCount, _stream(stream)))
+
+    # ---- the blocked layout contract (ecx_rs_blocked_layout, include/ecx.h)
+    def blockedLayout(self, byteCount: int):
+        """(block_bytes, full blocks, tail bytes) of the recommended blocked layout of this
+        code's stripes for a shard size (ecx_rs_blocked_layout)."""
+        out = np.zeros(3, np.int64)
+        check(lib().ecx_rs_blocked_layout(self.dataShardCount, self.parityShardCount, byteCount, out.ctypes.data))
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def recommendedPitch(self, byteCount: int) -> int:
+        """The recommended shard pitch of the plain [stripe][shard][pitch] layout (ecx_rs_recommended_pitch)."""
+        out = np.zeros(1, np.int64)
+        check(lib().ecx_rs_recommended_pitch(self.dataShardCount, self.parityShardCount, byteCount,
+                                             out.ctypes.data))
+        return int(out[0])
+
+    def encodeParityBlockedBatch(self, base, nstripes, byteCount, blockBytes=0, stream=None):
+        """encodeParity over nstripes stripes in the blocked layout, in place
+        (ecx_rs_encode_parity_blocked_batch; blockBytes 0 = the recommended block)."""
+        _check_extent(base, nstripes * self.getTotalShardCount() * byteCount, "base")
+        check(lib().ecx_rs_encode_parity_blocked_batch(self._h, _dev_ptr(base), nstripes, byteCount, blockBytes,
+                                                       _stream(stream)))
+
+    def decodeMissingBlockedBatch(self, base, shardPresent, nstripes, byteCount, blockBytes=0, stream=None):
+        """decodeMissing over nstripes stripes in the blocked layout, in place
+        (ecx_rs_decode_missing_blocked_batch)."""
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        if len(pres) != self.getTotalShardCount():
+            raise EcxError(-1, "wrong number of shardPresent flags")
+        _check_extent(base, nstripes * self.getTotalShardCount() * byteCount, "base")
+        check(lib().ecx_rs_decode_missing_blocked_batch(self._h, pres.ctypes.data, _dev_ptr(base), nstripes,
+                                                        byteCount, blockBytes, _stream(stream)))
 
     def isParityCorrectBatch(self, shards, stripe_stride, shard_stride, nstripes, firstByte, byteCount, verdict,
                              stream=None) -> None:

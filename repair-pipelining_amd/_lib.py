@@ -101,6 +101,10 @@ SIGNATURES = {
     "ecx_map_matrix": (I, [P, P, P, P]),
     "ecx_map_slot_extent": (I, [P, PI, PI]),
     "ecx_map_apply_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
+    "ecx_rs_blocked_layout": (I, [I, I, I64, P]),
+    "ecx_rs_recommended_pitch": (I, [I, I, I64, P]),
+    "ecx_rs_encode_parity_blocked_batch": (I, [P, P, I64, I64, I64, P]),
+    "ecx_rs_decode_missing_blocked_batch": (I, [P, P, P, I64, I64, I64, P]),
     "ecx_map_accumulate_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_rs_decode_map": (I, [P, P, ctypes.POINTER(P)]),

@@ -557,6 +557,104 @@ int ecx_rs_decode_missing_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_
     });
 }
 
+namespace {
+// The plain layout's pitch (scripts/rs_layout_contract.py): the smallest
+// ODD multiple of 4 KiB at or above the shard.  4 KiB-aligned shards run full-chunk kernels only,
+// and an odd count keeps the streams off the power-of-two boundaries whose address bits the HBM
+// interleave does not spread (section 4, "Where the streams collide": 4 MiB + 4 KiB, not 4 MiB).
+int64_t recommended_pitch(int64_t byte_count) {
+    constexpr int64_t kStep = 4 << 10;
+    int64_t c = (byte_count + kStep - 1) / kStep;
+    if (c % 2 == 0 && c > 0) ++c;
+    return c * kStep;
+}
+
+// The blocked layout's block: the largest power of two with n blocks
+// (one per shard of a stripe) within 1 MiB, 4 KiB..1 MiB -- 32 KiB for RS(17,3) (0.76 of HBM),
+// 64 KiB for RS(12,4) (0.816); one block of byte_count bytes for smaller shards.
+int64_t recommended_block(int n, int64_t byte_count) {
+    int64_t b = 1 << 20;
+    while (b > (4 << 10) && b * n > (1 << 20)) b >>= 1;
+    return byte_count >= b ? b : byte_count;
+}
+
+int64_t resolve_block(int n, int64_t byte_count, int64_t block_bytes) {
+    if (block_bytes < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative block size");
+    return block_bytes == 0 ? recommended_block(n, byte_count) : block_bytes;
+}
+
+// The map over a blocked batch (ecx.h): the full blocks as nstripes * full "stripes" of n
+// block-sized slots, then the tails as nstripes stripes of n tail-sized slots.
+void launch_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block,
+                    hipStream_t stream) {
+    if (nstripes == 0 || byte_count == 0) return;
+    const int64_t full = byte_count / block, tail = byte_count % block;
+    int64_t stride = 0, units = 0, body = 0;
+    if (__builtin_mul_overflow((int64_t)n, block, &stride) || __builtin_mul_overflow(nstripes, full, &units) ||
+        __builtin_mul_overflow(units, stride, &body))
+        throw Error(ECX_E_ILLEGAL_ARGUMENT, "blocked batch extent overflows");
+    if (full > 0) launch_apply(cm, base, stride, block, base, stride, block, units, block, stream);
+    if (tail > 0) {
+        uint8_t *t = base + body;
+        launch_apply(cm, t, (int64_t)n * tail, tail, t, (int64_t)n * tail, tail, nstripes, tail, stream);
+    }
+}
+}  // namespace
+
+int ecx_rs_blocked_layout(int data_shards, int parity_shards, int64_t byte_count, int64_t *layout) {
+    return guarded(__func__, [&]() -> int {
+        if (!layout) throw Error(ECX_E_NULL, "null layout");
+        if (byte_count < 0 || data_shards <= 0 || parity_shards <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "bad shape");
+        if (data_shards + parity_shards > 256) throw Error(ECX_E_TOO_MANY_SHARDS, "too many shards - max is 256");
+        const int64_t b = recommended_block(data_shards + parity_shards, byte_count);
+        layout[0] = b;
+        layout[1] = b ? byte_count / b : 0;
+        layout[2] = b ? byte_count % b : 0;
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_recommended_pitch(int data_shards, int parity_shards, int64_t byte_count, int64_t *pitch) {
+    return guarded(__func__, [&]() -> int {
+        if (!pitch) throw Error(ECX_E_NULL, "null pitch");
+        if (byte_count < 0 || data_shards <= 0 || parity_shards <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "bad shape");
+        if (data_shards + parity_shards > 256) throw Error(ECX_E_TOO_MANY_SHARDS, "too many shards - max is 256");
+        *pitch = recommended_pitch(byte_count);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_encode_parity_blocked_batch(ecx_rs *rs, uint8_t *base, int64_t nstripes, int64_t byte_count,
+                                       int64_t block_bytes, void *stream) {
+    return guarded(__func__, [&]() -> int {
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!base) throw Error(ECX_E_NULL, "null device pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_encode_map(rs, &m);
+        if (st) return st;
+        const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
+        launch_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block,
+                       (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_decode_missing_blocked_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base, int64_t nstripes,
+                                        int64_t byte_count, int64_t block_bytes, void *stream) {
+    return guarded(__func__, [&]() -> int {
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (!base) throw Error(ECX_E_NULL, "null device pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_decode_map(rs, shard_present, &m);  // Not enough shards -> -2
+        if (st) return st;
+        const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
+        if (m->cm.map().n_out == 0) return ECX_OK;  // all present (ReedSolomon.java:216-218)
+        launch_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block,
+                       (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
 int ecx_rs_encode_parity(ecx_rs *rs, uint8_t *const *shards, int shard_count, int shard_length, int offset,
                          int byte_count) {
     return guarded(__func__, [&]() -> int {

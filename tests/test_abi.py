@@ -361,3 +361,34 @@ def test_multi_gpu_host_batch_split_matches_shard_stripes(ecx):
             assert prev == n
     for bad in ((-1, 2, 0), (5, 0, 0), (5, 2, 2), (5, 2, -1)):
         assert f(*bad, ctypes.byref(b), ctypes.byref(e)) == -1
+
+
+def test_rs_blocked_layout_contract(ecx):
+    """The RS layout contract (ecx_rs_blocked_layout / ecx_rs_recommended_pitch):
+    64 KiB blocks (one block below that), the full / tail split, the plain layout's pitch; and
+    blocked_pack / blocked_unpack, the torch helpers that lay a [stripes][n][L] batch out that
+    way, are exact inverses over exactly stripes * n * L bytes (CPU tensors here)."""
+    import torch
+    r173, r124 = ecx.ReedSolomon.create(17, 3), ecx.ReedSolomon.create(12, 4)
+    assert r173.blockedLayout(200000) == (32768, 6, 200000 - 6 * 32768)
+    assert r124.blockedLayout(4 << 20) == (65536, 64, 0)
+    assert ecx.ReedSolomon.create(4, 2).blockedLayout(32768) == (32768, 1, 0)  # 6 shards: 128 KiB blocks
+    assert r173.blockedLayout(34) == (34, 1, 0) and r173.blockedLayout(0) == (0, 0, 0)
+    assert ecx.ReedSolomon.create(128, 128).blockedLayout(1 << 20)[0] == 4096  # never below 4 KiB
+    for L in (200000, 4 << 20, 104449, 34816, 1, 4096):
+        p = r173.recommendedPitch(L)
+        assert p >= L and p % 4096 == 0 and (p // 4096) % 2 == 1 and p - L < 8192, (L, p)
+    assert r124.recommendedPitch(4 << 20) == (4 << 20) + 4096 and r173.recommendedPitch(200000) == 200704
+    with pytest.raises(ecx.EcxError):
+        r173.blockedLayout(-1)
+    g = torch.Generator().manual_seed(3)
+    for S, n, L, b in ((3, 20, 200000, 65536), (2, 16, 3 * 4096, 4096), (2, 5, 1001, 64), (1, 4, 64, 64)):
+        x = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, generator=g)
+        flat = ecx.blocked_pack(x, b)
+        assert flat.numel() == S * n * L
+        full, tail = divmod(L, b)
+        if full:  # stripe 0, block 1 (or 0), shard 2 sits where the layout says
+            t = min(1, full - 1)
+            at = (t * n + 2) * b
+            assert torch.equal(flat[at:at + b], x[0, 2, t * b:(t + 1) * b])
+        assert torch.equal(ecx.blocked_unpack(flat, S, n, L, b), x)
