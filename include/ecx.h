@@ -226,6 +226,15 @@ int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_e
  * results equal the reference Clay(12,4) run with the virtual nodes zero-filled. */
 int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
                               ecx_clay **out);
+/* ecx_clay_create_shortened with flags.  ECX_CLAY_IS_TEST: the single-node repair's plane
+ * decode takes decodeDecoupledPlane's -DisTest=true branch (ClayCodeErasureDecodingStep.java:
+ * 571-581): decodeMissingSingle per helper, assuming the erased row is nodes 0..q-1 (bug B2).
+ * For the other rows it computes the reference's (different) map, and where that row holds a
+ * parity node the reference throws NullPointerException (B3): ECX_E_NULL from performCoding.
+ * Multi-erasure decodes (and encode) are unaffected, as in the reference. */
+enum { ECX_CLAY_IS_TEST = 1 };
+int ecx_clay_create_ex(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased, int flags,
+                       ecx_clay **out);
 void ecx_clay_destroy(ecx_clay *clay); /* drops one reference (see ecx_rs_create) */
 int ecx_clay_geometry(const ecx_clay *clay, int *q, int *t, int *alpha); /* ClayCodeUtil :690-695 */
 int ecx_clay_helper_planes(const ecx_clay *clay, int erased_index, int *out /* alpha */); /* :924-941 */

@@ -128,10 +128,12 @@
  *   "host_exec_kib"    per-call host entry points (the CodingLoop / ReedSolomon / Clay byte[][] calls):
  *                      byte counts up to this many KiB run on the calling thread (host_exec.cpp:
  *                      AVX-512 GFNI affine multiplies, else AVX2 nibble tables) instead of a device
- *                      round trip (default 8, a policy: on one core the executor beat the device at
- *                      every size measured, profiles/r05_percall_threshold.jsonl; 0 = every
- *                      call on the device).  Never a fallback: without a HIP device these calls
- *                      fail with ECX_E_DEVICE like the device path
+ *                      round trip (default 1024: the measured crossover -- one caller thread, the
+ *                      device first beats the executor at 2 MiB on Clay(4,2) performCoding and at no
+ *                      size up to 4 MiB on the RS(2,2) pair; 16 caller threads, at no size;
+ *                      profiles/r06_percall_threshold.jsonl; 0 = every call on the device).  Never a
+ *                      fallback: without a HIP device these calls fail with ECX_E_DEVICE like the
+ *                      device path
  *   "host_zero_copy"   per-call host entry points on the gather path: 1 = the kernel reads and
  *                      writes the pinned staging area over PCIe (no DMA copies; default);
  *                      0 = one H2D and one D2H copy

@@ -139,6 +139,7 @@ RULES = {
     "ecx_rs_decode_partial_batch": (("rs",), [A("shard_present", RS_N)]),
     "ecx_clay_create": ((), [NN("n_erased"), A("erased", "n_erased")]),
     "ecx_clay_create_shortened": ((), [NN("n_erased"), A("erased", "n_erased")]),
+    "ecx_clay_create_ex": ((), [NN("n_erased"), A("erased", "n_erased")]),
     "ecx_clay_geometry": ((), [A("q", "1"), A("t", "1"), A("alpha", "1")]),
     "ecx_clay_shape": ((), [A("nodes", "1"), A("n_erased", "1"), A("alpha", "1")]),
     "ecx_clay_helper_planes": (("clay",), [A("out", "cl_a / (cl_q > 0 ? cl_q : 1)")]),

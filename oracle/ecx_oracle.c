@@ -449,6 +449,7 @@ struct orc_clay {
     int k, m, n, q, t, alpha;
     int *erased;
     int n_erased;
+    int is_test; /* -DisTest=true: decodeDecoupledPlane's isTest branch on single repairs (:571-581) */
     orc_rs *pair; /* ReedSolomon.create(2,2) -- ClayCode.java:33 */
     orc_rs *rs;   /* ReedSolomon.create(k,m) -- ClayCode.java:34 */
 };
@@ -487,6 +488,13 @@ static int ipow(int b, int e) {
 }
 
 /* ClayCodeUtil ctor :690-695 (t is INTEGER division, alpha = q^t) */
+int orc_clay_create_ex(int data_units, int parity_units, const int *erased, int n_erased, int is_test,
+                       orc_clay **out) {
+    int st = orc_clay_create(data_units, parity_units, erased, n_erased, out);
+    if (st == ORC_OK) (*out)->is_test = is_test != 0;
+    return st;
+}
+
 int orc_clay_create(int data_units, int parity_units, const int *erased, int n_erased, orc_clay **out) {
     *out = NULL;
     if (parity_units <= 0 || data_units <= 0) return ORC_E_ILLEGAL_ARGUMENT;
@@ -616,6 +624,34 @@ static int decode_decoupled_plane(orc_clay *c, arena_t *ar, uint8_t **plane, con
     return ORC_OK;
 }
 
+/* decodeDecoupledPlane :542-597 with -DisTest=true on a single repair (isSingle), the branch
+ * of :571-581: after the same tmpOutputs / getShardPresent / getByteArray preamble (:548-567),
+ * for i = 0 .. n-|E|-1: rsRawDecoder.decodeMissingSingle(decoupledPlaneAsBytes[i + |E|],
+ * i + |E|, i, shardPresent, outputs, 0, bufSize, i == 0) into the fresh byte[|E|][bufSize]
+ * `outputs` (:569), then decoupledPlaneAsBytes[erasedIndexes[i]] = outputs[i] (:579-581).
+ * It takes shard i + |E| as the i-th present one (bug B2); a missing parity shard has no
+ * matrix row, the reference's NullPointerException (B3, orc_rs_decode_missing_single). */
+static int decode_decoupled_plane_is_test(orc_clay *c, arena_t *ar, uint8_t **plane, const int *erased, int ne) {
+    int n = c->n, nulls = 0;
+    uint8_t *arr[256], *outs[64];
+    uint8_t present[256];
+    for (int i = 0; i < n; i++)
+        if (plane[i] == NULL) nulls++;
+    if (nulls > ne) return ORC_E_INDEX; /* tmpOutputs[r++] overflow (:556-562) */
+    if (ne > 64) return ORC_E_INDEX;
+    for (int i = 0; i < n; i++) arr[i] = plane[i] ? plane[i] : arena_zero(ar); /* getByteArray :599-609 */
+    for (int i = 0; i < n; i++) present[i] = 1;
+    for (int i = 0; i < ne; i++)
+        if (erased[i] < n) present[erased[i]] = 0;
+    for (int j = 0; j < ne; j++) outs[j] = arena_zero(ar); /* new byte[erasedIndexes.length][bufSize] */
+    for (int i = 0; i < n - ne; i++) {
+        int st = orc_rs_decode_missing_single(c->rs, arr[i + ne], i + ne, i, present, outs, ne, 0, ar->size, i == 0);
+        if (st) return st;
+    }
+    for (int j = 0; j < ne; j++) plane[erased[j]] = outs[j];
+    return ORC_OK;
+}
+
 /* getDecoupledHelperPlane :435-492.  helper[hp*n + node] */
 static int decoupled_helper_plane(orc_clay *c, arena_t *ar, uint8_t *const *helper, const int *hidx, int nh,
                                   int hp, int erased, uint8_t **temp) {
@@ -655,7 +691,8 @@ static int decode_single_plane(orc_clay *c, arena_t *ar, uint8_t *const *helper,
     for (int j = 0; j < n; j++) plane[j] = NULL;
     int st = decoupled_helper_plane(c, ar, helper, hidx, nh, i, erased, plane);
     if (st) return st;
-    st = decode_decoupled_plane(c, ar, plane, column, c->q);
+    st = c->is_test ? decode_decoupled_plane_is_test(c, ar, plane, column, c->q)
+                    : decode_decoupled_plane(c, ar, plane, column, c->q);
     if (st) return st;
     for (int x = 0; x < c->q; x++) {
         int node = node_index(c, x, y);

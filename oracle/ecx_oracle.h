@@ -92,6 +92,9 @@ int orc_rs_decode_missing_single(orc_rs *rs, const uint8_t *shard, int shard_ind
 /* ---- ClayCodeErasureDecodingStep.java / ClayCode.java / ClayCodeHelper.kt ---- */
 typedef struct orc_clay orc_clay;
 int orc_clay_create(int data_units, int parity_units, const int *erased, int n_erased, orc_clay **out);
+/* is_test != 0: the reference run with -DisTest=true (decodeDecoupledPlane :571-581 on single repairs) */
+int orc_clay_create_ex(int data_units, int parity_units, const int *erased, int n_erased, int is_test,
+                       orc_clay **out);
 void orc_clay_free(orc_clay *c);
 int orc_clay_q(const orc_clay *c);
 int orc_clay_t(const orc_clay *c);

@@ -86,6 +86,7 @@ def _load():
         "orc_rs_decode_missing": (I, [P, PP, P, I, I, I, I]),
         "orc_rs_decode_missing_single": (I, [P, P, I, I, P, PP, I, I, I, I]),
         "orc_clay_create": (I, [I, I, P, I, ctypes.POINTER(P)]),
+        "orc_clay_create_ex": (I, [I, I, P, I, I, ctypes.POINTER(P)]),
         "orc_clay_free": (None, [P]),
         "orc_clay_alpha": (I, [P]),
         "orc_clay_q": (I, [P]),
@@ -286,10 +287,12 @@ class ReedSolomon:
 class Clay:
     """ClayCodeErasureDecodingStep + ClayCode restated."""
 
-    def __init__(self, data_units: int, parity_units: int, erased_indexes):
+    def __init__(self, data_units: int, parity_units: int, erased_indexes, is_test: bool = False):
+        """is_test: the reference run with -DisTest=true (decodeDecoupledPlane :571-581)."""
         er = np.ascontiguousarray(list(erased_indexes), dtype=np.int32)
         h = ctypes.c_void_p()
-        _check(lib().orc_clay_create(data_units, parity_units, _ptr(er), len(er), ctypes.byref(h)))
+        _check(lib().orc_clay_create_ex(data_units, parity_units, _ptr(er), len(er), 1 if is_test else 0,
+                                        ctypes.byref(h)))
         self._h = h
         self.k, self.m = data_units, parity_units
         self.n = data_units + parity_units

@@ -795,16 +795,22 @@ class ClayCodeUtil:
 class ClayCodeErasureDecodingStep:
     """new ClayCodeErasureDecodingStep(erasedIndexes, RS(2,2), RS(k,m)) (:43-51)."""
 
-    def __init__(self, erasedIndexes, numDataUnits: int, numParityUnits: int, virtualUnits: int = 0):
+    def __init__(self, erasedIndexes, numDataUnits: int, numParityUnits: int, virtualUnits: int = 0,
+                 isTest: bool = False):
         """virtualUnits > 0: shortened code, Clay(k+v, m) with v virtual zero data nodes
-        (e.g. Clay(10,4) = ClayCodeErasureDecodingStep(e, 10, 4, virtualUnits=2))."""
+        (e.g. Clay(10,4) = ClayCodeErasureDecodingStep(e, 10, 4, virtualUnits=2)).  isTest: the
+        reference run with -DisTest=true (decodeDecoupledPlane :571-581, ecx_clay_create_ex)."""
         er = np.ascontiguousarray(list(erasedIndexes), np.int32)
         h = ctypes.c_void_p()
-        if virtualUnits:
+        if isTest:
+            check(lib().ecx_clay_create_ex(numDataUnits, numParityUnits, virtualUnits, er.ctypes.data, len(er),
+                                           1, ctypes.byref(h)))
+        elif virtualUnits:
             check(lib().ecx_clay_create_shortened(numDataUnits, numParityUnits, virtualUnits, er.ctypes.data,
                                                   len(er), ctypes.byref(h)))
         else:
             check(lib().ecx_clay_create(numDataUnits, numParityUnits, er.ctypes.data, len(er), ctypes.byref(h)))
+        self.isTest = isTest
         self._h = h
         self.erasedIndexes = list(erasedIndexes)
         self.numDataUnits, self.numParityUnits = numDataUnits, numParityUnits

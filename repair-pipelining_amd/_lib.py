@@ -115,6 +115,7 @@ SIGNATURES = {
     "ecx_rs_encode_partial_batch": (I, [P, I, P, I64, P, I64, I64, I64, I64, I, P]),
     "ecx_clay_create": (I, [I, I, P, I, ctypes.POINTER(P)]),
     "ecx_clay_create_shortened": (I, [I, I, I, P, I, ctypes.POINTER(P)]),
+    "ecx_clay_create_ex": (I, [I, I, I, P, I, I, ctypes.POINTER(P)]),
     "ecx_clay_destroy": (None, [P]),
     "ecx_clay_geometry": (I, [P, PI, PI, PI]),
     "ecx_clay_helper_planes": (I, [P, I, P]),

@@ -181,9 +181,10 @@ int ipow(int b, int e) {
 }
 }  // namespace
 
-ClayPlanner::ClayPlanner(int data_units, int parity_units, std::vector<int> erased, int virtual_units)
-    : k_(data_units + virtual_units), m_(parity_units), v_(virtual_units), erased_real_(std::move(erased)),
-      pair_(2, 2), rs_(data_units + virtual_units, parity_units) {
+ClayPlanner::ClayPlanner(int data_units, int parity_units, std::vector<int> erased, int virtual_units,
+                         bool is_test)
+    : k_(data_units + virtual_units), m_(parity_units), v_(virtual_units), is_test_(is_test),
+      erased_real_(std::move(erased)), pair_(2, 2), rs_(data_units + virtual_units, parity_units) {
     if (parity_units <= 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "invalid unit counts");
     for (int e : erased_real_) {
         if (v_ > 0 && (e < 0 || e >= n_real())) throw Error(ECX_E_INDEX, "erased index out of range");
@@ -268,8 +269,14 @@ SymBuf ClayPlanner::pair_couple(SymBuf a, SymBuf a2, SymBuf b, SymBuf b2, int wi
     return arr[lost[0]];
 }
 
-// decodeDecoupledPlane (:542-597), default (non-isTest) branch.
-void ClayPlanner::decode_plane(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width) const {
+// decodeDecoupledPlane (:542-597): the default branch (decodeMissing), or for a single repair of
+// an is_test planner the -DisTest=true branch (:571-581).
+void ClayPlanner::decode_plane(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width,
+                               bool single) const {
+    if (single && is_test_) {
+        decode_plane_is_test(plane, erased, width);
+        return;
+    }
     int nulls = 0;
     for (auto &p : plane) nulls += !p;
     if (nulls > (int)erased.size()) throw Error(ECX_E_INDEX, "more absent shards than erasures in a plane");
@@ -282,6 +289,52 @@ void ClayPlanner::decode_plane(std::vector<SymBuf> &plane, const std::vector<int
     for (int e : erased) plane[e] = arr[e];
     for (auto &p : plane)
         if (!p) throw Error(ECX_E_NULL, "absent shard in a decoupled plane");
+}
+
+// decodeDecoupledPlane's isTest branch (:571-581): for i in 0 .. n-|E|-1,
+// decodeMissingSingle(plane[i + |E|], shardIndex i + |E|, index i, ..., isFirst = i == 0)
+// (ReedSolomon.java:288-333) -- i.e. shard i + |E| is taken as the i-th of the first k
+// present shards, which holds only when the erased indices are 0..|E|-1 (bug B2: otherwise
+// the map differs, reading the zero arrays getByteArray made for the erased rows).  Each call
+// inverts the first-k-present submatrix; when isFirst and shardIndex < k it replaces the
+// output of every missing DATA shard with a fresh array; it then writes outputs[j] (=, or ^=)
+// rows[j][index] * shard for every j < |E|, and a missing PARITY shard has no row: the
+// reference's NullPointerException (bug B3), here ECX_E_NULL.  The outputs replace the erased
+// entries of the plane.
+void ClayPlanner::decode_plane_is_test(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width) const {
+    const int nn = (int)plane.size(), ne = (int)erased.size();
+    std::vector<SymBuf> arr(plane.size());  // getByteArray: a null entry becomes a fresh zero array
+    for (int i = 0; i < nn; ++i) arr[(size_t)i] = plane[(size_t)i] ? plane[(size_t)i] : zeros(width);
+    std::vector<bool> present((size_t)nn, true);
+    for (int e : erased)
+        if (e < nn) present[(size_t)e] = false;
+    int np = 0;
+    for (bool p : present) np += p ? 1 : 0;
+    if (np < k_) throw Error(ECX_E_NOT_ENOUGH_SHARDS, "Not enough shards present");  // the inversion's submatrix
+    std::vector<SymBuf> outputs((size_t)ne);  // new byte[|E|][bufSize]
+    for (auto &o : outputs) o = zeros(width);
+    std::vector<int> used;
+    const Matrix dec = rs_.data_decoder(present, &used);
+    std::vector<int> missing_data;  // matrixRows: D^-1 rows of the missing data shards, ascending
+    for (int i = 0; i < k_; ++i)
+        if (!present[(size_t)i]) missing_data.push_back(i);
+    for (int i = 0; i < nn - ne; ++i) {
+        const SymBuf shard = arr[(size_t)(i + ne)];
+        const int shard_index = i + ne;
+        const bool first = i == 0;
+        if (shard_index < k_ && first)
+            for (size_t j = 0; j < missing_data.size(); ++j) outputs[j] = zeros(width);
+        for (int j = 0; j < ne; ++j) {
+            if (j >= (int)missing_data.size())
+                throw Error(ECX_E_NULL, "decodeMissingSingle: no matrix row for a missing parity shard (isTest branch)");
+            if (i >= k_) throw Error(ECX_E_INDEX, "decodeMissingSingle: index beyond the data shards (isTest branch)");
+            const uint8_t c = dec.at(missing_data[(size_t)j], i);
+            std::vector<uint8_t> acc = first ? std::vector<uint8_t>((size_t)width, 0) : *outputs[(size_t)j];
+            axpy(acc, c, *shard);
+            *outputs[(size_t)j] = std::move(acc);
+        }
+    }
+    for (int j = 0; j < ne; ++j) plane[(size_t)erased[(size_t)j]] = outputs[(size_t)j];
 }
 
 // Body of both doDecodeSingle overloads for helper plane i (:171-203, :255-281).
@@ -310,7 +363,7 @@ void ClayPlanner::single_plane(const std::vector<SymBuf> &helper, const std::vec
     }
     std::vector<int> column;
     for (int x = 0; x < q_; ++x) column.push_back(node(x, ey));
-    decode_plane(plane, column, width);
+    decode_plane(plane, column, width, true);
     for (int x = 0; x < q_; ++x) {
         const int nd = node(x, ey);
         if (nd == e) {

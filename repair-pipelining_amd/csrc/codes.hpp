@@ -116,7 +116,11 @@ struct ClayRepairProgram {
 // k + m REAL nodes (real node r < k is underlying r, r >= k is r + v).
 class ClayPlanner {
 public:
-    ClayPlanner(int data_units, int parity_units, std::vector<int> erased, int virtual_units = 0);
+    // is_test: the single-repair plane decode takes decodeDecoupledPlane's -DisTest=true branch
+    // (ClayCodeErasureDecodingStep.java:571-581, decodeMissingSingle per helper, bug B2 included).
+    ClayPlanner(int data_units, int parity_units, std::vector<int> erased, int virtual_units = 0,
+                bool is_test = false);
+    bool is_test() const { return is_test_; }
     int k() const { return k_; }
     int m() const { return m_; }
     int n() const { return k_ + m_; }           // underlying code
@@ -145,6 +149,7 @@ public:
 
 private:
     int k_, m_, v_, q_, t_, alpha_;
+    bool is_test_ = false;
     std::vector<int> erased_;       // underlying node indices
     std::vector<int> erased_real_;  // as given (real node indices)
     int under(int real_node) const { return real_node < k_ - v_ ? real_node : real_node + v_; }
@@ -162,7 +167,9 @@ private:
     bool is_erased(int idx) const;
 
     SymBuf pair_couple(SymBuf a, SymBuf a2, SymBuf b, SymBuf b2, int width) const;
-    void decode_plane(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width) const;
+    void decode_plane(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width,
+                      bool single = false) const;
+    void decode_plane_is_test(std::vector<SymBuf> &plane, const std::vector<int> &erased, int width) const;
     void single_plane(const std::vector<SymBuf> &helper, const std::vector<int> &hidx, int i, int e,
                       std::vector<SymBuf> &outputs, int width) const;
     void decode_multi(std::vector<SymBuf> in, std::vector<SymBuf> &outputs, int width) const;

@@ -35,7 +35,7 @@ struct ecx_rs {
 };
 
 struct ecx_clay {
-    ecx_clay(int k, int m, std::vector<int> e, int v = 0) : pl(k, m, std::move(e), v) {}
+    ecx_clay(int k, int m, std::vector<int> e, int v = 0, bool is_test = false) : pl(k, m, std::move(e), v, is_test) {}
     ClayPlanner pl;
     bool shared = false;  // owned by the process-wide codec registry (ecx_clay_create)
     std::mutex mu;
@@ -321,8 +321,8 @@ Registry<ecx_rs, std::pair<int, int>> &rs_registry() {
     static Registry<ecx_rs, std::pair<int, int>> r;
     return r;
 }
-Registry<ecx_clay, std::tuple<int, int, int, std::vector<int>>> &clay_registry() {
-    static Registry<ecx_clay, std::tuple<int, int, int, std::vector<int>>> r;
+Registry<ecx_clay, std::tuple<int, int, int, std::vector<int>, int>> &clay_registry() {
+    static Registry<ecx_clay, std::tuple<int, int, int, std::vector<int>, int>> r;
     return r;
 }
 }  // namespace
@@ -923,12 +923,21 @@ int ecx_clay_create(int data_units, int parity_units, const int *erased, int n_e
 
 int ecx_clay_create_shortened(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased,
                               ecx_clay **out) {
+    return ecx_clay_create_ex(data_units, parity_units, virtual_units, erased, n_erased, 0, out);
+}
+
+int ecx_clay_create_ex(int data_units, int parity_units, int virtual_units, const int *erased, int n_erased, int flags,
+                       ecx_clay **out) {
     return guarded(__func__, [&]() -> int {
+        if (!out) throw Error(ECX_E_NULL, "null out");
         *out = nullptr;
         if (n_erased < 0 || virtual_units < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "n_erased / virtual_units");
+        if (flags & ~ECX_CLAY_IS_TEST) throw Error(ECX_E_ILLEGAL_ARGUMENT, "unknown Clay flags");
+        if (n_erased > 0 && !erased) throw Error(ECX_E_NULL, "null erased list");
         const std::vector<int> e(erased, erased + n_erased);  // order matters (the reference's erasedIndexes)
-        *out = clay_registry().get(std::make_tuple(data_units, parity_units, virtual_units, e),
-                                   [&] { return new ecx_clay(data_units, parity_units, e, virtual_units); });
+        const bool is_test = (flags & ECX_CLAY_IS_TEST) != 0;
+        *out = clay_registry().get(std::make_tuple(data_units, parity_units, virtual_units, e, flags),
+                                   [&] { return new ecx_clay(data_units, parity_units, e, virtual_units, is_test); });
         return ECX_OK;
     });
 }

@@ -355,8 +355,10 @@ struct Tuning {
     int64_t host_gather_max = 512 << 10;
     int host_contexts = 1;  // per-call host APIs: 1 = a pool of contexts (streams) leased per call, 0 = one per device
     // per-call host APIs: byte counts up to this run on the calling thread (host_exec.cpp) instead of
-    // the device -- below the measured per-call crossover (profiles/r05_percall_threshold.jsonl); 0 = never
-    int64_t host_exec_max = 8 << 10;
+    // the device -- the measured per-call crossover (profiles/r06_percall_threshold.jsonl): with one
+    // caller thread the device first wins at 2 MiB (Clay(4,2) performCoding; the RS(2,2) pair never,
+    // to 4 MiB), with 16 at no size to 4 MiB; 0 = never
+    int64_t host_exec_max = 1 << 20;
     // single-tile maps: (stripe, chunk) units per workgroup with one load ring across them
     // (k_gf_apply_multi, apply_multi.hip): 1 = one unit per workgroup (k_gf_apply), 2 or 4
     int units = 1;

@@ -4,19 +4,23 @@
 // call of (a) libecx on the device (host_exec_kib 0), (b) libecx's host executor (host_exec_kib
 // large), (c) libecx's default, and (d) the oracle (the restated reference loop, liborc.so: the
 // baseline the drop-in is compared with), and checks that all outputs agree byte for byte.
-// One JSON line per (case, bytes).
+// One JSON line per (case, bytes).  With `--threads T`: the same sites from T caller threads at
+// once, sizes 2 KiB - 4 MiB (or up to an optional third argument; concurrent_main below).
 //
 //   case "rs31_single"  LRC chain word: RS(3,1) encodeParitySingle (NodeHelper.kt:89)
 //   case "rs22_pair"    Clay pair transform: RS(2,2) decodeMissing, 2 of 4 present (ClayCodeNode.kt:125-132)
 //   case "rs42_encode"  SampleEncoder: RS(4,2) encodeParity (SampleEncoder.java:83)
 //   case "clay42"       Clay(4,2) performCoding, node 1 erased (ClayCodeHelper.kt:90, ClayCodeRunner)
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ecx.h"
@@ -58,8 +62,122 @@ void emit(const char *cas, int bytes, double dev, double hx, double def, double 
 }
 }  // namespace
 
-int main() {
-    const int default_kib = 8;
+// ---- concurrent callers: the reference's drop-in sites run on one handler
+// thread per node object (ClayCodeNode.kt:38-40, :125-132, :271-274), so the per-call threshold is
+// measured with T caller threads at once, each on its own buffers: for each size, the aggregate
+// calls per second with every call on the device (host_exec_kib 0: leased per-call contexts,
+// separate streams) and on the host executor (host_exec_kib 1 GiB: the calling thread's core).
+// One JSON line per (case, threads, bytes); "crossover" rows name the smallest size at which the
+// device path's aggregate rate beats the host executor's.
+struct Site {
+    const char *name;
+    int in_slots, out_slots;
+    std::function<int(uint8_t *const *, uint8_t *const *, int)> call;  // (inputs, outputs, bytes)
+};
+
+double aggregate_calls_per_s(const Site &site, int threads, int bytes, double seconds,
+                             std::vector<Bufs> &ins, std::vector<Bufs> &outs) {
+    std::vector<std::thread> th;
+    std::vector<long> done((size_t)threads, 0);
+    std::atomic<int> ready{0}, bad{0};
+    std::atomic<bool> go{false};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> el((size_t)threads, 0.0);
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            if (site.call(ins[(size_t)t].p.data(), outs[(size_t)t].p.data(), bytes) < 0) bad.fetch_add(1);  // warm
+            ready.fetch_add(1);
+            while (!go.load()) std::this_thread::yield();
+            const auto s0 = std::chrono::steady_clock::now();
+            long n = 0;
+            double e = 0.0;
+            do {
+                if (site.call(ins[(size_t)t].p.data(), outs[(size_t)t].p.data(), bytes) < 0) bad.fetch_add(1);
+                ++n;
+                e = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+            } while (e < seconds);
+            done[(size_t)t] = n;
+            el[(size_t)t] = e;
+        });
+    while (ready.load() < threads) std::this_thread::yield();
+    go.store(true);
+    for (auto &x : th) x.join();
+    (void)t0;
+    if (bad.load()) return -1.0;
+    double rate = 0.0;
+    for (int t = 0; t < threads; ++t) rate += (double)done[(size_t)t] / el[(size_t)t];
+    return rate;
+}
+
+int concurrent_main(int threads, int max_bytes) {
+    int default_kib = 0;
+    ecx_tune_value("host_exec_kib", &default_kib);
+    const int erased = 1;
+    ecx_rs *rs = nullptr;
+    ecx_clay *clay = nullptr;
+    if (ecx_rs_create(2, 2, &rs) || ecx_clay_create(4, 2, &erased, 1, &clay)) return 1;
+    const uint8_t present[4] = {1, 0, 1, 0};
+    std::vector<Site> sites = {
+        // RS(2,2) decodeMissing of the pair transform: 2 shards read, 2 rebuilt in place
+        {"rs22_pair", 4, 0,
+         [&](uint8_t *const *in, uint8_t *const *, int L) { return ecx_rs_decode_missing(rs, in, present, 4, L, 0, L); }},
+        // Clay(4,2) performCoding of node 1: 40 present sub-chunks in (20 used), 8 repaired out
+        {"clay42", 48, 8,
+         [&](uint8_t *const *in, uint8_t *const *out, int B) {
+             const uint8_t *ip[48];
+             for (int i = 0; i < 48; ++i) ip[i] = (i % 6) == erased ? nullptr : in[i];
+             return ecx_clay_perform_coding(clay, ip, out, B);
+         }},
+    };
+    const std::vector<int> sizes = {2048, 4096, 8192, 16384, 32768, 65536, 131072, 262144, 524288, 1 << 20,
+                                    2 << 20, 4 << 20};
+    for (const Site &site : sites) {
+        int crossover = -1;
+        for (int L : sizes) {
+            if (L > max_bytes) break;
+            std::vector<Bufs> ins, outs;
+            for (int t = 0; t < threads; ++t) {
+                ins.emplace_back(site.in_slots, L);
+                outs.emplace_back(std::max(1, site.out_slots), L);
+            }
+            // the two paths give the same bytes (thread 0's buffers, one call each)
+            Bufs a(site.in_slots, L), ao(std::max(1, site.out_slots), L);
+            std::vector<std::vector<uint8_t>> b = a.v, bo = ao.v;
+            std::vector<uint8_t *> pb((size_t)site.in_slots), pbo(bo.size());
+            for (size_t i = 0; i < b.size(); ++i) pb[i] = b[i].data();
+            for (size_t i = 0; i < bo.size(); ++i) pbo[i] = bo[i].data();
+            ecx_tune("host_exec_kib", 0);
+            const int s1 = site.call(a.p.data(), ao.p.data(), L);
+            ecx_tune("host_exec_kib", 1 << 20);
+            const int s2 = site.call(pb.data(), pbo.data(), L);
+            const bool same = s1 >= 0 && s2 >= 0 && a.v == b && ao.v == bo;
+            const double secs = 0.25;
+            ecx_tune("host_exec_kib", 0);
+            const double dev = aggregate_calls_per_s(site, threads, L, secs, ins, outs);
+            ecx_tune("host_exec_kib", 1 << 20);
+            const double host = aggregate_calls_per_s(site, threads, L, secs, ins, outs);
+            ecx_tune("host_exec_kib", default_kib);
+            if (crossover < 0 && dev > host) crossover = L;
+            std::printf("{\"case\": \"%s\", \"threads\": %d, \"bytes\": %d, \"device_calls_per_s\": %.1f, "
+                        "\"host_exec_calls_per_s\": %.1f, \"device_us_per_call\": %.2f, \"host_exec_us_per_call\": %.2f, "
+                        "\"outputs_agree\": %s}\n",
+                        site.name, threads, L, dev, host, dev > 0 ? threads * 1e6 / dev : -1.0,
+                        host > 0 ? threads * 1e6 / host : -1.0, same ? "true" : "false");
+            std::fflush(stdout);
+        }
+        std::printf("{\"case\": \"%s\", \"threads\": %d, \"crossover_bytes\": %d}\n", site.name, threads, crossover);
+        std::fflush(stdout);
+    }
+    ecx_rs_destroy(rs);
+    ecx_clay_destroy(clay);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 3 && std::strcmp(argv[1], "--threads") == 0)
+        return concurrent_main(std::atoi(argv[2]), argc >= 4 ? std::atoi(argv[3]) : (4 << 20));
+    int default_kib = 0;
+    ecx_tune_value("host_exec_kib", &default_kib);
     auto with_kib = [&](int kib, const std::function<int()> &f, int reps) {
         ecx_tune("host_exec_kib", kib);
         const double t = median_us(f, reps);

@@ -160,7 +160,7 @@ def test_tuning_keys(ecx):
     defaults = {"depth": 0, "nontemporal": 1, "xcd_group": 0, "lds_tables": 1, "store_scope": 0,
                 "chunk_major": 0, "stagger": 0, "block_threads": 0, "small_tiles": 2, "host_zero_copy": 1, "wide_tiles": 1, "skew_chunks": 1, "layout_select": 1, "plan_cache": 256, "roctx": 0, "host_contexts": 1, "clay_rtc": 1, "rtc_lookahead": 1, "rtc_waves": 3, "rtc_xcd": 2, "rtc_group": 1, "rtc_sched": 2, "rtc_nt": 5, "rtc_wide": 0, "xcd_run": 8, "xcd_misaligned": 1,
                 "map_planes": 1, "planes_lookahead": 12, "planes_waves": 2,
-                "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512, "host_exec_kib": 8}
+                "host_chunk_kib": 65536, "host_buffers": 3, "host_gather_kib": 512, "host_exec_kib": 1024}
     assert sorted(documented) == sorted(defaults)
     integration = (ROOT / "INTEGRATION.md").read_text()
     assert all("`%s`" % k in integration for k in documented), "INTEGRATION.md must list every tuning key"
@@ -322,7 +322,7 @@ f.argtypes, f.restype = [ctypes.c_char_p, ctypes.c_int], ctypes.c_int
 out = {}
 for k, v in [("layout_select", 1), ("plan_cache", 256), ("roctx", 0), ("host_chunk_kib", 65536),
              ("host_buffers", 3), ("host_gather_kib", 512), ("host_zero_copy", 1), ("host_contexts", 1),
-             ("host_exec_kib", 8),
+             ("host_exec_kib", 1024),
              ("depth", 0), ("nontemporal", 1), ("xcd_group", 0), ("stagger", 0), ("block_threads", 0),
              ("skew_chunks", 1), ("wide_tiles", 1), ("lds_tables", 1), ("store_scope", 0), ("rtc_nt", 5),
              ("clay_rtc", 1), ("map_planes", 1), ("small_tiles", 2), ("chunk_major", 0)]:

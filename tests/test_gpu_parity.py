@@ -252,6 +252,42 @@ def test_clay_perform_coding_vs_oracle(ecx, k, m, erased):
         assert (got[o] == ref[o]).all(), o
 
 
+@pytest.mark.parametrize("k,m,e", [(4, 2, 1), (4, 2, 2), (4, 2, 4), (12, 4, 5)])
+def test_clay_is_test_branch_on_device(ecx, torch_dev, k, m, e):
+    """The reference run with -DisTest=true (decodeDecoupledPlane :571-581, ecx_clay_create_ex):
+    per call and as a device batch, the repair equals the oracle's restatement of that branch on
+    random non-codeword inputs -- the default map for row 0 (e = 1), the branch's own map (bug B2)
+    for another row (e = 2; Clay(12,4) e = 5, where the composed-map kernel runs: the generated
+    plane-group kernel implements the default branch only) -- and a row holding a parity node
+    (e = 4) fails with NullPointerException's status (-6, bug B3) on both paths."""
+    torch = torch_dev
+    n = k + m
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, isTest=True)
+    a = step.subPacketSize
+    B = 4096
+    rng = np.random.default_rng(500 + e)
+    inputs = [None if (i % n) == e else rng.integers(0, 256, B, dtype=np.uint8) for i in range(n * a)]
+    got = [np.zeros(B, np.uint8) for _ in range(a)]
+    pool = torch.from_numpy(np.stack([x if x is not None else np.zeros(B, np.uint8) for x in inputs])).cuda()
+    out = torch.zeros((a, B), dtype=torch.uint8, device="cuda")
+    if e == 4:
+        with pytest.raises(ecx.EcxError) as ei:
+            step.performCoding(inputs, got, B)
+        assert ei.value.code == -6
+        with pytest.raises(ecx.EcxError) as ei:
+            step.performCodingBatch(pool, n * a * B, B, out, a * B, B, 1, B)
+        assert ei.value.code == -6
+        return
+    ref = [np.zeros(B, np.uint8) for _ in range(a)]
+    O.Clay(k, m, [e], is_test=True).perform_coding([x if x is None else x.copy() for x in inputs], ref, B)
+    step.performCoding(inputs, got, B)
+    assert all((got[z] == ref[z]).all() for z in range(a))
+    step.performCodingBatch(pool, n * a * B, B, out, a * B, B, 1, B)
+    torch.cuda.synchronize()
+    dev = out.cpu().numpy()
+    assert all((dev[z] == ref[z]).all() for z in range(a))
+
+
 def test_clay_multi_nonnull_erased_inputs(ecx):
     """doDecodeMulti with non-null buffers at erased slots (the reference reads them)."""
     k, m, erased, B = 4, 2, [0, 1], 100

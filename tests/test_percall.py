@@ -31,10 +31,26 @@ def default_host_exec_kib() -> int:
     return int(r.stdout.strip().splitlines()[-1])
 
 
-def test_default_threshold_below_the_reference_sub_chunk(ecx):
-    """The default host_exec_kib (8) keeps 32 KiB sub-chunk calls (the reference's
-    CLAY_BLOCK_SIZE) on the device path; the getter refuses shape keys."""
-    assert 0 < default_host_exec_kib() < 32
+def measured_crossover_bytes() -> int:
+    """The per-call crossover in the committed concurrency sweep (profiles/r06_percall_threshold
+    .jsonl, tests/native/percall_threshold.cpp --threads 1 / 16): the smallest size at which the
+    device path's aggregate rate beats the host executor's, over every site and thread count."""
+    rows = [json.loads(ln) for ln in (ROOT / "profiles" / "r06_percall_threshold.jsonl").read_text().splitlines()]
+    cross = [x["crossover_bytes"] for x in rows if "crossover_bytes" in x and x["crossover_bytes"] > 0]
+    sizes = [x for x in rows if "bytes" in x]
+    assert {x["threads"] for x in sizes} == {1, 16} and {x["case"] for x in sizes} == {"rs22_pair", "clay42"}
+    assert all(x["outputs_agree"] for x in sizes)
+    return min(cross) if cross else max(x["bytes"] for x in sizes) * 2
+
+
+def test_default_threshold_is_the_measured_crossover(ecx):
+    """the default host_exec_kib is the measured crossover -- the largest size
+    below the smallest one at which the device beats the host executor under the reference's
+    concurrency (1 and 16 caller threads: 2 MiB, Clay(4,2) at one thread), i.e. 1 MiB; the
+    reference's 32 KiB sub-chunk calls run on the calling thread.  The getter refuses shape keys."""
+    cross = measured_crossover_bytes()
+    assert cross == 2 << 20
+    assert default_host_exec_kib() * 1024 == cross // 2
     with pytest.raises(ecx.EcxError):
         ecx.tune_value("depth")
 
@@ -77,9 +93,26 @@ def test_percall_crossover_vs_oracle(ecx):
     for key in (("rs31_single", 34), ("rs22_pair", 2174)):  # round-4 verdict item 4's bar
         x = by[key]
         assert x["default_us"] <= 2 * x["oracle_us"] + 0.5, x
-    # the library's default threshold (a fresh process: this suite sets 0) sits below 32 KiB, so
-    # the reference's 32 KiB sub-chunk calls keep the device path
-    assert 0 < default_host_exec_kib() < 32
+    # the library's default threshold (a fresh process: this suite sets 0) is the measured crossover
+    assert default_host_exec_kib() * 1024 == measured_crossover_bytes() // 2
+
+
+@pytest.mark.gpu
+@pytest.mark.host_exec
+def test_percall_concurrent_callers_agree(ecx):
+    """The concurrent-caller mode of the threshold measurement (the full
+    1- and 16-thread sweep to 4 MiB is profiles/r06_percall_threshold.jsonl): 4 threads on the
+    RS(2,2) pair and Clay(4,2) performCoding sites up to 64 KiB, both paths byte-identical and
+    every call successful under concurrency."""
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    r = subprocess.run([str(EXE), "--threads", "4", "65536"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    sizes = [x for x in rows if "bytes" in x]
+    assert len(sizes) == 2 * 6 and {x["case"] for x in sizes} == {"rs22_pair", "clay42"}
+    for x in sizes:
+        assert x["outputs_agree"] and x["device_calls_per_s"] > 0 and x["host_exec_calls_per_s"] > 0, x
+    assert len([x for x in rows if "crossover_bytes" in x]) == 2
 
 
 @pytest.mark.gpu

@@ -524,3 +524,49 @@ def test_plane_group_kernel_wide_addresses_compile(ecx):
     finally:
         ecx.tune("rtc_wide", 0)
     assert step.rtcSource() == narrow
+
+
+@pytest.mark.parametrize("k,m,e", [(4, 2, 0), (4, 2, 1), (4, 2, 2), (4, 2, 3), (12, 4, 2), (12, 4, 5), (12, 4, 10),
+                                   (2, 2, 1)])
+def test_clay_is_test_branch_vs_oracle(ecx, k, m, e):
+    """decodeDecoupledPlane's -DisTest=true branch (ClayCodeErasureDecodingStep
+    .java:571-581; ecx_clay_create_ex ECX_CLAY_IS_TEST) -- decodeMissingSingle per helper, shard
+    i + |E| taken as the i-th present one (bug B2).  The planner's map equals the oracle's
+    restatement of that branch on random non-codeword inputs; for a repair whose erased row is
+    nodes 0..q-1 it equals the default branch (B2 does not bite), for the other rows it differs,
+    as the reference's does."""
+    import oracle as O
+    n = k + m
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, isTest=True)
+    a, q = step.subPacketSize, step.q
+    B = 8 if a >= 64 else 24
+    rng = np.random.default_rng(100 * k + e)
+    inputs = [None if (i % n) == e else rng.integers(0, 256, B, dtype=np.uint8) for i in range(n * a)]
+    ref = [np.zeros(B, np.uint8) for _ in range(a)]
+    O.Clay(k, m, [e], is_test=True).perform_coding([x if x is None else x.copy() for x in inputs], ref, B)
+    mat, ins, outs = step.map().matrix()
+    got = gf_apply_numpy(mat, [inputs[j] for j in ins])
+    assert all((got[o] == ref[o]).all() for o in range(a))
+    std = _oracle_perform(k, m, [e], inputs, B)
+    same = all((std[o] == ref[o]).all() for o in range(a))
+    assert same == (e // q == 0), (e, same)  # row y = 0 holds nodes 0..q-1
+    assert step.isTest and not ecx.ClayCodeErasureDecodingStep([e], k, m).isTest
+
+
+@pytest.mark.parametrize("k,m,e", [(4, 2, 4), (4, 2, 5), (12, 4, 13)])
+def test_clay_is_test_branch_parity_row_throws(ecx, k, m, e):
+    """The isTest branch on a repair whose erased row holds a parity node: decodeMissingSingle has
+    no matrix row for it and the reference throws NullPointerException (bug B3) -- the oracle's
+    restatement returns ORC_E_NULL, libecx's map build ECX_E_NULL (-6); the default branch repairs."""
+    import oracle as O
+    n = k + m
+    step = ecx.ClayCodeErasureDecodingStep([e], k, m, isTest=True)
+    with pytest.raises(ecx.EcxError) as ei:
+        step.map()
+    assert ei.value.code == -6
+    a = step.subPacketSize
+    inputs = [None if (i % n) == e else np.zeros(8, np.uint8) for i in range(n * a)]
+    with pytest.raises(Exception) as eo:
+        O.Clay(k, m, [e], is_test=True).perform_coding(inputs, [np.zeros(8, np.uint8) for _ in range(a)], 8)
+    assert "-6" in str(eo.value) or "Null" in str(eo.value)
+    assert ecx.ClayCodeErasureDecodingStep([e], k, m).map() is not None
