@@ -94,7 +94,9 @@ def test_percall_crossover_vs_oracle(ecx):
         x = by[key]
         assert x["default_us"] <= 2 * x["oracle_us"] + 0.5, x
     # the library's default threshold (a fresh process: this suite sets 0) is the measured crossover
-    assert default_host_exec_kib() * 1024 == measured_crossover_bytes() // 2
+    # (1 MiB; test_default_threshold_is_the_measured_crossover ties it to the committed profile,
+    # which does not travel to the GPU box)
+    assert default_host_exec_kib() == 1024
 
 
 @pytest.mark.gpu
