@@ -342,6 +342,22 @@ def kernel_source_hash(kernel: str = "") -> str:
     return h.hexdigest()[:16]
 
 
+def profile_key(args) -> str:
+    """The PMC profile a run's line reads (profiles/pmc_traffic.json): the workload, plus the
+    layout or sub-chunk size when the run is not the workload's default one (scripts/pmc.sh
+    profiles those variants under the same names, e.g. rs173_blocked, clay104_sub1048576)."""
+    key = args.workload
+    if getattr(args, "layout", "natural") == "blocked":
+        key += "_blocked"
+    if getattr(args, "pitch", None) is not None:
+        key += "_pitch%s" % args.pitch
+    if getattr(args, "pitch_pad", 0):
+        key += "_pad%d" % args.pitch_pad
+    if args.workload == "clay104" and getattr(args, "sub_bytes", None) and args.sub_bytes != Clay104.b:
+        key += "_sub%d" % args.sub_bytes
+    return key
+
+
 def pmc_traffic(workload: str, pool: int, kernel: str, shape: str = None):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (scripts/pmc.sh + scripts/pmc_summary.py), used only if it was taken on this
@@ -1356,7 +1372,7 @@ def main():
     total_stripes = stripes_per_step * args.steps * world
     metric_bytes = wl.metric_bytes or wl.unit_bytes
     value = total_stripes * metric_bytes / el / wl.metric_scale
-    traffic, traffic_note = pmc_traffic(args.workload, P, kernel, shape)
+    traffic, traffic_note = pmc_traffic(profile_key(args), P, kernel, shape)
 
     # per-rank rates, so an N-GPU efficiency shortfall can be attributed to a rank
     per_rank = [own_el]
@@ -1410,7 +1426,7 @@ def main():
 
     if rank == 0 and args.meta:
         Path(args.meta).write_text(json.dumps({
-            "workload": args.workload, "kernel": kernel, "launch_shape": shape, "tune": args.tune,
+            "workload": profile_key(args), "kernel": kernel, "launch_shape": shape, "tune": args.tune,
             "pool_stripes": P, "unit_bytes": wl.unit_bytes,
             "write_bytes_per_unit": wl.write_bytes, "algorithmic_bytes_per_launch": per_launch_bytes,
             "kernel_source_hash": kernel_source_hash(kernel), "avg_launch_ms": launch_ms}) + "\n")

@@ -31,11 +31,24 @@ CAND_TUNES=("layout_select=0" "block_threads=256 skew_chunks=0" "block_threads=2
             "block_threads=64 skew_chunks=0" "block_threads=64 skew_chunks=0 stagger=2"
             "block_threads=64 skew_chunks=0 stagger=8" "block_threads=256 skew_chunks=0 stagger=4")
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+# Variants of a workload (bench.py profile_key): <workload>_blocked (--layout blocked),
+# <workload>_pitch<P> (--pitch P, e.g. _pitchrecommended), clay104_sub<B> (--sub-bytes B).
+variant_args() {
+  local w=$1 base=${1%%_*} v=${1#*_}
+  [ "$w" = "$base" ] && { echo "--workload $w"; return; }
+  case $v in
+    blocked) echo "--workload $base --layout blocked" ;;
+    pitch*) echo "--workload $base --pitch ${v#pitch}" ;;
+    sub*) echo "--workload $base --sub-bytes ${v#sub}" ;;
+    *) echo "unknown variant $w" >&2; exit 2 ;;
+  esac
+}
 for W in $WORKLOADS; do
-  case $W in
+  case ${W%%_*} in
     clay42|clay42x2) POOL=32768 ;; clay104) POOL=2048 ;; rs124) POOL=512 ;; rs173|rs173check) POOL=4096 ;; lrcenc) POOL=32768 ;; lrc) POOL=32768 ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
+  [ "$W" = clay104_sub1048576 ] && POOL=16  # bench.py's pool for 1 MiB sub-chunks
   if [ $CANDIDATES = 1 ]; then NC=${#CAND_TUNES[@]}; else NC=1; fi
   for ((c = 0; c < NC; c++)); do
     TUNE=(); TAG=""
@@ -50,7 +63,7 @@ for W in $WORKLOADS; do
     for C in "${PASSES[@]}"; do
       D="$OUT/pmc_${W}${TAG}_$i"; mkdir -p "$D"
       timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
-          -- python3 "$ROOT/bench.py" --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 --e2e-seconds 0 \
+          -- python3 "$ROOT/bench.py" $(variant_args "$W") --steps 1 --warmup 0 --cpu-seconds 0 --e2e-seconds 0 \
              --stripes-per-step $((POOL * 16)) --no-probes --meta "$D/meta.json" "${TUNE[@]}" > "$D.log" 2>&1
       rc=$?; echo "pmc $W$TAG pass$i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D.log"; exit $rc; }
       i=$((i + 1))
