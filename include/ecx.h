@@ -11,11 +11,15 @@
  *   - Every function returns int: 0 (ECX_OK) or a non-negative result on
  *     success, a negative ECX_E_* code where the Java code throws.
  *     ecx_last_error() gives the thread-local message.
- *   - "Host" entry points take caller-owned host buffers (the Java byte[][]
- *     of the reference) and run the arithmetic on the current HIP device:
- *     the bytes are staged to HBM, one fused kernel applies the composed
- *     GF(256) map, and the results are copied back.  There is no CPU
- *     arithmetic fallback: without a usable device they return ECX_E_DEVICE.
+ *   - "Host" (per-call) entry points take caller-owned host buffers (the Java
+ *     byte[][] of the reference).  Above the per-call crossover (ecx_tune.h
+ *     "host_exec_kib", default 1 MiB per shard / sub-chunk, measured with 1 and
+ *     16 caller threads) the bytes are staged to HBM, one fused kernel applies
+ *     the composed GF(256) map and the results are copied back; at or below it
+ *     the calling thread applies the same map (AVX-512 GFNI / AVX2, host_exec.cpp),
+ *     which is faster than a PCIe round trip there.  That is a latency path of a
+ *     device-backed library, not a fallback: without a usable HIP device every
+ *     such call returns ECX_E_DEVICE, whatever its size.
  *   - "Batch" entry points take DEVICE pointers (HBM-resident stripes) and a
  *     hipStream_t passed as void*; they only enqueue work.  For the many-stream
  *     RS / LRC-encode maps on batches of >= 256 MiB of input, the first calls of a
