@@ -924,8 +924,6 @@ class RS173(_RsLayout, Workload):
         else:
             self.pitch = _resolve_pitch(self.rs, pitch, L)
             self.pool = torch.empty((P, 20, self.pitch), dtype=torch.uint8, device=dev)
-            if self.pitch != L:
-                self.host_ok = False  # the e2e leg runs the published (natural) shape only
         ecx.fill_random(self.pool, self.pool.numel(), seed)
         self.region = self.pool
         self.description = ("RS(17,3) encodeParity in place, 200,000-B shards, %s%s" %
@@ -945,7 +943,8 @@ class RS173(_RsLayout, Workload):
         return 0
 
     def host_call(self, hin, hout, n):
-        self.rs.encode_map().apply_batch_host(hin, 20 * self.L, self.L, hin, 20 * self.L, self.L, n, self.L)
+        p = self.pitch
+        self.rs.encode_map().apply_batch_host(hin, 20 * p, p, hin, 20 * p, p, n, self.L)
 
     def verify(self):
         """The parity the GPU wrote equals the oracle's on two stripes, and re-encoding
