@@ -1273,6 +1273,7 @@ def main():
         ecx.tune(key, int(val))
 
     P = args.pool
+    rss_stages = {"init": _peak_rss_bytes()}  # peak host RSS after each stage (the line's host_rss_MiB)
     passes = max(1, args.stripes_per_step // P)
     stripes_per_step = passes * P
     seed = 0x5EED + rank
@@ -1298,6 +1299,7 @@ def main():
     wl.launch()
     torch.cuda.synchronize()
     kernel = ecx.last_kernel()  # the instance launch_apply actually chose for this map and layout
+    rss_stages["pool"] = _peak_rss_bytes()
     verified = None
     if not args.no_verify:
         verified = wl.verify()
@@ -1334,6 +1336,7 @@ def main():
         kernel = ecx.last_kernel()  # after the layout selection: the instance the timed region runs
     shape = ecx.last_launch_shape()  # the kernel instance plus the unit order (stagger, XCD runs)
 
+    rss_stages["verify_warmup"] = _peak_rss_bytes()
     stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps * passes)]
@@ -1470,6 +1473,7 @@ def main():
                                "ranks": [round(v, 3) for v in per_rank_gibs]},
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "host_rss_MiB": {k: round(v / 2**20) for k, v in dict(rss_stages, end=_peak_rss_bytes()).items()},
             "verified": verified,
         }
         print(json.dumps(line), flush=True)
