@@ -593,3 +593,30 @@ def test_map_batch_host_buffer_via_jni_vs_oracle(J):
                 assert (out[base + slot * pitch:base + slot * pitch + L] == r).all()
     finally:
         J.call("mapDestroy", mp)
+
+
+def test_round6_entry_points_through_binding(J):
+    """Round 6's exports through their generated forwarders (CPU, no device work): the RS layout
+    contract's long[] outputs (rsBlockedLayout / rsRecommendedPitch, pinned and released, a short
+    array refused with ArrayIndexOutOfBounds before any pin), and clayCreateEx with the isTest
+    flag (its int[] erased list copied, not pinned) -- a distinct shared codec from clayCreate's."""
+    lay = np.zeros(3, np.int64)
+    assert J.call("rsBlockedLayout", 17, 3, 200000, J.array(lay)) == OK
+    assert lay.tolist() == [32768, 6, 200000 - 6 * 32768]
+    pitch = np.zeros(1, np.int64)
+    assert J.call("rsRecommendedPitch", 12, 4, 4 << 20, J.array(pitch)) == OK and pitch[0] == (4 << 20) + 4096
+    J.reset()
+    assert J.call("rsBlockedLayout", 17, 3, 200000, J.array(np.zeros(2, np.int64))) == IDX
+    assert J.call("rsBlockedLayout", 17, 3, 200000, None) == NUL
+    assert J.counters()["pins"] == 0
+    c = J.counters()
+    assert c["violations"] == 0 and c["pins_now"] == 0
+    test = handle(J, "clayCreateEx", 4, 2, 0, J.ints([2]), 1, 1)
+    std = handle(J, "clayCreate", 4, 2, J.ints([2]), 1)
+    try:
+        assert test != std
+        assert J.counters()["pins_now"] == 0
+        assert J.call("clayCreateEx", 4, 2, 0, J.ints([2]), 1, 2, J.array(np.zeros(1, np.int64))) == ILL  # unknown flag
+    finally:
+        J.call("clayDestroy", test)
+        J.call("clayDestroy", std)
