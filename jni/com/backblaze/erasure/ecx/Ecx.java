@@ -82,6 +82,31 @@ public final class Ecx {
         check(EcxNative.hostFree(EcxNative.directAddress(buffer)));
     }
 
+    /**
+     * The shard pitch to give a pool of RS(dataShards, parityShards) stripes kept as
+     * [stripe][shard][pitch] (ecx_rs_recommended_pitch, DESIGN.md section 4.6): the smallest odd
+     * multiple of 4 KiB at or above {@code byteCount}, e.g. to size an {@link #allocatePinned}
+     * pool as nstripes * (dataShards + parityShards) * pitch bytes.
+     */
+    public static long recommendedPitch(int dataShards, int parityShards, long byteCount) {
+        long[] p = new long[1];
+        check(EcxNative.rsRecommendedPitch(dataShards, parityShards, byteCount, p));
+        return p[0];
+    }
+
+    /**
+     * The engine's blocked layout for RS(dataShards, parityShards) stripes of byteCount-byte
+     * shards (ecx_rs_blocked_layout): {block bytes, full blocks per shard, tail bytes}.  A stripe's
+     * full blocks lie block-major, [block][shard][block bytes]; the tails of all stripes follow the
+     * full blocks of all stripes, [stripe][shard][tail].  rsEncodeParityBlockedBatch /
+     * rsDecodeMissingBlockedBatch run over device pools in that layout.
+     */
+    public static long[] blockedLayout(int dataShards, int parityShards, long byteCount) {
+        long[] layout = new long[3];
+        check(EcxNative.rsBlockedLayout(dataShards, parityShards, byteCount, layout));
+        return layout;
+    }
+
     /** Creates the codec handle of ReedSolomon.create(k, m) (ReedSolomon.java:34-61). */
     public static long createReedSolomon(int dataShards, int parityShards) {
         long[] h = new long[1];
