@@ -473,7 +473,10 @@ def e2e_rate(ecx, torch, wl, seconds: float, world: int = 1):
             return {"skipped": "one %d-B stripe exceeds this rank's host budget" % sb, "host_cap": cap}
     hin = ecx.HostBuffer(n * sb)
     hout = ecx.HostBuffer(n * ob) if ob else None
-    _copy_chunked(torch.from_numpy(hin.array), wl.pool[:n].reshape(-1))
+    at = 0
+    for region in wl.host_source(n):  # the first n stripes as they lie in HBM, in host order
+        _copy_chunked(torch.from_numpy(hin.array[at:at + region.numel()]), region)
+        at += region.numel()
     ha, ho = hin.array, (hout.array if hout else None)
     wl.host_call(ha, ho, n)  # warm-up: plans, pipe buffers
     ok = wl.host_expect(ha, ho if ho is not None else np.empty(0, np.uint8), n)
@@ -581,15 +584,24 @@ class Workload:
         E2E_COPY_CHUNK steps: no full-size host copy of the device side)."""
         import numpy as np
         if self.host_out_bytes() == 0:  # written in place: the whole host stripes equal the device pool's
-            got, want = hin[:n * self.host_stripe_bytes()], self.pool[:n].reshape(-1)
+            got, wants = hin[:n * self.host_stripe_bytes()], self.host_source(n)
         else:
-            got, want = hout[:n * self.host_out_bytes()], self.out[:n].reshape(-1)
-        if got.size != want.numel():
+            got, wants = hout[:n * self.host_out_bytes()], [self.out[:n].reshape(-1)]
+        if got.size != sum(w.numel() for w in wants):
             return False
-        for a in range(0, got.size, E2E_COPY_CHUNK):
-            if not np.array_equal(got[a:a + E2E_COPY_CHUNK], want[a:a + E2E_COPY_CHUNK].cpu().numpy()):
-                return False
+        at = 0
+        for want in wants:
+            for a in range(0, want.numel(), E2E_COPY_CHUNK):
+                b = min(a + E2E_COPY_CHUNK, want.numel())
+                if not np.array_equal(got[at + a:at + b], want[a:b].cpu().numpy()):
+                    return False
+            at += want.numel()
         return True
+
+    def host_source(self, n):
+        """The first n stripes of the resident pool as flat device regions, in the order the host
+        input buffer holds them (the end-to-end leg copies and checks them region by region)."""
+        return [self.pool[:n].reshape(-1)]
 
     def pcie_bytes(self):
         """(H2D, D2H) bytes per stripe: only the map's used input / output slots cross PCIe."""
@@ -817,6 +829,34 @@ class _RsLayout:
     def host_units(self, k):
         return [self.stripes(i, 1)[0].cpu().numpy() for i in range(min(k, self.P))]
 
+    def host_stripe_bytes(self):
+        return self.n * self.L if self.layout == "blocked" else self.pool[0].numel()
+
+    def host_source(self, n):
+        """Blocked: the full blocks of the first n stripes, then their tails (a blocked batch of
+        n stripes in host memory, ecx.h's layout)."""
+        if self.layout != "blocked":
+            return [self.pool[:n].reshape(-1)]
+        full, tail = divmod(self.L, self.block)
+        body = full * self.n * self.block
+        out = [self.pool[:n * body]] if full else []
+        if tail:
+            t0 = self.P * body
+            out.append(self.pool[t0:t0 + n * self.n * tail])
+        return out
+
+    def _blocked_host_call(self, gm, hin, n):
+        """The blocked layout from host memory: the map over the full blocks, then over the tails
+        (two pipelined host batches, ecx_map_apply_batch_host)."""
+        full, tail = divmod(self.L, self.block)
+        b, nn = self.block, self.n
+        body = n * full * nn * b
+        if full:
+            gm.apply_batch_host(hin[:body], nn * b, b, hin[:body], nn * b, b, n * full, b)
+        if tail:
+            t = hin[body:body + n * nn * tail]
+            gm.apply_batch_host(t, nn * tail, tail, t, nn * tail, tail, n, tail)
+
 
 class RS124(_RsLayout, Workload):
     """Config 5: RS(12,4), 4 MiB shards, erasures {0,1} decoded in place (the first 12
@@ -845,7 +885,6 @@ class RS124(_RsLayout, Workload):
             self.pool = ecx.blocked_pack(nat[:, :, :L], self.block)
             del nat
             self.pitch = self.block  # the slot pitch the decode's launches see
-            self.host_ok = False
         else:
             self.pool = nat
         self.region = self.pool
@@ -865,6 +904,9 @@ class RS124(_RsLayout, Workload):
         return 0
 
     def host_call(self, hin, hout, n):
+        if self.layout == "blocked":
+            self._blocked_host_call(self.dmap, hin, n)
+            return
         p = self.pitch
         self.dmap.apply_batch_host(hin, 16 * p, p, hin, 16 * p, p, n, self.L)
 
@@ -920,7 +962,6 @@ class RS173(_RsLayout, Workload):
             self.block = self.rs.blockedLayout(L)[0]
             self.pitch = self.block
             self.pool = torch.empty(P * 20 * L, dtype=torch.uint8, device=dev)
-            self.host_ok = False
         else:
             self.pitch = _resolve_pitch(self.rs, pitch, L)
             self.pool = torch.empty((P, 20, self.pitch), dtype=torch.uint8, device=dev)
@@ -943,6 +984,9 @@ class RS173(_RsLayout, Workload):
         return 0
 
     def host_call(self, hin, hout, n):
+        if self.layout == "blocked":
+            self._blocked_host_call(self.rs.encode_map(), hin, n)
+            return
         p = self.pitch
         self.rs.encode_map().apply_batch_host(hin, 20 * p, p, hin, 20 * p, p, n, self.L)
 

@@ -317,3 +317,28 @@ def test_clay104_sub_bytes_reading(monkeypatch):
     wl = _bare(bench.Clay104, erased=3, n=14, unit_bytes=1088 * b, b=b)
     cpu = bench.cpu_baseline(wl, 0.2, None, max_units=2)
     assert cpu["value"] > 0 and "alias 1 distinct" in cpu["sample"] and "65536-B sub-chunks" in cpu["sample"]
+
+
+def test_e2e_blocked_layout_host_batch_order(monkeypatch):
+    """The blocked RS layout's end-to-end leg: the host input of n stripes is the
+    full blocks of the first n pool stripes followed by their tails -- itself the blocked layout
+    of those n stripes (blocked_pack of their natural shards) -- and the leg verifies region by
+    region (CPU tensors and a numpy HostBuffer stand in for HBM and pinned memory)."""
+    import torch
+    import rpamd
+    ecx = rpamd.load()
+    monkeypatch.setattr(bench, "E2E_COPY_CHUNK", 777)
+    S, n, L, b = 7, 20, 1000, 256  # 3 full blocks + a 232-B tail per shard
+    nat = torch.randint(0, 256, (S, n, L), dtype=torch.uint8)
+    wl = _bare(bench.RS173, pool=ecx.blocked_pack(nat, b), L=L, P=S, n=n, layout="blocked", block=b, ecx=ecx)
+    k = 4
+    src = torch.cat(wl.host_source(k))
+    assert torch.equal(src, ecx.blocked_pack(nat[:k].contiguous(), b))
+    assert wl.host_stripe_bytes() == n * L
+    wl.host_call = lambda ha, ho, m: None  # the host map itself runs on the GPU box
+
+    class Ecx:
+        HostBuffer = _FakeHostBuffer
+    monkeypatch.setattr(bench, "E2E_HOST_BYTES", k * n * L)
+    r = bench.e2e_rate(Ecx, torch, wl, 0.01, world=1)
+    assert r["verified"] and r["stripes_per_call"] == k
