@@ -132,9 +132,12 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     const Tuning &t = tuning();
     const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes), rout = runs_of(outs, out_slot_stride, nbytes);
     // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a stripe's used
-    // slots fall into many runs (shortened Clay(10,4): 128 runs of 3-10 sub-chunks), so each strided
-    // copy moves whole rows of many stripes instead of a few KiB per call -- within 8x host_chunk.
-    constexpr int64_t kMinRows = 64;
+    // slots fall into many runs (shortened Clay(10,4): 128 runs of 3-10 sub-chunks; Clay(4,2) {0,3}:
+    // 16 runs of 2), so each strided copy moves whole rows of many stripes instead of a few KiB per
+    // call -- within 8x host_chunk.  The DMA queue idles ~16 us between copies (the copy trace,
+    // DESIGN.md 6); 160 rows beat 64, 96, 256 and 512 and equal-size chunks
+    // (profiles/r06_minrows_ab*.jsonl).
+    constexpr int64_t kMinRows = 160;
     int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
     if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
     chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
@@ -186,7 +189,7 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
     const int64_t in_per = (int64_t)ins.size() * nbytes;
     const Tuning &t = tuning();
     const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes);
-    constexpr int64_t kMinRows = 64;
+    constexpr int64_t kMinRows = 160;
     int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
     if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
     chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
