@@ -845,18 +845,6 @@ class _RsLayout:
             out.append(self.pool[t0:t0 + n * self.n * tail])
         return out
 
-    def _blocked_host_call(self, gm, hin, n):
-        """The blocked layout from host memory: the map over the full blocks, then over the tails
-        (two pipelined host batches, ecx_map_apply_batch_host)."""
-        full, tail = divmod(self.L, self.block)
-        b, nn = self.block, self.n
-        body = n * full * nn * b
-        if full:
-            gm.apply_batch_host(hin[:body], nn * b, b, hin[:body], nn * b, b, n * full, b)
-        if tail:
-            t = hin[body:body + n * nn * tail]
-            gm.apply_batch_host(t, nn * tail, tail, t, nn * tail, tail, n, tail)
-
 
 class RS124(_RsLayout, Workload):
     """Config 5: RS(12,4), 4 MiB shards, erasures {0,1} decoded in place (the first 12
@@ -905,7 +893,8 @@ class RS124(_RsLayout, Workload):
 
     def host_call(self, hin, hout, n):
         if self.layout == "blocked":
-            self._blocked_host_call(self.dmap, hin, n)
+            # the full blocks, then the tails: two pipelined host batches (ecx_rs_*_blocked_batch_host)
+            self.rs.decodeMissingBlockedBatchHost(hin, self.present, n, self.L, self.block)
             return
         p = self.pitch
         self.dmap.apply_batch_host(hin, 16 * p, p, hin, 16 * p, p, n, self.L)
@@ -985,7 +974,7 @@ class RS173(_RsLayout, Workload):
 
     def host_call(self, hin, hout, n):
         if self.layout == "blocked":
-            self._blocked_host_call(self.rs.encode_map(), hin, n)
+            self.rs.encodeParityBlockedBatchHost(hin, n, self.L, self.block)
             return
         p = self.pitch
         self.rs.encode_map().apply_batch_host(hin, 20 * p, p, hin, 20 * p, p, n, self.L)

@@ -190,6 +190,17 @@ int ecx_rs_encode_parity_blocked_batch(ecx_rs *rs, uint8_t *base, int64_t nstrip
 int ecx_rs_decode_missing_blocked_batch(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base, int64_t nstripes,
                                         int64_t byte_count, int64_t block_bytes, void *stream);
 
+/* The same two blocked batches (encodeParity / decodeMissing, ReedSolomon.java:94-108, :189-286)
+ * from HOST memory, in place (base: nstripes * n * byte_count bytes of
+ * pageable or pinned host memory in the blocked layout): the full blocks, then the tails, each a
+ * pipelined host batch (H2D -> map -> D2H of the written shards only, as ecx_map_apply_batch_host).
+ * Synchronous; a caller that keeps its stripes blocked on the host feeds the device the layout
+ * the kernels run fastest on without an unpacking pass. */
+int ecx_rs_encode_parity_blocked_batch_host(ecx_rs *rs, uint8_t *base, int64_t nstripes, int64_t byte_count,
+                                            int64_t block_bytes);
+int ecx_rs_decode_missing_blocked_batch_host(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base,
+                                             int64_t nstripes, int64_t byte_count, int64_t block_bytes);
+
 /* As ecx_map_apply_batch, but XOR-accumulates: out ^= M * in. */
 int ecx_map_accumulate_batch(const ecx_map *map, const uint8_t *in, int64_t in_stripe_stride,
                              int64_t in_slot_stride, uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride,

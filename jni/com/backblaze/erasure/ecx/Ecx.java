@@ -99,7 +99,8 @@ public final class Ecx {
      * shards (ecx_rs_blocked_layout): {block bytes, full blocks per shard, tail bytes}.  A stripe's
      * full blocks lie block-major, [block][shard][block bytes]; the tails of all stripes follow the
      * full blocks of all stripes, [stripe][shard][tail].  rsEncodeParityBlockedBatch /
-     * rsDecodeMissingBlockedBatch run over device pools in that layout.
+     * rsDecodeMissingBlockedBatch run over device pools in that layout,
+     * {@link EcxBlockedStripes} over direct host buffers in it.
      */
     public static long[] blockedLayout(int dataShards, int parityShards, long byteCount) {
         long[] layout = new long[3];

@@ -158,6 +158,7 @@ RULES = {
     "ecx_map_apply_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
     "ecx_clay_perform_coding_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
     "ecx_rs_is_parity_correct_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
+    "ecx_rs_decode_missing_blocked_batch_host": (("rs",), [A("shard_present", RS_N)]),
 }
 
 
@@ -182,9 +183,19 @@ BUFFER_VARIANTS["ecx_rs_is_parity_correct_batch_host"] = ("rs", "    max_in = rs
 BUFFER_VARIANTS["ecx_map_apply_batch_host_devices"] = BUFFER_VARIANTS["ecx_map_apply_batch_host"]
 BUFFER_VARIANTS["ecx_clay_perform_coding_batch_host_devices"] = BUFFER_VARIANTS["ecx_clay_perform_coding_batch_host"]
 BUFFER_VARIANTS["ecx_rs_is_parity_correct_batch_host_devices"] = BUFFER_VARIANTS["ecx_rs_is_parity_correct_batch_host"]
-# buffers laid out other than (stripe stride, slot stride) after the address: param -> (stripe
-# stride, slot stride, max slot, bytes per slot), as C expressions
-BUFFER_SHAPES = {"verdict": ("1", "0", "0", "1")}
+# The blocked RS batches from host memory: one buffer of nstripes whole stripes (n * byte_count
+# bytes each, the body and the tails together), the stripe size overflow-checked first.
+BLOCKED_EXTENT = ("    int64_t stripe_bytes = 0;\n"
+                  "    if (st == ECX_OK && __builtin_mul_overflow((int64_t)rs_k + rs_m, byte_count, &stripe_bytes))\n"
+                  "        st = ECX_E_ILLEGAL_ARGUMENT;\n"
+                  "    max_in = 0;")
+BUFFER_VARIANTS["ecx_rs_encode_parity_blocked_batch_host"] = ("rs", BLOCKED_EXTENT, None)
+BUFFER_VARIANTS["ecx_rs_decode_missing_blocked_batch_host"] = ("rs", BLOCKED_EXTENT, None)
+# buffers laid out other than (stripe stride, slot stride) after the address: param (or (export,
+# param)) -> (stripe stride, slot stride, max slot, bytes per slot), as C expressions
+BUFFER_SHAPES = {"verdict": ("1", "0", "0", "1"),
+                 ("ecx_rs_encode_parity_blocked_batch_host", "base"): ("stripe_bytes", "0", "0", "stripe_bytes"),
+                 ("ecx_rs_decode_missing_blocked_batch_host", "base"): ("stripe_bytes", "0", "0", "stripe_bytes")}
 
 
 def host_address_native(name):
@@ -192,6 +203,14 @@ def host_address_native(name):
     package-private, so Java callers outside com.backblaze.erasure.ecx reach them only
     through the capacity-checked <camel>Buffer forwarders (ClayCoordinator.kt:378-390)."""
     return "_batch_host" in name
+
+
+def copied(name, kind, ctype):
+    """A read-only array argument the forwarder copies instead of pinning: every const int[], and
+    the const byte[] flags of a host batch (which runs for as long as its PCIe transfers)."""
+    if not ctype.startswith("const"):
+        return False
+    return kind == "ints" or (kind == "bytes" and host_address_native(name))
 
 
 def buffer_variant(ret, name, params):
@@ -204,7 +223,7 @@ def buffer_variant(ret, name, params):
     if "offset" in names:  # a window [offset, offset + byte_count) of every slot
         negative += " || offset < 0"
         length = "(int64_t)offset + %s" % length
-    jparams, cparams, args, bufs, ints = [], ["JNIEnv *env", "jclass cls"], [], [], []
+    jparams, cparams, args, bufs, ints, flags = [], ["JNIEnv *env", "jclass cls"], [], [], [], []
     for i, (t, p) in enumerate(params):
         kind = classify(name, t, p)[0]
         if kind == "int":
@@ -216,10 +235,17 @@ def buffer_variant(ret, name, params):
             cparams.append("jintArray %s" % p)
             ints.append((p, names[i + 1]))
             args.append("%s_c" % p)
+        elif kind == "bytes":  # a *_present flag array: copied out (no critical region), length-checked
+            jparams.append("byte[] %s" % camel("ecx_" + p))
+            cparams.append("jbyteArray %s" % p)
+            flags.append((p, dict((r[1], r[2]) for r in RULES[name][1] if r[0] == "array")[p]))
+            args.append("%s_c" % p)
         elif kind == "addr":
             jparams.append("ByteBuffer %s" % camel("ecx_" + p))
             cparams.append("jobject %s" % p)
-            if p in BUFFER_SHAPES:
+            if (name, p) in BUFFER_SHAPES:
+                bufs.append((p,) + BUFFER_SHAPES[(name, p)])
+            elif p in BUFFER_SHAPES:
                 bufs.append((p,) + BUFFER_SHAPES[p])
             else:  # (stripe stride, slot stride) follow; the map's slots; the batch's bytes per slot
                 bufs.append((p, names[i + 1], names[i + 2], "max_in" if p in ("in", "base") else "max_out", length))
@@ -248,8 +274,15 @@ def buffer_variant(ret, name, params):
         body.append("    if (st == ECX_OK && !(%s_c = (int *)malloc(sizeof(int) * ((size_t)%s + 1)))) st = ECX_E_NOMEM;"
                     % (p, cnt))
         body.append("    if (st == ECX_OK) (*env)->GetIntArrayRegion(env, %s, 0, %s, (jint *)%s_c);" % (p, cnt, p))
+    for p, need in flags:
+        body.append("    uint8_t *%s_c = NULL;" % p)
+        body.append("    if (st == ECX_OK) st = array_check(env, %s, %s, 0, ECX_E_INDEX);" % (p, need))
+        body.append("    if (st == ECX_OK && !(%s_c = (uint8_t *)malloc((size_t)(%s) + 1))) st = ECX_E_NOMEM;"
+                    % (p, need))
+        body.append("    if (st == ECX_OK) (*env)->GetByteArrayRegion(env, %s, 0, (jsize)(%s), (jbyte *)%s_c);"
+                    % (p, need, p))
     body.append("    if (st == ECX_OK) st = %s(%s);" % (name, ", ".join(args)))
-    for p, _ in ints:
+    for p, _ in ints + flags:
         body.append("    free(%s_c);" % p)
     body.append("    return st;")
     jname = camel(name) + "Buffer"
@@ -547,16 +580,19 @@ public final class EcxNative {
                 args.append("&%s_h" % p)
                 post.append("    if (st >= 0 && %s) { jlong v = (jlong)(intptr_t)%s_h; (*env)->SetLongArrayRegion(env, %s, 0, 1, &v); }"
                             % (p, p, p))
-            elif kind == "ints" and t.startswith("const"):
-                # read-only int[] (device lists, slots, erased indices): copied out of the Java
-                # array before any critical region opens, never pinned, so a long export (a
-                # multi-GPU host batch) holds no GC-blocking pin ("pinning")
+            elif copied(name, kind, t):
+                # read-only int[] (device lists, slots, erased indices) and the flag byte[] of a
+                # host batch: copied out of the Java array before any critical region opens, never
+                # pinned, so a long export (a host batch) holds no GC-blocking pin
+                # ("pinning")
                 need = next(r[2] for r in rules if r[0] == "array" and r[1] == p)
-                pre.append("    int *%s_p = NULL;" % p)
-                copies.append("    if (st == ECX_OK && %s && !(%s_p = (int *)malloc(sizeof(int) * ((size_t)(%s) + 1))))"
-                              " st = ECX_E_NOMEM;" % (p, p, need))
-                copies.append("    if (st == ECX_OK && %s) (*env)->GetIntArrayRegion(env, %s, 0, (jsize)(%s), (jint *)%s_p);"
-                              % (p, p, need, p))
+                cty, jty, get = (("int", "jint", "GetIntArrayRegion") if kind == "ints" else
+                                 ("uint8_t", "jbyte", "GetByteArrayRegion"))
+                pre.append("    %s *%s_p = NULL;" % (cty, p))
+                copies.append("    if (st == ECX_OK && %s && !(%s_p = (%s *)malloc(sizeof(%s) * ((size_t)(%s) + 1))))"
+                              " st = ECX_E_NOMEM;" % (p, p, cty, cty, need))
+                copies.append("    if (st == ECX_OK && %s) (*env)->%s(env, %s, 0, (jsize)(%s), (%s *)%s_p);"
+                              % (p, get, p, need, jty, p))
                 post.append("    free(%s_p);" % p)
                 args.append("%s_p" % p)
             elif kind in ("bytes", "ints", "shorts", "longs"):
@@ -596,7 +632,7 @@ public final class EcxNative {
             if pinned:
                 # every PIN that returned NULL for a non-null array is an allocation failure
                 checks = ["(%s && !%s_p)" % (p, p) for (kind, _, _), t, p in kinds
-                          if kind in ("bytes", "ints", "shorts", "longs") and not (kind == "ints" and t.startswith("const"))]
+                          if kind in ("bytes", "ints", "shorts", "longs") and not copied(name, kind, t)]
                 if checks:
                     body.append("    if (st == ECX_OK && (%s)) st = ECX_E_NOMEM;" % " || ".join(checks))
             body.append("    if (st == ECX_OK) st = %s;" % call)

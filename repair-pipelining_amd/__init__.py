@@ -671,6 +671,24 @@ class ReedSolomon:
         check(lib().ecx_rs_decode_missing_blocked_batch(self._h, pres.ctypes.data, _dev_ptr(base), nstripes,
                                                         byteCount, blockBytes, _stream(stream)))
 
+    def encodeParityBlockedBatchHost(self, base, nstripes, byteCount, blockBytes=0):
+        """encodeParityBlockedBatch over HOST-memory stripes in the blocked layout, in place
+        (ecx_rs_encode_parity_blocked_batch_host: the full blocks, then the tails, each a
+        pipelined host batch)."""
+        _check_extent(base, nstripes * self.getTotalShardCount() * byteCount, "base")
+        check(lib().ecx_rs_encode_parity_blocked_batch_host(self._h, _host_ptr(base), nstripes, byteCount,
+                                                            blockBytes))
+
+    def decodeMissingBlockedBatchHost(self, base, shardPresent, nstripes, byteCount, blockBytes=0):
+        """decodeMissingBlockedBatch over HOST-memory stripes, in place
+        (ecx_rs_decode_missing_blocked_batch_host)."""
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        if len(pres) != self.getTotalShardCount():
+            raise EcxError(-1, "wrong number of shardPresent flags")
+        _check_extent(base, nstripes * self.getTotalShardCount() * byteCount, "base")
+        check(lib().ecx_rs_decode_missing_blocked_batch_host(self._h, pres.ctypes.data, _host_ptr(base), nstripes,
+                                                             byteCount, blockBytes))
+
     def isParityCorrectBatch(self, shards, stripe_stride, shard_stride, nstripes, firstByte, byteCount, verdict,
                              stream=None) -> None:
         """isParityCorrect over nstripes device-resident stripes, read-only

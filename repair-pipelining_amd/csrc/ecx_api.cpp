@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
+#include <functional>
 #include <list>
 #include <map>
 #include <memory>
@@ -583,21 +584,35 @@ int64_t resolve_block(int n, int64_t byte_count, int64_t block_bytes) {
     return block_bytes == 0 ? recommended_block(n, byte_count) : block_bytes;
 }
 
-// The map over a blocked batch (ecx.h): the full blocks as nstripes * full "stripes" of n
-// block-sized slots, then the tails as nstripes stripes of n tail-sized slots.
-void launch_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block,
-                    hipStream_t stream) {
+// The two passes of a blocked batch (ecx.h), each in place: the full blocks as nstripes * full
+// "stripes" of n block-sized slots, then the tails as nstripes stripes of n tail-sized slots.
+// pass(offset, stripe_stride, slot_bytes, units) runs the map over one of them.
+// (a std::function: this file's helpers sit inside the extern "C" block, where templates cannot)
+void blocked_passes(int n, int64_t nstripes, int64_t byte_count, int64_t block,
+                    const std::function<void(int64_t, int64_t, int64_t, int64_t)> &pass) {
     if (nstripes == 0 || byte_count == 0) return;
     const int64_t full = byte_count / block, tail = byte_count % block;
     int64_t stride = 0, units = 0, body = 0;
     if (__builtin_mul_overflow((int64_t)n, block, &stride) || __builtin_mul_overflow(nstripes, full, &units) ||
         __builtin_mul_overflow(units, stride, &body))
         throw Error(ECX_E_ILLEGAL_ARGUMENT, "blocked batch extent overflows");
-    if (full > 0) launch_apply(cm, base, stride, block, base, stride, block, units, block, stream);
-    if (tail > 0) {
-        uint8_t *t = base + body;
-        launch_apply(cm, t, (int64_t)n * tail, tail, t, (int64_t)n * tail, tail, nstripes, tail, stream);
-    }
+    if (full > 0) pass((int64_t)0, stride, block, units);
+    if (tail > 0) pass(body, (int64_t)n * tail, tail, nstripes);
+}
+
+void launch_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block,
+                    hipStream_t stream) {
+    blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
+        launch_apply(cm, base + off, ss, len, base + off, ss, len, units, len, stream);
+    });
+}
+
+// The same two passes from host memory: two pipelined host batches (host_pipe.cpp), the second
+// after the first has drained (each is synchronous).
+void host_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block) {
+    blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
+        run_host_batch(cm, base + off, ss, len, base + off, ss, len, units, len);
+    });
 }
 }  // namespace
 
@@ -651,6 +666,37 @@ int ecx_rs_decode_missing_blocked_batch(ecx_rs *rs, const uint8_t *shard_present
         if (m->cm.map().n_out == 0) return ECX_OK;  // all present (ReedSolomon.java:216-218)
         launch_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block,
                        (hipStream_t)stream);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_encode_parity_blocked_batch_host(ecx_rs *rs, uint8_t *base, int64_t nstripes, int64_t byte_count,
+                                            int64_t block_bytes) {
+    return guarded(__func__, [&]() -> int {
+        if (!rs) throw Error(ECX_E_NULL, "null codec");
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (nstripes > 0 && !base) throw Error(ECX_E_NULL, "null host pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_encode_map(rs, &m);
+        if (st) return st;
+        const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
+        host_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_decode_missing_blocked_batch_host(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base,
+                                             int64_t nstripes, int64_t byte_count, int64_t block_bytes) {
+    return guarded(__func__, [&]() -> int {
+        if (!rs) throw Error(ECX_E_NULL, "null codec");
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (nstripes > 0 && !base) throw Error(ECX_E_NULL, "null host pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_decode_map(rs, shard_present, &m);  // Not enough shards -> -2
+        if (st) return st;
+        const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
+        if (m->cm.map().n_out == 0) return ECX_OK;  // all present (ReedSolomon.java:216-218)
+        host_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block);
         return ECX_OK;
     });
 }

@@ -64,6 +64,16 @@ static void f_GetIntArrayRegion(JNIEnv *env, jintArray a, jsize start, jsize len
     memcpy(buf, (jint *)a->data + start, (size_t)len * 4);
 }
 
+static void f_GetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize start, jsize len, jbyte *buf) {
+    (void)env;
+    jni_call();
+    if (!a || a->kind != 1 || a->elem_size != 1 || start < 0 || len < 0 || start + len > a->len) {
+        ++g_violations;
+        return;
+    }
+    memcpy(buf, (jbyte *)a->data + start, (size_t)len);
+}
+
 static void f_SetLongArrayRegion(JNIEnv *env, jlongArray a, jsize start, jsize len, const jlong *buf) {
     (void)env;
     jni_call();
@@ -137,7 +147,8 @@ static jobject f_NewDirectByteBuffer(JNIEnv *env, void *address, jlong capacity)
 }
 
 static const struct JNINativeInterface_ g_table = {
-    f_GetArrayLength,          f_GetObjectArrayElement, f_GetIntArrayRegion,    f_SetLongArrayRegion,
+    f_GetArrayLength,          f_GetObjectArrayElement, f_GetIntArrayRegion,    f_GetByteArrayRegion,
+    f_SetLongArrayRegion,
     f_GetPrimitiveArrayCritical, f_ReleasePrimitiveArrayCritical, f_DeleteLocalRef, f_NewStringUTF,
     f_GetDirectBufferAddress,  f_NewDirectByteBuffer,    f_GetDirectBufferCapacity,
 };

@@ -35,6 +35,7 @@ struct JNINativeInterface_ {
     jsize (*GetArrayLength)(JNIEnv *env, jarray array);
     jobject (*GetObjectArrayElement)(JNIEnv *env, jobjectArray array, jsize index);
     void (*GetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len, jint *buf);
+    void (*GetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, jbyte *buf);
     void (*SetLongArrayRegion)(JNIEnv *env, jlongArray array, jsize start, jsize len, const jlong *buf);
     void *(*GetPrimitiveArrayCritical)(JNIEnv *env, jarray array, jboolean *isCopy);
     void (*ReleasePrimitiveArrayCritical)(JNIEnv *env, jarray array, void *carray, jint mode);

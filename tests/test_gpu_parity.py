@@ -1215,6 +1215,55 @@ def test_rs_blocked_batches_vs_oracle(ecx, torch_dev, k, m, L, block):
         assert all((got[s, i] == ref[i]).all() for i in range(n)), (s, present)
 
 
+@pytest.mark.parametrize("k,m,L,block,pinned,small", [(17, 3, 200000, 0, True, False), (17, 3, 200000, 0, False, True),
+                                                      (12, 4, 3 * 65536, 0, True, True), (4, 2, 104449, 4096, False, False),
+                                                      (5, 5, 1001, 64, True, True), (3, 1, 34, 0, False, False)])
+def test_rs_blocked_batches_host_vs_oracle(ecx, torch_dev, k, m, L, block, pinned, small):
+    """The blocked batches from HOST memory (ecx_rs_encode_parity_blocked_batch_host /
+    ecx_rs_decode_missing_blocked_batch_host: the full blocks, then the tails, each a pipelined host
+    batch), pageable and pinned, with the default chunks and with one stripe per chunk (ring reuse):
+    every stripe equals the oracle's encodeParity / decodeMissing on its natural shards, the
+    present shards of a decode are left as they were, and nothing past the batch is written."""
+    torch = torch_dev
+    n, S = k + m, 6
+    rs = ecx.ReedSolomon.create(k, m)
+    b = block or rs.blockedLayout(L)[0]
+    rng = np.random.default_rng(1300 + k + L)
+    nat = rng.integers(0, 256, (S, n, L), dtype=np.uint8)
+    total = S * n * L
+    if small:
+        ecx.tune("host_chunk_kib", 16)
+    try:
+        for op in ("encode", "decode"):
+            packed = ecx.blocked_pack(torch.from_numpy(nat), b).numpy()
+            if pinned:
+                hb = ecx.HostBuffer(total + 64)
+                buf = hb.array
+            else:
+                buf = np.empty(total + 64, np.uint8)
+            buf[:total] = packed
+            buf[total:] = 0xE7
+            present = [True] * n
+            if op == "encode":
+                rs.encodeParityBlockedBatchHost(buf, S, L, block)
+            else:
+                for i in (0, n - 1)[:m]:
+                    present[i] = False
+                rs.decodeMissingBlockedBatchHost(buf, present, S, L, block)
+            assert (buf[total:] == 0xE7).all()
+            got = ecx.blocked_unpack(torch.from_numpy(buf[:total].copy()), S, n, L, b).numpy()
+            for s in range(S):
+                ref = [nat[s, i].copy() for i in range(n)]
+                if op == "encode":
+                    O.ReedSolomon(k, m).encode_parity(ref, 0, L)
+                else:
+                    O.ReedSolomon(k, m).decode_missing(ref, present, 0, L)
+                assert all((got[s, i] == ref[i]).all() for i in range(n)), (op, s)
+                assert all((got[s, i] == nat[s, i]).all() for i in range(n) if present[i] and (op == "decode" or i < k))
+    finally:
+        ecx.tune("host_chunk_kib", 65536)
+
+
 @pytest.mark.parametrize("k,m", [(4, 2), (12, 4), (3, 1)])
 def test_rs_batch_codec_entry_points(ecx, torch_dev, k, m):
     """ecx_rs_encode_parity_batch / ecx_rs_decode_missing_batch: encodeParity and

@@ -363,6 +363,66 @@ def test_rs_check_batch_host_buffer_checks(J):
         J.call("rsDestroy", rs)
 
 
+def _np_blocked(nat, block):
+    """[S][n][L] -> the blocked layout (include/ecx.h): body [S][full][n][block], tails [S][n][tail]."""
+    S, n, L = nat.shape
+    full, tail = divmod(L, block)
+    body = nat[:, :, :full * block].reshape(S, n, full, block).transpose(0, 2, 1, 3).reshape(-1)
+    return np.concatenate([body, nat[:, :, full * block:].reshape(-1)])
+
+
+def test_rs_blocked_batch_host_buffer_checks(J):
+    """rsEncodeParityBlockedBatchHostBuffer / rsDecodeMissingBlockedBatchHostBuffer (round 6): the
+    ByteBuffer must hold nstripes whole stripes (n * byteCount bytes each, blocks and tails), the
+    shardPresent flags n bytes (copied, never pinned); short, heap or null buffers, short flags and
+    an overflowing stripe size are refused before anything is touched; on the GPU the blocked
+    stripes come back equal to the oracle's encodeParity / decodeMissing."""
+    k, m, S, L, blk = 5, 3, 3, 1000, 256
+    n = k + m
+    rs = handle(J, "rsCreate", k, m)
+    try:
+        nat = np.random.default_rng(61).integers(0, 256, (S, n, L), dtype=np.uint8)
+        buf = _np_blocked(nat, blk)
+        need = S * n * L
+        pres = np.ones(n, np.uint8)
+        pres[[0, 6]] = 0
+        J.reset()
+        enc = lambda b, **kw: J.call("rsEncodeParityBlockedBatchHostBuffer", rs, b, kw.get("S", S), kw.get("L", L),  # noqa: E731
+                                     blk)
+        dec = lambda p, b, **kw: J.call("rsDecodeMissingBlockedBatchHostBuffer", rs, p, b, kw.get("S", S),  # noqa: E731
+                                        kw.get("L", L), blk)
+        before = buf.copy()
+        assert enc(J.direct(buf, need - 1)) == IDX and dec(J.array(pres), J.direct(buf, need - 1)) == IDX
+        assert enc(J.direct(buf), S=S + 1) == IDX                          # one stripe too many
+        assert enc(J.direct(buf), L=1 << 62) == ILL                        # n * byteCount overflows
+        assert enc(J.direct(buf), S=-1) == ILL and enc(J.direct(buf), L=-1) == ILL
+        assert enc(J.array(buf)) == NUL and enc(None) == NUL               # heap / null buffer
+        assert dec(J.array(pres[:n - 1]), J.direct(buf)) == IDX            # flags one short
+        assert dec(None, J.direct(buf)) == NUL
+        assert J.call("rsEncodeParityBlockedBatchHostBuffer", 0, J.direct(buf), S, L, blk) == NUL
+        assert J.counters()["pins"] == 0 and (buf == before).all()
+        st = enc(J.direct(buf))
+        assert st == (OK if has_device(J) else DEV), st
+        if st == OK:
+            assert (buf == _np_blocked(_oracle_rs(k, m, nat, "encode"), blk)).all()
+            buf[:] = _np_blocked(nat, blk)
+            assert dec(J.array(pres), J.direct(buf)) == OK
+            assert (buf == _np_blocked(_oracle_rs(k, m, nat, "decode", pres), blk)).all()
+    finally:
+        J.call("rsDestroy", rs)
+
+
+def _oracle_rs(k, m, nat, op, pres=None):
+    out = nat.copy()
+    for s in range(nat.shape[0]):
+        shards = [out[s, i] for i in range(k + m)]  # views: the oracle writes in place
+        if op == "encode":
+            O.ReedSolomon(k, m).encode_parity(shards, 0, nat.shape[2])
+        else:
+            O.ReedSolomon(k, m).decode_missing(shards, [bool(x) for x in pres], 0, nat.shape[2])
+    return out
+
+
 def test_codec_reference_survives_other_releases(J):
     """The registry side of ADVICE r04 (EcxPartialSums / EcxClayCodeErasureDecodingStep close):
     two handles of one (k, m) codec are one shared object; releasing one and then more than
@@ -385,6 +445,7 @@ def test_codec_reference_survives_other_releases(J):
     root = Path(__file__).resolve().parents[1] / "jni"
     for f, field in (("com/backblaze/erasure/ecx/EcxPartialSums.java", "rs"),
                      ("com/backblaze/erasure/ecx/EcxParityCheck.java", "rs"),
+                     ("com/backblaze/erasure/ecx/EcxBlockedStripes.java", "rs"),
                      ("distributed/erasure/coding/clay/EcxClayCodeErasureDecodingStep.java", "clay")):
         src = (root / f).read_text()
         close = src[src.index("public synchronized void close()"):]
