@@ -24,6 +24,7 @@
 namespace ecx {
 namespace {
 
+
 struct Run {
     int slot0;     // first host slot
     int compact0;  // first compact (device) slot
@@ -40,6 +41,37 @@ std::vector<Run> runs_of(const std::vector<int> &slots, int64_t slot_stride, int
         runs.push_back({slots[i], (int)i, 1});
     }
     return runs;
+}
+
+// The runs of a stripe often repeat with a fixed step: a Clay repair reads the same helper nodes
+// of every plane (Clay(4,2) {0,3}: nodes 1-2 and 4-5 of all 8 planes, 16 runs), a check on a
+// padded pitch reads every shard.  When runs[i + period] is runs[i] moved by a fixed number of
+// host slots and of compact slots for every i, and `count` such steps span exactly one stripe on
+// both sides, the k-th run of every period in every stripe of a chunk lies at a fixed pitch: one
+// strided copy of count x stripes rows per run of the first period moves them all (Clay(4,2)
+// {0,3}: 1 copy per chunk instead of 16, e2e 71.6 -> 75.9 GiB/s, profiles/r06_fold_ab.jsonl).
+struct Fold {
+    size_t period;        // runs copied per chunk
+    int64_t count;        // rows per stripe of each of those copies
+    int64_t host_pitch;   // bytes between the rows on the host side
+    int64_t dev_pitch;    // ... and in the compact device buffer
+};
+
+Fold fold_runs(const std::vector<Run> &runs, int64_t stripe_stride, int64_t slot_stride, int64_t per,
+               int64_t nbytes) {
+    const size_t n = runs.size();
+    for (size_t p = 1; p < n; ++p) {
+        if (n % p) continue;
+        const int64_t ds = runs[p].slot0 - runs[0].slot0, dc = runs[p].compact0 - runs[0].compact0;
+        const int64_t count = (int64_t)(n / p);
+        if (ds <= 0 || dc <= 0 || count * ds * slot_stride != stripe_stride || count * dc * nbytes != per) continue;
+        bool ok = true;
+        for (size_t i = 0; ok && i + p < n; ++i)
+            ok = runs[i + p].len == runs[i].len && runs[i + p].slot0 - runs[i].slot0 == ds &&
+                 runs[i + p].compact0 - runs[i].compact0 == dc;
+        if (ok) return {p, count, ds * slot_stride, dc * nbytes};
+    }
+    return {n, 1, stripe_stride, per};
 }
 
 // Copy `rows` rows of `width` bytes between two pitched layouts.
@@ -132,8 +164,8 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     const Tuning &t = tuning();
     const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes), rout = runs_of(outs, out_slot_stride, nbytes);
     // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a stripe's used
-    // slots fall into many runs (shortened Clay(10,4): 128 runs of 3-10 sub-chunks; Clay(4,2) {0,3}:
-    // 16 runs of 2), so each strided copy moves whole rows of many stripes instead of a few KiB per
+    // slots fall into many runs (shortened Clay(10,4), node 3: 65 runs of 3-13 sub-chunks; Clay(4,2)
+    // {0,3}: 16 runs of 2), so each strided copy moves whole rows of many stripes instead of a few KiB per
     // call -- within 8x host_chunk.  The DMA queue idles ~16 us between copies (the copy trace,
     // DESIGN.md 6); 160 rows beat 64, 96, 256 and 512 and equal-size chunks
     // (profiles/r06_minrows_ab*.jsonl).
@@ -143,6 +175,8 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
     const int64_t nchunks = (nstripes + chunk - 1) / chunk;
     const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
+    const Fold fin = fold_runs(rin, in_stripe_stride, in_slot_stride, in_per, nbytes),
+               fout = fold_runs(rout, out_stripe_stride, out_slot_stride, out_per, nbytes);
 
     HostPipe &p = HostPipe::current();
     std::lock_guard<std::mutex> lk(p.mu);
@@ -152,18 +186,23 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
             HostPipe::Set &b = p.sets[(size_t)(i % nb)];
             const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
             if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
-            for (const Run &r : rin)
-                copy_rows(b.in + r.compact0 * nbytes, in_per, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
-                          in_stripe_stride, r.len * nbytes, n, hipMemcpyHostToDevice, p.h2d);
+            for (size_t j = 0; j < fin.period; ++j) {
+                const Run &r = rin[j];
+                copy_rows(b.in + r.compact0 * nbytes, fin.dev_pitch, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
+                          fin.host_pitch, r.len * nbytes, n * fin.count, hipMemcpyHostToDevice, p.h2d);
+            }
             check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
             if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");
             launch_apply(cc, b.in, in_per, nbytes, b.out, out_per, nbytes, n, nbytes, p.cmp);
             check_hip(hipEventRecord(b.computed, p.cmp), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.d2h, b.computed, 0), "hipStreamWaitEvent");
-            for (const Run &r : rout)
-                copy_rows(out + lo * out_stripe_stride + r.slot0 * out_slot_stride, out_stripe_stride,
-                          b.out + r.compact0 * nbytes, out_per, r.len * nbytes, n, hipMemcpyDeviceToHost, p.d2h);
+            for (size_t j = 0; j < fout.period; ++j) {
+                const Run &r = rout[j];
+                copy_rows(out + lo * out_stripe_stride + r.slot0 * out_slot_stride, fout.host_pitch,
+                          b.out + r.compact0 * nbytes, fout.dev_pitch, r.len * nbytes, n * fout.count,
+                          hipMemcpyDeviceToHost, p.d2h);
+            }
             check_hip(hipEventRecord(b.drained, p.d2h), "hipEventRecord");
         }
         check_hip(hipStreamSynchronize(p.d2h), "hipStreamSynchronize (host batch)");
@@ -195,6 +234,7 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
     chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
     const int64_t nchunks = (nstripes + chunk - 1) / chunk;
     const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
+    const Fold fin = fold_runs(rin, in_stripe_stride, in_slot_stride, in_per, nbytes);
 
     HostPipe &p = HostPipe::current();
     std::lock_guard<std::mutex> lk(p.mu);
@@ -204,9 +244,11 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
             HostPipe::Set &b = p.sets[(size_t)(i % nb)];
             const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
             if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
-            for (const Run &r : rin)
-                copy_rows(b.in + r.compact0 * nbytes, in_per, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
-                          in_stripe_stride, r.len * nbytes, n, hipMemcpyHostToDevice, p.h2d);
+            for (size_t j = 0; j < fin.period; ++j) {
+                const Run &r = rin[j];
+                copy_rows(b.in + r.compact0 * nbytes, fin.dev_pitch, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
+                          fin.host_pitch, r.len * nbytes, n * fin.count, hipMemcpyHostToDevice, p.h2d);
+            }
             check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
             if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");

@@ -2687,6 +2687,39 @@ def test_every_entry_kind_at_once(ecx, torch_dev):
     assert not errors, errors[:6]
 
 
+@pytest.mark.parametrize("small", [False, True])
+def test_host_batch_folded_runs_match_device_batch(ecx, torch_dev, small):
+    """Host batches whose used slots repeat with a fixed step (host_pipe.cpp fold_runs: one strided
+    copy of count x stripes rows per run of the first period) -- shortened Clay(10,4) single-node
+    repairs of nodes in each of the four y-groups (periods of 2 to 8 runs a plane group), the
+    Clay(4,2) two-node repair {0, 3} and a Clay(4,2) repair on a padded sub-chunk pitch -- write
+    exactly what the device batch writes on the same stripes, with default chunks and with one
+    stripe per chunk, and leave the output pitch's padding alone."""
+    torch = torch_dev
+    cases = [(10, 4, 2, [e], 512, 0) for e in (0, 3, 5, 9, 12)] + [(4, 2, 0, [0, 3], 1024, 0), (4, 2, 0, [1], 1000, 24)]
+    if small:
+        ecx.tune("host_chunk_kib", 16)
+    try:
+        for k, m, v, er, B, pad in cases:
+            n = k + m
+            step = ecx.ClayCodeErasureDecodingStep(er, k, m, virtualUnits=v)
+            a = step.map().info()["n_out"] // len(er)
+            S, P = 5, B + pad
+            src = torch.empty((S, n * a, P), dtype=torch.uint8, device="cuda")
+            ecx.fill_random(src, src.numel(), 300 + B + len(er) + er[0])
+            dev_out = torch.zeros((S, len(er) * a, P), dtype=torch.uint8, device="cuda")
+            step.performCodingBatch(src, n * a * P, P, dev_out, len(er) * a * P, P, S, B)
+            torch.cuda.synchronize()
+            host_in = src.cpu().numpy()
+            host_out = np.full((S, len(er) * a, P), 0x3C, np.uint8)
+            step.performCodingBatchHost(host_in, n * a * P, P, host_out, len(er) * a * P, P, S, B)
+            want = dev_out.cpu().numpy()
+            assert (host_out[:, :, :B] == want[:, :, :B]).all(), (k, m, er, B, pad)
+            assert (host_out[:, :, B:] == 0x3C).all(), (k, m, er, B, pad)
+    finally:
+        ecx.tune("host_chunk_kib", 65536)
+
+
 def test_host_check_batch_random_layouts(ecx):
     """isParityCorrectBatchHost(Devices) over 24 random layouts -- RS(k, m) with k + m <= 24,
     shard lengths 1 .. 20,000 B, byte windows at random offsets, padded pitches, 1 .. 9 stripes,
