@@ -44,6 +44,32 @@ public final class EcxBlockedStripes {
      */
     public void decodeMissing(ByteBuffer stripes, boolean[] shardPresent, long nstripes, long byteCount,
                               long blockBytes) {
+        byte[] flags = flags(shardPresent);
+        checkExtent(stripes, nstripes, byteCount);
+        Ecx.check(EcxNative.rsDecodeMissingBlockedBatchHostBuffer(handle(), flags, stripes, nstripes, byteCount,
+                blockBytes));
+    }
+
+    /**
+     * encodeParity split over several GPUs of this JVM: contiguous stripe ranges, one worker thread
+     * and stream set per entry of {@code devices} (ecx_rs_encode_parity_blocked_batch_host_devices).
+     */
+    public void encodeParity(ByteBuffer stripes, long nstripes, long byteCount, long blockBytes, int[] devices) {
+        checkExtent(stripes, nstripes, byteCount);
+        Ecx.check(EcxNative.rsEncodeParityBlockedBatchHostDevicesBuffer(handle(), stripes, nstripes, byteCount,
+                blockBytes, devices, devices == null ? 0 : devices.length));
+    }
+
+    /** decodeMissing split over several GPUs of this JVM (ecx_rs_decode_missing_blocked_batch_host_devices). */
+    public void decodeMissing(ByteBuffer stripes, boolean[] shardPresent, long nstripes, long byteCount,
+                              long blockBytes, int[] devices) {
+        byte[] flags = flags(shardPresent);
+        checkExtent(stripes, nstripes, byteCount);
+        Ecx.check(EcxNative.rsDecodeMissingBlockedBatchHostDevicesBuffer(handle(), flags, stripes, nstripes,
+                byteCount, blockBytes, devices, devices == null ? 0 : devices.length));
+    }
+
+    private byte[] flags(boolean[] shardPresent) {
         int n = dataShards + parityShards;
         if (shardPresent == null) {
             throw new NullPointerException("shardPresent");
@@ -55,9 +81,7 @@ public final class EcxBlockedStripes {
         for (int i = 0; i < n; i++) {
             flags[i] = (byte) (shardPresent[i] ? 1 : 0);
         }
-        checkExtent(stripes, nstripes, byteCount);
-        Ecx.check(EcxNative.rsDecodeMissingBlockedBatchHostBuffer(handle(), flags, stripes, nstripes, byteCount,
-                blockBytes));
+        return flags;
     }
 
     // The forwarder checks the same extent from the buffer's capacity; this gives the message.

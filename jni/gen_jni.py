@@ -159,6 +159,9 @@ RULES = {
     "ecx_clay_perform_coding_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
     "ecx_rs_is_parity_correct_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
     "ecx_rs_decode_missing_blocked_batch_host": (("rs",), [A("shard_present", RS_N)]),
+    "ecx_rs_encode_parity_blocked_batch_host_devices": ((), [NN("ndev"), A("devices", "ndev", err=ILL)]),
+    "ecx_rs_decode_missing_blocked_batch_host_devices": (("rs",), [A("shard_present", RS_N), NN("ndev"),
+                                                                   A("devices", "ndev", err=ILL)]),
 }
 
 
@@ -191,11 +194,16 @@ BLOCKED_EXTENT = ("    int64_t stripe_bytes = 0;\n"
                   "    max_in = 0;")
 BUFFER_VARIANTS["ecx_rs_encode_parity_blocked_batch_host"] = ("rs", BLOCKED_EXTENT, None)
 BUFFER_VARIANTS["ecx_rs_decode_missing_blocked_batch_host"] = ("rs", BLOCKED_EXTENT, None)
+BUFFER_VARIANTS["ecx_rs_encode_parity_blocked_batch_host_devices"] = ("rs", BLOCKED_EXTENT, None)
+BUFFER_VARIANTS["ecx_rs_decode_missing_blocked_batch_host_devices"] = ("rs", BLOCKED_EXTENT, None)
 # buffers laid out other than (stripe stride, slot stride) after the address: param (or (export,
 # param)) -> (stripe stride, slot stride, max slot, bytes per slot), as C expressions
 BUFFER_SHAPES = {"verdict": ("1", "0", "0", "1"),
                  ("ecx_rs_encode_parity_blocked_batch_host", "base"): ("stripe_bytes", "0", "0", "stripe_bytes"),
-                 ("ecx_rs_decode_missing_blocked_batch_host", "base"): ("stripe_bytes", "0", "0", "stripe_bytes")}
+                 ("ecx_rs_decode_missing_blocked_batch_host", "base"): ("stripe_bytes", "0", "0", "stripe_bytes"),
+                 ("ecx_rs_encode_parity_blocked_batch_host_devices", "base"): ("stripe_bytes", "0", "0", "stripe_bytes"),
+                 ("ecx_rs_decode_missing_blocked_batch_host_devices", "base"): ("stripe_bytes", "0", "0",
+                                                                                "stripe_bytes")}
 
 
 def host_address_native(name):

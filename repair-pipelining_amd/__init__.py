@@ -689,6 +689,29 @@ class ReedSolomon:
         check(lib().ecx_rs_decode_missing_blocked_batch_host(self._h, pres.ctypes.data, _host_ptr(base), nstripes,
                                                              byteCount, blockBytes))
 
+    def encodeParityBlockedBatchHostDevices(self, base, nstripes, byteCount, devices, blockBytes=0):
+        """encodeParityBlockedBatchHost split over several GPUs of this process
+        (ecx_rs_encode_parity_blocked_batch_host_devices): contiguous stripe ranges, one worker
+        thread and pipe per device entry."""
+        _check_extent(base, nstripes * self.getTotalShardCount() * byteCount, "base")
+        devs = list(devices)
+        arr = np.ascontiguousarray(devs + [0], np.int32)  # never a null list: an empty one is ndev 0
+        check(lib().ecx_rs_encode_parity_blocked_batch_host_devices(self._h, _host_ptr(base), nstripes, byteCount,
+                                                                    blockBytes, arr.ctypes.data, len(devs)))
+
+    def decodeMissingBlockedBatchHostDevices(self, base, shardPresent, nstripes, byteCount, devices, blockBytes=0):
+        """decodeMissingBlockedBatchHost split over several GPUs of this process
+        (ecx_rs_decode_missing_blocked_batch_host_devices)."""
+        pres = np.array([1 if p else 0 for p in shardPresent], np.uint8)
+        if len(pres) != self.getTotalShardCount():
+            raise EcxError(-1, "wrong number of shardPresent flags")
+        _check_extent(base, nstripes * self.getTotalShardCount() * byteCount, "base")
+        devs = list(devices)
+        arr = np.ascontiguousarray(devs + [0], np.int32)
+        check(lib().ecx_rs_decode_missing_blocked_batch_host_devices(self._h, pres.ctypes.data, _host_ptr(base),
+                                                                     nstripes, byteCount, blockBytes,
+                                                                     arr.ctypes.data, len(devs)))
+
     def isParityCorrectBatch(self, shards, stripe_stride, shard_stride, nstripes, firstByte, byteCount, verdict,
                              stream=None) -> None:
         """isParityCorrect over nstripes device-resident stripes, read-only

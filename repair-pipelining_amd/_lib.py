@@ -107,6 +107,8 @@ SIGNATURES = {
     "ecx_rs_decode_missing_blocked_batch": (I, [P, P, P, I64, I64, I64, P]),
     "ecx_rs_encode_parity_blocked_batch_host": (I, [P, P, I64, I64, I64]),
     "ecx_rs_decode_missing_blocked_batch_host": (I, [P, P, P, I64, I64, I64]),
+    "ecx_rs_encode_parity_blocked_batch_host_devices": (I, [P, P, I64, I64, I64, P, I]),
+    "ecx_rs_decode_missing_blocked_batch_host_devices": (I, [P, P, P, I64, I64, I64, P, I]),
     "ecx_map_accumulate_batch": (I, [P, P, I64, I64, P, I64, I64, I64, I64, P]),
     "ecx_rs_encode_map": (I, [P, ctypes.POINTER(P)]),
     "ecx_rs_decode_map": (I, [P, P, ctypes.POINTER(P)]),

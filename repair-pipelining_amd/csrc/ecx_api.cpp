@@ -608,10 +608,26 @@ void launch_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int
 }
 
 // The same two passes from host memory: two pipelined host batches (host_pipe.cpp), the second
-// after the first has drained (each is synchronous).
-void host_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block) {
-    blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
-        run_host_batch(cm, base + off, ss, len, base + off, ss, len, units, len);
+// after the first has drained (each is synchronous).  With a device list (ndev > 0), contiguous
+// stripe ranges per entry: a range's full blocks and its tails are each contiguous in the batch.
+void host_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block,
+                  const int *devices = nullptr, int ndev = 0) {
+    if (ndev == 0 && !devices) {
+        blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
+            run_host_batch(cm, base + off, ss, len, base + off, ss, len, units, len);
+        });
+        return;
+    }
+    int64_t body = 0;  // the whole batch's full blocks: its extent is checked before any worker starts
+    blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t, int64_t, int64_t) { body = std::max(body, off); });
+    const int64_t full = block > 0 ? byte_count / block : 0, tail = block > 0 ? byte_count % block : 0;
+    for_device_ranges(devices, ndev, byte_count > 0 ? nstripes : 0, [&](int64_t lo, int64_t cnt) {
+        blocked_passes(n, cnt, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
+            (void)off;  // the range's own offsets; its place in the batch: the full-block pass has
+                        // slots of `block` bytes, the tail pass slots of `tail` < block bytes
+            uint8_t *p = len == block ? base + lo * full * n * block : base + body + lo * n * tail;
+            run_host_batch(cm, p, ss, len, p, ss, len, units, len);
+        });
     });
 }
 }  // namespace
@@ -697,6 +713,43 @@ int ecx_rs_decode_missing_blocked_batch_host(ecx_rs *rs, const uint8_t *shard_pr
         const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
         if (m->cm.map().n_out == 0) return ECX_OK;  // all present (ReedSolomon.java:216-218)
         host_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_encode_parity_blocked_batch_host_devices(ecx_rs *rs, uint8_t *base, int64_t nstripes, int64_t byte_count,
+                                                    int64_t block_bytes, const int *devices, int ndev) {
+    return guarded(__func__, [&]() -> int {
+        if (!rs) throw Error(ECX_E_NULL, "null codec");
+        if (!devices) throw Error(ECX_E_NULL, "null device list");
+        if (ndev <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "empty device list");
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (nstripes > 0 && !base) throw Error(ECX_E_NULL, "null host pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_encode_map(rs, &m);
+        if (st) return st;
+        const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
+        host_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), nstripes, byte_count, block, devices, ndev);
+        return ECX_OK;
+    });
+}
+
+int ecx_rs_decode_missing_blocked_batch_host_devices(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base,
+                                                     int64_t nstripes, int64_t byte_count, int64_t block_bytes,
+                                                     const int *devices, int ndev) {
+    return guarded(__func__, [&]() -> int {
+        if (!rs) throw Error(ECX_E_NULL, "null codec");
+        if (!devices) throw Error(ECX_E_NULL, "null device list");
+        if (ndev <= 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "empty device list");
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        if (nstripes > 0 && !base) throw Error(ECX_E_NULL, "null host pointer");
+        const ecx_map *m = nullptr;
+        const int st = ecx_rs_decode_map(rs, shard_present, &m);  // Not enough shards -> -2
+        if (st) return st;
+        const int64_t block = resolve_block(rs->code.n(), byte_count, block_bytes);
+        // all present (ReedSolomon.java:216-218): nothing to touch, the device list still checked
+        host_blocked(const_cast<ecx_map *>(m)->cm, base, rs->code.n(), m->cm.map().n_out == 0 ? 0 : nstripes,
+                     byte_count, block, devices, ndev);
         return ECX_OK;
     });
 }

@@ -326,6 +326,11 @@ void on_devices(const int *devices, int ndev, int64_t nstripes, F &&range) {
 
 }  // namespace
 
+void for_device_ranges(const int *devices, int ndev, int64_t nstripes,
+                       const std::function<void(int64_t, int64_t)> &range) {
+    on_devices(devices, ndev, nstripes, range);
+}
+
 void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                             uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                             int64_t nbytes, const int *devices, int ndev) {

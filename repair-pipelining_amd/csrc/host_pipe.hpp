@@ -2,6 +2,8 @@
 // map batches are declared with the engine, engine.hpp).
 #pragma once
 
+#include <functional>
+
 #include "engine.hpp"
 
 namespace ecx {
@@ -15,5 +17,11 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
 void run_host_check_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride,
                                   int64_t in_slot_stride, int64_t nstripes, int64_t nbytes, uint8_t *verdict,
                                   const int *devices, int ndev);
+
+// range(lo, count) over contiguous stripe ranges of nstripes split over a device list, one worker
+// thread per entry with that device current: the split, validation and error reporting of
+// run_host_batch_devices, for host batches made of several passes (the blocked RS layout).
+void for_device_ranges(const int *devices, int ndev, int64_t nstripes,
+                       const std::function<void(int64_t, int64_t)> &range);
 
 }  // namespace ecx

@@ -1215,13 +1215,15 @@ def test_rs_blocked_batches_vs_oracle(ecx, torch_dev, k, m, L, block):
         assert all((got[s, i] == ref[i]).all() for i in range(n)), (s, present)
 
 
-@pytest.mark.parametrize("k,m,L,block,pinned,small", [(17, 3, 200000, 0, True, False), (17, 3, 200000, 0, False, True),
-                                                      (12, 4, 3 * 65536, 0, True, True), (4, 2, 104449, 4096, False, False),
-                                                      (5, 5, 1001, 64, True, True), (3, 1, 34, 0, False, False)])
-def test_rs_blocked_batches_host_vs_oracle(ecx, torch_dev, k, m, L, block, pinned, small):
+@pytest.mark.parametrize("k,m,L,block,pinned,small,devs", [
+    (17, 3, 200000, 0, True, False, None), (17, 3, 200000, 0, False, True, [0, 0]),
+    (12, 4, 3 * 65536, 0, True, True, None), (4, 2, 104449, 4096, False, False, [0, 0, 0]),
+    (5, 5, 1001, 64, True, True, [0, 0]), (3, 1, 34, 0, False, False, None), (3, 1, 34, 0, True, True, [0, 0, 0])])
+def test_rs_blocked_batches_host_vs_oracle(ecx, torch_dev, k, m, L, block, pinned, small, devs):
     """The blocked batches from HOST memory (ecx_rs_encode_parity_blocked_batch_host /
     ecx_rs_decode_missing_blocked_batch_host: the full blocks, then the tails, each a pipelined host
-    batch), pageable and pinned, with the default chunks and with one stripe per chunk (ring reuse):
+    batch; the _devices forms split the stripes over a device list, here device 0 two or three
+    times), pageable and pinned, with the default chunks and with one stripe per chunk (ring reuse):
     every stripe equals the oracle's encodeParity / decodeMissing on its natural shards, the
     present shards of a decode are left as they were, and nothing past the batch is written."""
     torch = torch_dev
@@ -1245,11 +1247,17 @@ def test_rs_blocked_batches_host_vs_oracle(ecx, torch_dev, k, m, L, block, pinne
             buf[total:] = 0xE7
             present = [True] * n
             if op == "encode":
-                rs.encodeParityBlockedBatchHost(buf, S, L, block)
+                if devs:
+                    rs.encodeParityBlockedBatchHostDevices(buf, S, L, devs, block)
+                else:
+                    rs.encodeParityBlockedBatchHost(buf, S, L, block)
             else:
                 for i in (0, n - 1)[:m]:
                     present[i] = False
-                rs.decodeMissingBlockedBatchHost(buf, present, S, L, block)
+                if devs:
+                    rs.decodeMissingBlockedBatchHostDevices(buf, present, S, L, devs, block)
+                else:
+                    rs.decodeMissingBlockedBatchHost(buf, present, S, L, block)
             assert (buf[total:] == 0xE7).all()
             got = ecx.blocked_unpack(torch.from_numpy(buf[:total].copy()), S, n, L, b).numpy()
             for s in range(S):

@@ -114,14 +114,17 @@ def test_no_public_native_takes_a_raw_host_address():
     for name in ("directAddress", "wrapAddress", "mapApplyBatchHost", "clayPerformCodingBatchHost",
                  "mapApplyBatchHostDevices", "clayPerformCodingBatchHostDevices", "rsIsParityCorrectBatchHost",
                  "rsIsParityCorrectBatchHostDevices", "rsEncodeParityBlockedBatchHost",
-                 "rsDecodeMissingBlockedBatchHost"):
+                 "rsDecodeMissingBlockedBatchHost", "rsEncodeParityBlockedBatchHostDevices",
+                 "rsDecodeMissingBlockedBatchHostDevices"):
         assert name not in public, name
         assert re.search(r"\n    static native [\w\[\]]+ %s\(" % name, JAVA_SRC), name
     host_batch = {n: p for n, p in public.items() if "BatchHost" in n}
     assert set(host_batch) == {"mapApplyBatchHostBuffer", "clayPerformCodingBatchHostBuffer",
                                "mapApplyBatchHostDevicesBuffer", "clayPerformCodingBatchHostDevicesBuffer",
                                "rsIsParityCorrectBatchHostBuffer", "rsIsParityCorrectBatchHostDevicesBuffer",
-                               "rsEncodeParityBlockedBatchHostBuffer", "rsDecodeMissingBlockedBatchHostBuffer"}
+                               "rsEncodeParityBlockedBatchHostBuffer", "rsDecodeMissingBlockedBatchHostBuffer",
+                               "rsEncodeParityBlockedBatchHostDevicesBuffer",
+                               "rsDecodeMissingBlockedBatchHostDevicesBuffer"}
     blocked = {n for n in host_batch if "Blocked" in n}  # one buffer of whole blocked stripes, in place
     for n, params in host_batch.items():
         if n in blocked:

@@ -400,6 +400,14 @@ def test_rs_blocked_batch_host_buffer_checks(J):
         assert dec(J.array(pres[:n - 1]), J.direct(buf)) == IDX            # flags one short
         assert dec(None, J.direct(buf)) == NUL
         assert J.call("rsEncodeParityBlockedBatchHostBuffer", 0, J.direct(buf), S, L, blk) == NUL
+        denc = lambda b, devs, nd: J.call("rsEncodeParityBlockedBatchHostDevicesBuffer", rs, b, S, L, blk,  # noqa: E731
+                                          devs, nd)
+        ddec = lambda p, devs, nd: J.call("rsDecodeMissingBlockedBatchHostDevicesBuffer", rs, p, J.direct(buf),  # noqa: E731
+                                          S, L, blk, devs, nd)
+        assert denc(J.direct(buf, need - 1), J.ints([0]), 1) == IDX
+        assert denc(J.direct(buf), J.ints([0]), 2) == ILL and denc(J.direct(buf), None, 1) == NUL
+        assert denc(J.direct(buf), J.ints([0]), -1) == ILL and denc(J.array(buf), J.ints([0]), 1) == NUL
+        assert ddec(J.array(pres[:n - 1]), J.ints([0]), 1) == IDX and ddec(J.array(pres), J.ints([0]), 2) == ILL
         assert J.counters()["pins"] == 0 and (buf == before).all()
         st = enc(J.direct(buf))
         assert st == (OK if has_device(J) else DEV), st
@@ -407,6 +415,12 @@ def test_rs_blocked_batch_host_buffer_checks(J):
             assert (buf == _np_blocked(_oracle_rs(k, m, nat, "encode"), blk)).all()
             buf[:] = _np_blocked(nat, blk)
             assert dec(J.array(pres), J.direct(buf)) == OK
+            assert (buf == _np_blocked(_oracle_rs(k, m, nat, "decode", pres), blk)).all()
+            buf[:] = _np_blocked(nat, blk)
+            assert denc(J.direct(buf), J.ints([0, 0]), 2) == OK
+            assert (buf == _np_blocked(_oracle_rs(k, m, nat, "encode"), blk)).all()
+            buf[:] = _np_blocked(nat, blk)
+            assert ddec(J.array(pres), J.ints([0, 0]), 2) == OK
             assert (buf == _np_blocked(_oracle_rs(k, m, nat, "decode", pres), blk)).all()
     finally:
         J.call("rsDestroy", rs)
