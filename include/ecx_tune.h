@@ -218,6 +218,15 @@ int ecx_map_layout_choice(const struct ecx_map *map, int64_t slot_pitch, float *
  * launched between the probing stream's previous launch and the probe's end (a launch that
  * finds the probe already finished does not count).  Either pointer may be NULL. */
 int ecx_map_layout_state(const struct ecx_map *map, int64_t slot_pitch, int *state, int *dropped);
+/* How ecx_map_apply_batch_host would move a batch of this layout (host_pipe.cpp; host-only, no
+ * device touched): plan[7] = {stripes per pipelined chunk, chunks, device buffer sets in flight,
+ * strided H2D copies per chunk, rows per stripe of each H2D copy, D2H copies per chunk, rows per
+ * stripe of each D2H copy}.  Runs of used slots that repeat with a fixed step across the stripe
+ * are folded into one copy per period (rows per stripe > 1).  All zero when the batch moves
+ * nothing (no stripes, no bytes, nothing to write). */
+int ecx_map_host_plan(const struct ecx_map *map, int64_t in_stripe_stride, int64_t in_slot_stride,
+                      int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t byte_count,
+                      int64_t *plan);
 /* The kernel instance of the last full-chunk launch this thread enqueued, named as
  * rocprofv3 names it (e.g. "k_gf_apply<false, true, 1, 20, false, 256, 8>"), copied
  * NUL-terminated into buf.  Returns its length (0 = no launch yet), or

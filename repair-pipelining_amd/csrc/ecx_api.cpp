@@ -1687,6 +1687,20 @@ int ecx_map_layout_state(const ecx_map *map, int64_t slot_pitch, int *state, int
     });
 }
 
+int ecx_map_host_plan(const ecx_map *map, int64_t in_stripe_stride, int64_t in_slot_stride, int64_t out_stripe_stride,
+                      int64_t out_slot_stride, int64_t nstripes, int64_t byte_count, int64_t *plan) {
+    return guarded(__func__, [&]() -> int {
+        if (!map || !plan) throw Error(ECX_E_NULL, "null map or plan");
+        if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
+        const HostBatchPlan hp = plan_host_batch(const_cast<ecx_map *>(map)->cm, in_stripe_stride, in_slot_stride,
+                                                 out_stripe_stride, out_slot_stride, nstripes, byte_count);
+        const int64_t v[7] = {hp.chunk, hp.nchunks, hp.buffers, hp.h2d_copies, hp.h2d_rows, hp.d2h_copies,
+                              hp.d2h_rows};
+        std::memcpy(plan, v, sizeof(v));
+        return ECX_OK;
+    });
+}
+
 int ecx_last_launch_shape(char *buf, int len) {
     const std::string k = last_launch_shape();
     if (!buf || len < (int)k.size() + 1) return ECX_E_ILLEGAL_ARGUMENT;

@@ -74,6 +74,48 @@ Fold fold_runs(const std::vector<Run> &runs, int64_t stripe_stride, int64_t slot
     return {n, 1, stripe_stride, per};
 }
 
+// The chunking and copy plan of one host batch (run_host_batch; run_host_check_batch, whose only
+// output is one verdict byte per stripe).
+struct Plan {
+    std::vector<Run> rin, rout;
+    Fold fin{}, fout{};
+    int64_t in_per = 0, out_per = 0, chunk = 1, nchunks = 0;
+    int nb = 1;
+};
+
+Plan make_plan(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride, int64_t out_stripe_stride,
+               int64_t out_slot_stride, int64_t nstripes, int64_t nbytes, bool outputs) {
+    Plan pl;
+    const std::vector<int> &ins = cm.used_in_slots();
+    pl.in_per = (int64_t)ins.size() * nbytes;
+    pl.rin = runs_of(ins, in_slot_stride, nbytes);
+    if (outputs) {
+        const std::vector<int> &outs = cm.used_out_slots();
+        pl.out_per = (int64_t)outs.size() * nbytes;
+        pl.rout = runs_of(outs, out_slot_stride, nbytes);
+    }
+    const Tuning &t = tuning();
+    const int64_t in_per = pl.in_per;
+    const std::vector<Run> &rin = pl.rin;
+    // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a stripe's used
+    // slots fall into many runs (shortened Clay(10,4), node 3: 65 runs of 3-13 sub-chunks; Clay(4,2)
+    // {0,3}: 16 runs of 2), so each strided copy moves whole rows of many stripes instead of a few KiB per
+    // call -- within 8x host_chunk.  The DMA queue idles ~16 us between copies (the copy trace,
+    // DESIGN.md 6); 160 rows beat 64, 96, 256 and 512 and equal-size chunks
+    // (profiles/r06_minrows_ab*.jsonl).
+    constexpr int64_t kMinRows = 160;
+    int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
+    if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
+    chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
+    const int64_t nchunks = (nstripes + chunk - 1) / chunk;
+    pl.chunk = chunk;
+    pl.nchunks = nchunks;
+    pl.nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), std::max<int64_t>(1, nchunks));
+    pl.fin = fold_runs(rin, in_stripe_stride, in_slot_stride, in_per, nbytes);
+    if (outputs) pl.fout = fold_runs(pl.rout, out_stripe_stride, out_slot_stride, pl.out_per, nbytes);
+    return pl;
+}
+
 // Copy `rows` rows of `width` bytes between two pitched layouts.
 void copy_rows(uint8_t *dst, int64_t dpitch, const uint8_t *src, int64_t spitch, int64_t width, int64_t rows,
                hipMemcpyKind kind, hipStream_t s) {
@@ -159,24 +201,12 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
                     int64_t nbytes) {
     if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return;
     CompiledMap &cc = cm.compact();
-    const std::vector<int> &ins = cm.used_in_slots(), &outs = cm.used_out_slots();
-    const int64_t in_per = (int64_t)ins.size() * nbytes, out_per = (int64_t)outs.size() * nbytes;
-    const Tuning &t = tuning();
-    const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes), rout = runs_of(outs, out_slot_stride, nbytes);
-    // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a stripe's used
-    // slots fall into many runs (shortened Clay(10,4), node 3: 65 runs of 3-13 sub-chunks; Clay(4,2)
-    // {0,3}: 16 runs of 2), so each strided copy moves whole rows of many stripes instead of a few KiB per
-    // call -- within 8x host_chunk.  The DMA queue idles ~16 us between copies (the copy trace,
-    // DESIGN.md 6); 160 rows beat 64, 96, 256 and 512 and equal-size chunks
-    // (profiles/r06_minrows_ab*.jsonl).
-    constexpr int64_t kMinRows = 160;
-    int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
-    if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
-    chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
-    const int64_t nchunks = (nstripes + chunk - 1) / chunk;
-    const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
-    const Fold fin = fold_runs(rin, in_stripe_stride, in_slot_stride, in_per, nbytes),
-               fout = fold_runs(rout, out_stripe_stride, out_slot_stride, out_per, nbytes);
+    const Plan pl = make_plan(cm, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes,
+                              nbytes, true);
+    const std::vector<Run> &rin = pl.rin, &rout = pl.rout;
+    const Fold &fin = pl.fin, &fout = pl.fout;
+    const int64_t in_per = pl.in_per, out_per = pl.out_per, chunk = pl.chunk, nchunks = pl.nchunks;
+    const int nb = pl.nb;
 
     HostPipe &p = HostPipe::current();
     std::lock_guard<std::mutex> lk(p.mu);
@@ -212,6 +242,22 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     }
 }
 
+HostBatchPlan plan_host_batch(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride,
+                              int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes) {
+    HostBatchPlan hp;
+    if (nstripes <= 0 || nbytes <= 0 || cm.map().n_out == 0) return hp;  // run_host_batch moves nothing
+    const Plan pl = make_plan(cm, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes,
+                              nbytes, true);
+    hp.chunk = pl.chunk;
+    hp.nchunks = pl.nchunks;
+    hp.buffers = pl.nb;
+    hp.h2d_copies = (int64_t)pl.fin.period;
+    hp.h2d_rows = pl.fin.count;
+    hp.d2h_copies = (int64_t)pl.fout.period;
+    hp.d2h_rows = pl.fout.count;
+    return hp;
+}
+
 void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride, int64_t in_slot_stride,
                           int64_t nstripes, int64_t nbytes, uint8_t *verdict) {
     if (nstripes <= 0) return;
@@ -224,17 +270,11 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
     // compact buffer, k_gf_check writes one verdict byte per stripe of the chunk into the set's
     // output area, and only those bytes come back.
     CompiledMap &cc = cm.compact();
-    const std::vector<int> &ins = cm.used_in_slots();
-    const int64_t in_per = (int64_t)ins.size() * nbytes;
-    const Tuning &t = tuning();
-    const std::vector<Run> rin = runs_of(ins, in_slot_stride, nbytes);
-    constexpr int64_t kMinRows = 160;
-    int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
-    if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
-    chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
-    const int64_t nchunks = (nstripes + chunk - 1) / chunk;
-    const int nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), nchunks);
-    const Fold fin = fold_runs(rin, in_stripe_stride, in_slot_stride, in_per, nbytes);
+    const Plan pl = make_plan(cm, in_stripe_stride, in_slot_stride, 0, 0, nstripes, nbytes, false);
+    const std::vector<Run> &rin = pl.rin;
+    const Fold &fin = pl.fin;
+    const int64_t in_per = pl.in_per, chunk = pl.chunk, nchunks = pl.nchunks;
+    const int nb = pl.nb;
 
     HostPipe &p = HostPipe::current();
     std::lock_guard<std::mutex> lk(p.mu);

@@ -18,6 +18,17 @@ void run_host_check_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in
                                   int64_t in_slot_stride, int64_t nstripes, int64_t nbytes, uint8_t *verdict,
                                   const int *devices, int ndev);
 
+// How run_host_batch moves a batch (ecx_map_host_plan, include/ecx_tune.h): stripes per chunk, the
+// chunk count, device buffer sets in flight, and per chunk the strided H2D / D2H copies and the
+// rows each copy moves per stripe (> 1 where periodic runs are folded into one copy).
+struct HostBatchPlan {
+    int64_t chunk = 0, nchunks = 0;
+    int buffers = 0;
+    int64_t h2d_copies = 0, h2d_rows = 0, d2h_copies = 0, d2h_rows = 0;
+};
+HostBatchPlan plan_host_batch(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride,
+                              int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes);
+
 // range(lo, count) over contiguous stripe ranges of nstripes split over a device list, one worker
 // thread per entry with that device current: the split, validation and error reporting of
 // run_host_batch_devices, for host batches made of several passes (the blocked RS layout).
