@@ -519,14 +519,15 @@ class GfMap:
     def host_plan(self, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes, byte_count):
         """How apply_batch_host would move this batch (ecx_map_host_plan, host-only): a dict of the
         stripes per chunk, the chunk count, the buffer sets, and per chunk the H2D / D2H strided
-        copies with the rows per stripe each moves (> 1 where periodic runs are folded)."""
+        copies with the most rows per stripe one copy moves (> 1 where runs are folded or copied in
+        3D) and how many of them are 3D."""
         f = lib().ecx_map_host_plan
         f.argtypes = [ctypes.c_void_p] + [ctypes.c_int64] * 6 + [ctypes.c_void_p]
         f.restype = ctypes.c_int
-        out = np.zeros(7, np.int64)
+        out = np.zeros(9, np.int64)
         check(f(self._h, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes, byte_count,
                 out.ctypes.data))
-        keys = ("chunk", "chunks", "buffers", "h2d_copies", "h2d_rows", "d2h_copies", "d2h_rows")
+        keys = ("chunk", "chunks", "buffers", "h2d_copies", "h2d_rows", "d2h_copies", "d2h_rows", "h2d_3d", "d2h_3d")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def layout_state(self, slot_pitch: int):

@@ -44,23 +44,33 @@ std::vector<Run> runs_of(const std::vector<int> &slots, int64_t slot_stride, int
 }
 
 // The runs of a stripe often repeat with a fixed step: a Clay repair reads the same helper nodes
-// of every plane (Clay(4,2) {0,3}: nodes 1-2 and 4-5 of all 8 planes, 16 runs), a check on a
-// padded pitch reads every shard.  When runs[i + period] is runs[i] moved by a fixed number of
-// host slots and of compact slots for every i, and `count` such steps span exactly one stripe on
-// both sides, the k-th run of every period in every stripe of a chunk lies at a fixed pitch: one
-// strided copy of count x stripes rows per run of the first period moves them all (Clay(4,2)
-// {0,3}: 1 copy per chunk instead of 16, e2e 71.6 -> 75.9 GiB/s, profiles/r06_fold_ab.jsonl).
-struct Fold {
-    size_t period;        // runs copied per chunk
-    int64_t count;        // rows per stripe of each of those copies
-    int64_t host_pitch;   // bytes between the rows on the host side
-    int64_t dev_pitch;    // ... and in the compact device buffer
+// of every plane of a plane group (Clay(4,2) {0,3}: nodes 1-2 and 4-5 of all 8 planes, 16 runs;
+// shortened Clay(10,4), node 0: nodes 1-13 of planes 0-63, 64 runs), a check on a padded pitch
+// reads every shard.  One copy then moves many runs of every stripe of a chunk:
+//  * folded 2D: when runs[i + period] is runs[i] moved by fixed host and compact steps for every i
+//    and `count` steps span exactly one stripe on both sides, the k-th run of every period of
+//    every stripe lies at a fixed pitch -- one strided copy of count x stripes rows per run of
+//    the first period (Clay(4,2) {0,3}: 1 copy per chunk instead of 16, e2e 71.6 -> 75.9 GiB/s,
+//    profiles/r06_fold_ab.jsonl);
+//  * 3D: otherwise each maximal progression of equal runs at fixed steps (that divide the stripe
+//    on both sides) is one hipMemcpy3DAsync -- its rows, then the next stripe (Clay(10,4) node 3:
+//    3 copies per chunk instead of 65; H2D of node 0's 64 runs 53.2 -> 57.2 GB/s,
+//    profiles/r06_copy3d_probe.jsonl; its e2e 56.7 -> 62.5 GiB/s, the headline's 68.0 -> 69.4,
+//    profiles/r06_copy3d_ab.jsonl);
+//  * any other run: one strided copy of its rows of the chunk's stripes.
+struct Copy {
+    int64_t host_off, dev_off;      // the copy's first byte in the chunk's first stripe
+    int64_t width;                  // bytes per row
+    int64_t rows;                   // rows per stripe
+    int64_t host_pitch, dev_pitch;  // between a stripe's rows (folded: continuing across stripes)
+    bool three_d;                   // rows of one stripe, then the next stripe a stripe stride on
 };
 
-Fold fold_runs(const std::vector<Run> &runs, int64_t stripe_stride, int64_t slot_stride, int64_t per,
-               int64_t nbytes) {
+std::vector<Copy> plan_copies(const std::vector<Run> &runs, int64_t stripe_stride, int64_t slot_stride, int64_t per,
+                              int64_t nbytes) {
+    std::vector<Copy> cs;
     const size_t n = runs.size();
-    for (size_t p = 1; p < n; ++p) {
+    for (size_t p = 1; p < n; ++p) {  // folded 2D
         if (n % p) continue;
         const int64_t ds = runs[p].slot0 - runs[0].slot0, dc = runs[p].compact0 - runs[0].compact0;
         const int64_t count = (int64_t)(n / p);
@@ -69,16 +79,42 @@ Fold fold_runs(const std::vector<Run> &runs, int64_t stripe_stride, int64_t slot
         for (size_t i = 0; ok && i + p < n; ++i)
             ok = runs[i + p].len == runs[i].len && runs[i + p].slot0 - runs[i].slot0 == ds &&
                  runs[i + p].compact0 - runs[i].compact0 == dc;
-        if (ok) return {p, count, ds * slot_stride, dc * nbytes};
+        if (!ok) continue;
+        for (size_t k = 0; k < p; ++k)
+            cs.push_back({runs[k].slot0 * slot_stride, runs[k].compact0 * nbytes, runs[k].len * nbytes, count,
+                          ds * slot_stride, dc * nbytes, false});
+        return cs;
     }
-    return {n, 1, stripe_stride, per};
+    for (size_t i = 0; i < n;) {
+        size_t j = i;
+        int64_t ds = 0, dc = 0;
+        if (i + 1 < n && runs[i + 1].len == runs[i].len) {
+            ds = runs[i + 1].slot0 - runs[i].slot0;
+            dc = runs[i + 1].compact0 - runs[i].compact0;
+            while (j + 1 < n && runs[j + 1].len == runs[i].len && runs[j + 1].slot0 - runs[j].slot0 == ds &&
+                   runs[j + 1].compact0 - runs[j].compact0 == dc)
+                ++j;
+        }
+        const int64_t hp = ds * slot_stride, dp = dc * nbytes;
+        if (j > i && hp > 0 && dp > 0 && stripe_stride > 0 && stripe_stride % hp == 0 &&
+            per % dp == 0) {
+            cs.push_back({runs[i].slot0 * slot_stride, runs[i].compact0 * nbytes, runs[i].len * nbytes,
+                          (int64_t)(j - i + 1), hp, dp, true});
+        } else {
+            for (size_t k = i; k <= j; ++k)
+                cs.push_back({runs[k].slot0 * slot_stride, runs[k].compact0 * nbytes, runs[k].len * nbytes, 1,
+                              stripe_stride, per, false});
+        }
+        i = j + 1;
+    }
+    return cs;
 }
 
 // The chunking and copy plan of one host batch (run_host_batch; run_host_check_batch, whose only
 // output is one verdict byte per stripe).
 struct Plan {
     std::vector<Run> rin, rout;
-    Fold fin{}, fout{};
+    std::vector<Copy> cin, cout;
     int64_t in_per = 0, out_per = 0, chunk = 1, nchunks = 0;
     int nb = 1;
 };
@@ -97,22 +133,22 @@ Plan make_plan(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride
     const Tuning &t = tuning();
     const int64_t in_per = pl.in_per;
     const std::vector<Run> &rin = pl.rin;
-    // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a stripe's used
-    // slots fall into many runs (shortened Clay(10,4), node 3: 65 runs of 3-13 sub-chunks; Clay(4,2)
-    // {0,3}: 16 runs of 2), so each strided copy moves whole rows of many stripes instead of a few KiB per
-    // call -- within 8x host_chunk.  The DMA queue idles ~16 us between copies (the copy trace,
-    // DESIGN.md 6); 160 rows beat 64, 96, 256 and 512 and equal-size chunks
-    // (profiles/r06_minrows_ab*.jsonl).
+    // Stripes per chunk: host_chunk bytes of input, but at least kMinRows stripes when a chunk still
+    // takes more than 8 copies after folding and 3D (Clay(10,4) node 4: 17), so each copy moves rows
+    // of many stripes instead of a few KiB -- within 8x host_chunk.  The DMA queue idles ~16 us
+    // between copies (the copy trace); with one copy per run, 160 rows beat 64, 96, 256
+    // and 512 and equal-size chunks (profiles/r06_minrows_ab*.jsonl); once 3D copies took Clay(10,4)
+    // node 3 to 3 copies, dropping the floor for it gained another 4 % (profiles/r06_floor_ab.jsonl).
     constexpr int64_t kMinRows = 160;
+    pl.cin = plan_copies(rin, in_stripe_stride, in_slot_stride, in_per, nbytes);
     int64_t chunk = t.host_chunk / std::max<int64_t>(1, in_per);
-    if (rin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
+    if (pl.cin.size() > 8) chunk = std::max(chunk, std::min(kMinRows, 8 * t.host_chunk / std::max<int64_t>(1, in_per)));
     chunk = std::max<int64_t>(1, std::min<int64_t>(nstripes, chunk));
     const int64_t nchunks = (nstripes + chunk - 1) / chunk;
     pl.chunk = chunk;
     pl.nchunks = nchunks;
     pl.nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), std::max<int64_t>(1, nchunks));
-    pl.fin = fold_runs(rin, in_stripe_stride, in_slot_stride, in_per, nbytes);
-    if (outputs) pl.fout = fold_runs(pl.rout, out_stripe_stride, out_slot_stride, pl.out_per, nbytes);
+    if (outputs) pl.cout = plan_copies(pl.rout, out_stripe_stride, out_slot_stride, pl.out_per, nbytes);
     return pl;
 }
 
@@ -131,6 +167,36 @@ void copy_rows(uint8_t *dst, int64_t dpitch, const uint8_t *src, int64_t spitch,
     for (int64_t r = 0; r < rows; ++r)
         check_hip(hipMemcpyAsync(dst + r * dpitch, src + r * spitch, (size_t)width, kind, s),
                   "hipMemcpyAsync (host batch row)");
+}
+
+// One planned copy for the `n` stripes of a chunk: host side at `host` (stripe stride
+// `host_stripe`), device side at `dev` (stripe stride `dev_stripe`), in direction `kind`.
+void issue_copy(const Copy &c, const uint8_t *host_base, uint8_t *dev_base, int64_t host_stripe, int64_t dev_stripe,
+                int64_t n, hipMemcpyKind kind, hipStream_t s) {
+    uint8_t *host = const_cast<uint8_t *>(host_base) + c.host_off;
+    uint8_t *dev = dev_base + c.dev_off;
+    const bool h2d = kind == hipMemcpyHostToDevice;
+    if (c.three_d) {
+        hipMemcpy3DParms p;
+        std::memset(&p, 0, sizeof(p));
+        const hipPitchedPtr hptr = make_hipPitchedPtr(host, (size_t)c.host_pitch, (size_t)c.width,
+                                                      (size_t)(host_stripe / c.host_pitch));
+        const hipPitchedPtr dptr = make_hipPitchedPtr(dev, (size_t)c.dev_pitch, (size_t)c.width,
+                                                      (size_t)(dev_stripe / c.dev_pitch));
+        p.srcPtr = h2d ? hptr : dptr;
+        p.dstPtr = h2d ? dptr : hptr;
+        p.extent = make_hipExtent((size_t)c.width, (size_t)c.rows, (size_t)n);
+        p.kind = kind;
+        if (hipMemcpy3DAsync(&p, s) == hipSuccess) return;
+        (void)hipGetLastError();  // refused shape (nothing enqueued): the same rows as per-stripe 2D copies
+        for (int64_t t = 0; t < n; ++t)
+            copy_rows(h2d ? dev + t * dev_stripe : host + t * host_stripe, h2d ? c.dev_pitch : c.host_pitch,
+                      h2d ? host + t * host_stripe : dev + t * dev_stripe, h2d ? c.host_pitch : c.dev_pitch, c.width,
+                      c.rows, kind, s);
+        return;
+    }
+    if (h2d) copy_rows(dev, c.dev_pitch, host, c.host_pitch, c.width, n * c.rows, kind, s);
+    else copy_rows(host, c.host_pitch, dev, c.dev_pitch, c.width, n * c.rows, kind, s);
 }
 
 // Per-device streams, buffer sets and events of the host-batch pipeline.
@@ -203,8 +269,6 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     CompiledMap &cc = cm.compact();
     const Plan pl = make_plan(cm, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes,
                               nbytes, true);
-    const std::vector<Run> &rin = pl.rin, &rout = pl.rout;
-    const Fold &fin = pl.fin, &fout = pl.fout;
     const int64_t in_per = pl.in_per, out_per = pl.out_per, chunk = pl.chunk, nchunks = pl.nchunks;
     const int nb = pl.nb;
 
@@ -216,23 +280,17 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
             HostPipe::Set &b = p.sets[(size_t)(i % nb)];
             const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
             if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
-            for (size_t j = 0; j < fin.period; ++j) {
-                const Run &r = rin[j];
-                copy_rows(b.in + r.compact0 * nbytes, fin.dev_pitch, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
-                          fin.host_pitch, r.len * nbytes, n * fin.count, hipMemcpyHostToDevice, p.h2d);
-            }
+            for (const Copy &c : pl.cin)
+                issue_copy(c, in + lo * in_stripe_stride, b.in, in_stripe_stride, in_per, n, hipMemcpyHostToDevice, p.h2d);
             check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
             if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");
             launch_apply(cc, b.in, in_per, nbytes, b.out, out_per, nbytes, n, nbytes, p.cmp);
             check_hip(hipEventRecord(b.computed, p.cmp), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.d2h, b.computed, 0), "hipStreamWaitEvent");
-            for (size_t j = 0; j < fout.period; ++j) {
-                const Run &r = rout[j];
-                copy_rows(out + lo * out_stripe_stride + r.slot0 * out_slot_stride, fout.host_pitch,
-                          b.out + r.compact0 * nbytes, fout.dev_pitch, r.len * nbytes, n * fout.count,
-                          hipMemcpyDeviceToHost, p.d2h);
-            }
+            for (const Copy &c : pl.cout)
+                issue_copy(c, out + lo * out_stripe_stride, b.out, out_stripe_stride, out_per, n, hipMemcpyDeviceToHost,
+                           p.d2h);
             check_hip(hipEventRecord(b.drained, p.d2h), "hipEventRecord");
         }
         check_hip(hipStreamSynchronize(p.d2h), "hipStreamSynchronize (host batch)");
@@ -251,10 +309,10 @@ HostBatchPlan plan_host_batch(CompiledMap &cm, int64_t in_stripe_stride, int64_t
     hp.chunk = pl.chunk;
     hp.nchunks = pl.nchunks;
     hp.buffers = pl.nb;
-    hp.h2d_copies = (int64_t)pl.fin.period;
-    hp.h2d_rows = pl.fin.count;
-    hp.d2h_copies = (int64_t)pl.fout.period;
-    hp.d2h_rows = pl.fout.count;
+    hp.h2d_copies = (int64_t)pl.cin.size();
+    hp.d2h_copies = (int64_t)pl.cout.size();
+    for (const Copy &c : pl.cin) hp.h2d_rows = std::max(hp.h2d_rows, c.rows), hp.h2d_3d += c.three_d;
+    for (const Copy &c : pl.cout) hp.d2h_rows = std::max(hp.d2h_rows, c.rows), hp.d2h_3d += c.three_d;
     return hp;
 }
 
@@ -271,8 +329,6 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
     // output area, and only those bytes come back.
     CompiledMap &cc = cm.compact();
     const Plan pl = make_plan(cm, in_stripe_stride, in_slot_stride, 0, 0, nstripes, nbytes, false);
-    const std::vector<Run> &rin = pl.rin;
-    const Fold &fin = pl.fin;
     const int64_t in_per = pl.in_per, chunk = pl.chunk, nchunks = pl.nchunks;
     const int nb = pl.nb;
 
@@ -284,11 +340,8 @@ void run_host_check_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_
             HostPipe::Set &b = p.sets[(size_t)(i % nb)];
             const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
             if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
-            for (size_t j = 0; j < fin.period; ++j) {
-                const Run &r = rin[j];
-                copy_rows(b.in + r.compact0 * nbytes, fin.dev_pitch, in + lo * in_stripe_stride + r.slot0 * in_slot_stride,
-                          fin.host_pitch, r.len * nbytes, n * fin.count, hipMemcpyHostToDevice, p.h2d);
-            }
+            for (const Copy &c : pl.cin)
+                issue_copy(c, in + lo * in_stripe_stride, b.in, in_stripe_stride, in_per, n, hipMemcpyHostToDevice, p.h2d);
             check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
             if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");

@@ -19,12 +19,12 @@ void run_host_check_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in
                                   const int *devices, int ndev);
 
 // How run_host_batch moves a batch (ecx_map_host_plan, include/ecx_tune.h): stripes per chunk, the
-// chunk count, device buffer sets in flight, and per chunk the strided H2D / D2H copies and the
-// rows each copy moves per stripe (> 1 where periodic runs are folded into one copy).
+// chunk count, device buffer sets in flight, and per chunk the H2D / D2H copies, the most rows per
+// stripe one copy moves (> 1 where runs are folded or copied in 3D) and how many copies are 3D.
 struct HostBatchPlan {
     int64_t chunk = 0, nchunks = 0;
     int buffers = 0;
-    int64_t h2d_copies = 0, h2d_rows = 0, d2h_copies = 0, d2h_rows = 0;
+    int64_t h2d_copies = 0, h2d_rows = 0, d2h_copies = 0, d2h_rows = 0, h2d_3d = 0, d2h_3d = 0;
 };
 HostBatchPlan plan_host_batch(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride,
                               int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes);
