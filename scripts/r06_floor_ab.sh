@@ -1,3 +1,4 @@
+# (the ECX_AB_* override existed only for this A/B; the measured winner is now fixed in host_pipe.cpp.)
 # After 3D copies: does the many-run chunk floor still pay?  ECX_AB_FLOOR=1 (this A/B only) keys the
 # 160-stripe floor on the planned copies per chunk instead of the runs per stripe, which drops it for
 # Clay(10,4) (3 copies) and Clay(4,2) {0,3} (1 copy).  A B B A.
