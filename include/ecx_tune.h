@@ -219,12 +219,14 @@ int ecx_map_layout_choice(const struct ecx_map *map, int64_t slot_pitch, float *
  * finds the probe already finished does not count).  Either pointer may be NULL. */
 int ecx_map_layout_state(const struct ecx_map *map, int64_t slot_pitch, int *state, int *dropped);
 /* How ecx_map_apply_batch_host would move a batch of this layout (host_pipe.cpp; host-only, no
- * device touched): plan[9] = {stripes per pipelined chunk, chunks, device buffer sets in flight,
+ * device touched): plan[10] = {stripes per pipelined chunk, chunks, device buffer sets in flight,
  * H2D copies per chunk, the most rows per stripe one H2D copy moves, D2H copies per chunk, the
- * same for D2H, H2D copies that are 3D, D2H copies that are 3D}.  Runs of used slots that repeat
- * with a fixed step across the stripe are folded into one 2D copy per period, other progressions
- * of equal runs at fixed steps are one 3D copy each (rows per stripe > 1).  All zero when the
- * batch moves nothing (no stripes, no bytes, nothing to write). */
+ * same for D2H, H2D copies that are 3D, D2H copies that are 3D, column slices}.  Runs of used
+ * slots that repeat with a fixed step across the stripe are folded into one 2D copy per period,
+ * other progressions of equal runs at fixed steps are one 3D copy each (rows per stripe > 1).  A
+ * batch that fits one chunk of stripes but holds at least 4 chunks of input is pipelined over
+ * column slices of ~host_chunk_kib instead (slices > 1; the copies are then per slice: one per
+ * progression of runs per stripe).  All zero when the batch moves nothing. */
 int ecx_map_host_plan(const struct ecx_map *map, int64_t in_stripe_stride, int64_t in_slot_stride,
                       int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t byte_count,
                       int64_t *plan);

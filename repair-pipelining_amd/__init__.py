@@ -524,10 +524,11 @@ class GfMap:
         f = lib().ecx_map_host_plan
         f.argtypes = [ctypes.c_void_p] + [ctypes.c_int64] * 6 + [ctypes.c_void_p]
         f.restype = ctypes.c_int
-        out = np.zeros(9, np.int64)
+        out = np.zeros(10, np.int64)
         check(f(self._h, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes, byte_count,
                 out.ctypes.data))
-        keys = ("chunk", "chunks", "buffers", "h2d_copies", "h2d_rows", "d2h_copies", "d2h_rows", "h2d_3d", "d2h_3d")
+        keys = ("chunk", "chunks", "buffers", "h2d_copies", "h2d_rows", "d2h_copies", "d2h_rows", "h2d_3d", "d2h_3d",
+                "slices")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def layout_state(self, slot_pitch: int):

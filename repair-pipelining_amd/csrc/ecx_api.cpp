@@ -1694,8 +1694,8 @@ int ecx_map_host_plan(const ecx_map *map, int64_t in_stripe_stride, int64_t in_s
         if (nstripes < 0 || byte_count < 0) throw Error(ECX_E_ILLEGAL_ARGUMENT, "negative count");
         const HostBatchPlan hp = plan_host_batch(const_cast<ecx_map *>(map)->cm, in_stripe_stride, in_slot_stride,
                                                  out_stripe_stride, out_slot_stride, nstripes, byte_count);
-        const int64_t v[9] = {hp.chunk, hp.nchunks, hp.buffers, hp.h2d_copies, hp.h2d_rows, hp.d2h_copies,
-                              hp.d2h_rows, hp.h2d_3d, hp.d2h_3d};
+        const int64_t v[10] = {hp.chunk, hp.nchunks, hp.buffers, hp.h2d_copies, hp.h2d_rows, hp.d2h_copies,
+                               hp.d2h_rows, hp.h2d_3d, hp.d2h_3d, hp.slices};
         std::memcpy(plan, v, sizeof(v));
         return ECX_OK;
     });

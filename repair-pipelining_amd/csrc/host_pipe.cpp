@@ -110,12 +110,43 @@ std::vector<Copy> plan_copies(const std::vector<Run> &runs, int64_t stripe_strid
     return cs;
 }
 
+// A progression of equal runs -- runs i..j of one length, `ds` host slots and `dc` compact slots
+// apart -- for the column-sliced copies below.
+struct Segment {
+    size_t i, j;
+    int64_t ds, dc;
+};
+
+std::vector<Segment> segments_of(const std::vector<Run> &runs) {
+    std::vector<Segment> sg;
+    for (size_t i = 0; i < runs.size();) {
+        size_t j = i;
+        int64_t ds = 0, dc = 0;
+        if (i + 1 < runs.size() && runs[i + 1].len == runs[i].len) {
+            ds = runs[i + 1].slot0 - runs[i].slot0;
+            dc = runs[i + 1].compact0 - runs[i].compact0;
+            while (j + 1 < runs.size() && runs[j + 1].len == runs[i].len && runs[j + 1].slot0 - runs[j].slot0 == ds &&
+                   runs[j + 1].compact0 - runs[j].compact0 == dc)
+                ++j;
+        }
+        sg.push_back({i, j, ds, dc});
+        i = j + 1;
+    }
+    return sg;
+}
+
 // The chunking and copy plan of one host batch (run_host_batch; run_host_check_batch, whose only
-// output is one verdict byte per stripe).
+// output is one verdict byte per stripe).  A batch whose stripes all fit one chunk but carry far
+// more than a chunk of input (config 4 with 1 MiB sub-chunks: one 3.5 GiB stripe per call) is cut
+// into column slices instead -- bytes [c0, c0 + slice) of every slot, the map being bytewise --
+// so its H2D, kernel and D2H still overlap, the way the reference's repair pipelining slices a
+// block (PipelineUtil.kt:13-28).
 struct Plan {
     std::vector<Run> rin, rout;
     std::vector<Copy> cin, cout;
+    std::vector<Segment> sin, sout;  // the runs' progressions, for column slices
     int64_t in_per = 0, out_per = 0, chunk = 1, nchunks = 0;
+    int64_t slice = 0, nslices = 1;  // column slices (slice 0: whole slots)
     int nb = 1;
 };
 
@@ -149,6 +180,17 @@ Plan make_plan(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride
     pl.nchunks = nchunks;
     pl.nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), std::max<int64_t>(1, nchunks));
     if (outputs) pl.cout = plan_copies(pl.rout, out_stripe_stride, out_slot_stride, pl.out_per, nbytes);
+    constexpr int64_t kSliceAlign = 4096;
+    if (outputs && nchunks == 1 && nbytes >= 2 * kSliceAlign && nstripes * in_per >= 4 * t.host_chunk) {
+        const int64_t want = (nstripes * in_per + t.host_chunk - 1) / t.host_chunk;  // slices of ~host_chunk
+        int64_t w = (nbytes + want - 1) / want;
+        w = (w + kSliceAlign - 1) / kSliceAlign * kSliceAlign;
+        pl.slice = std::min(w, nbytes);
+        pl.nslices = (nbytes + pl.slice - 1) / pl.slice;
+        pl.sin = segments_of(rin);
+        pl.sout = segments_of(pl.rout);
+        pl.nb = (int)std::min<int64_t>(std::max(1, std::min(t.host_buffers, 8)), pl.nslices);
+    }
     return pl;
 }
 
@@ -197,6 +239,40 @@ void issue_copy(const Copy &c, const uint8_t *host_base, uint8_t *dev_base, int6
     }
     if (h2d) copy_rows(dev, c.dev_pitch, host, c.host_pitch, c.width, n * c.rows, kind, s);
     else copy_rows(host, c.host_pitch, dev, c.dev_pitch, c.width, n * c.rows, kind, s);
+}
+
+// Bytes [c0, c0 + w) of every used slot of `n` stripes between the host layout (stripe stride
+// host_stripe, slot stride slot_stride) and a compact device slice ([stripe][used slot][w]): per
+// stripe, each progression of runs is one 3D copy -- w bytes of each of a run's slots (slot_stride
+// apart), runs ds slots apart -- or a 2D copy for a lone run.
+void issue_sliced(const std::vector<Run> &runs, const std::vector<Segment> &segs, const uint8_t *host_base,
+                  uint8_t *dev_base, int64_t host_stripe, int64_t slot_stride, int64_t used, int64_t n, int64_t w,
+                  hipMemcpyKind kind, hipStream_t s) {
+    const bool h2d = kind == hipMemcpyHostToDevice;
+    for (int64_t t = 0; t < n; ++t)
+        for (const Segment &g : segs) {
+            const Run &r = runs[g.i];
+            uint8_t *host = const_cast<uint8_t *>(host_base) + t * host_stripe + r.slot0 * slot_stride;
+            uint8_t *dev = dev_base + (t * used + r.compact0) * w;
+            if (g.j > g.i) {
+                hipMemcpy3DParms p;
+                std::memset(&p, 0, sizeof(p));
+                const hipPitchedPtr hptr = make_hipPitchedPtr(host, (size_t)slot_stride, (size_t)w, (size_t)g.ds);
+                const hipPitchedPtr dptr = make_hipPitchedPtr(dev, (size_t)w, (size_t)w, (size_t)g.dc);
+                p.srcPtr = h2d ? hptr : dptr;
+                p.dstPtr = h2d ? dptr : hptr;
+                p.extent = make_hipExtent((size_t)w, (size_t)r.len, g.j - g.i + 1);
+                p.kind = kind;
+                if (hipMemcpy3DAsync(&p, s) == hipSuccess) continue;
+                (void)hipGetLastError();  // refused shape (nothing enqueued): run by run
+            }
+            for (size_t k = g.i; k <= g.j; ++k) {
+                uint8_t *hk = host + (runs[k].slot0 - r.slot0) * slot_stride;
+                uint8_t *dk = dev + (runs[k].compact0 - r.compact0) * w;
+                if (h2d) copy_rows(dk, w, hk, slot_stride, w, runs[k].len, kind, s);
+                else copy_rows(hk, slot_stride, dk, w, w, runs[k].len, kind, s);
+            }
+        }
 }
 
 // Per-device streams, buffer sets and events of the host-batch pipeline.
@@ -269,28 +345,44 @@ void run_host_batch(CompiledMap &cm, const uint8_t *in, int64_t in_stripe_stride
     CompiledMap &cc = cm.compact();
     const Plan pl = make_plan(cm, in_stripe_stride, in_slot_stride, out_stripe_stride, out_slot_stride, nstripes,
                               nbytes, true);
-    const int64_t in_per = pl.in_per, out_per = pl.out_per, chunk = pl.chunk, nchunks = pl.nchunks;
+    const int64_t in_per = pl.in_per, out_per = pl.out_per, chunk = pl.chunk;
     const int nb = pl.nb;
+    const bool sliced = pl.nslices > 1;
+    const int64_t units = sliced ? pl.nslices : pl.nchunks;
+    const int64_t used_in = (int64_t)cm.used_in_slots().size(), used_out = (int64_t)cm.used_out_slots().size();
 
     HostPipe &p = HostPipe::current();
     std::lock_guard<std::mutex> lk(p.mu);
     try {
-        p.ensure(nb, (size_t)(chunk * in_per), (size_t)(chunk * out_per));
-        for (int64_t i = 0; i < nchunks; ++i) {
+        if (sliced) p.ensure(nb, (size_t)(nstripes * used_in * pl.slice), (size_t)(nstripes * used_out * pl.slice));
+        else p.ensure(nb, (size_t)(chunk * in_per), (size_t)(chunk * out_per));
+        for (int64_t i = 0; i < units; ++i) {
             HostPipe::Set &b = p.sets[(size_t)(i % nb)];
-            const int64_t lo = i * chunk, n = std::min(chunk, nstripes - lo);
+            // a chunk of whole-slot stripes, or (sliced) bytes [c0, c0 + w) of every stripe
+            const int64_t lo = sliced ? 0 : i * chunk, n = sliced ? nstripes : std::min(chunk, nstripes - lo);
+            const int64_t c0 = sliced ? i * pl.slice : 0, w = sliced ? std::min(pl.slice, nbytes - c0) : nbytes;
+            const int64_t in_ss = sliced ? used_in * w : in_per, out_ss = sliced ? used_out * w : out_per;
             if (i >= nb) check_hip(hipStreamWaitEvent(p.h2d, b.computed, 0), "hipStreamWaitEvent");
-            for (const Copy &c : pl.cin)
-                issue_copy(c, in + lo * in_stripe_stride, b.in, in_stripe_stride, in_per, n, hipMemcpyHostToDevice, p.h2d);
+            if (sliced)
+                issue_sliced(pl.rin, pl.sin, in + c0, b.in, in_stripe_stride, in_slot_stride, used_in, n, w,
+                             hipMemcpyHostToDevice, p.h2d);
+            else
+                for (const Copy &c : pl.cin)
+                    issue_copy(c, in + lo * in_stripe_stride, b.in, in_stripe_stride, in_per, n, hipMemcpyHostToDevice,
+                               p.h2d);
             check_hip(hipEventRecord(b.loaded, p.h2d), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.cmp, b.loaded, 0), "hipStreamWaitEvent");
             if (i >= nb) check_hip(hipStreamWaitEvent(p.cmp, b.drained, 0), "hipStreamWaitEvent");
-            launch_apply(cc, b.in, in_per, nbytes, b.out, out_per, nbytes, n, nbytes, p.cmp);
+            launch_apply(cc, b.in, in_ss, w, b.out, out_ss, w, n, w, p.cmp);
             check_hip(hipEventRecord(b.computed, p.cmp), "hipEventRecord");
             check_hip(hipStreamWaitEvent(p.d2h, b.computed, 0), "hipStreamWaitEvent");
-            for (const Copy &c : pl.cout)
-                issue_copy(c, out + lo * out_stripe_stride, b.out, out_stripe_stride, out_per, n, hipMemcpyDeviceToHost,
-                           p.d2h);
+            if (sliced)
+                issue_sliced(pl.rout, pl.sout, out + c0, b.out, out_stripe_stride, out_slot_stride, used_out, n, w,
+                             hipMemcpyDeviceToHost, p.d2h);
+            else
+                for (const Copy &c : pl.cout)
+                    issue_copy(c, out + lo * out_stripe_stride, b.out, out_stripe_stride, out_per, n,
+                               hipMemcpyDeviceToHost, p.d2h);
             check_hip(hipEventRecord(b.drained, p.d2h), "hipEventRecord");
         }
         check_hip(hipStreamSynchronize(p.d2h), "hipStreamSynchronize (host batch)");
@@ -313,6 +405,12 @@ HostBatchPlan plan_host_batch(CompiledMap &cm, int64_t in_stripe_stride, int64_t
     hp.d2h_copies = (int64_t)pl.cout.size();
     for (const Copy &c : pl.cin) hp.h2d_rows = std::max(hp.h2d_rows, c.rows), hp.h2d_3d += c.three_d;
     for (const Copy &c : pl.cout) hp.d2h_rows = std::max(hp.d2h_rows, c.rows), hp.d2h_3d += c.three_d;
+    hp.slices = pl.nslices;
+    if (pl.nslices > 1) {  // per slice: a copy per progression per stripe
+        hp.buffers = pl.nb;
+        hp.h2d_copies = (int64_t)pl.sin.size() * nstripes;
+        hp.d2h_copies = (int64_t)pl.sout.size() * nstripes;
+    }
     return hp;
 }
 

@@ -25,6 +25,7 @@ struct HostBatchPlan {
     int64_t chunk = 0, nchunks = 0;
     int buffers = 0;
     int64_t h2d_copies = 0, h2d_rows = 0, d2h_copies = 0, d2h_rows = 0, h2d_3d = 0, d2h_3d = 0;
+    int64_t slices = 0;  // column slices of a one-chunk batch (1: whole slots)
 };
 HostBatchPlan plan_host_batch(CompiledMap &cm, int64_t in_stripe_stride, int64_t in_slot_stride,
                               int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes, int64_t nbytes);

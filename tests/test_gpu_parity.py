@@ -2728,6 +2728,45 @@ def test_host_batch_folded_runs_match_device_batch(ecx, torch_dev, small):
         ecx.tune("host_chunk_kib", 65536)
 
 
+def test_host_batch_column_slices_match_device_batch(ecx, torch_dev):
+    """A one-stripe host batch far larger than a chunk is pipelined in column slices (host_pipe.cpp:
+    bytes [c0, c0 + slice) of every slot per unit, 3D copies per progression of runs): with 16 KiB
+    chunks that happens at small sizes, so a Clay(4,2) repair with a ragged last slice, a shortened
+    Clay(10,4) repair of node 3 (runs in 3D) and an in-place RS(12,4) decode on a padded pitch (one
+    slot per run, the output slots between inputs) equal the device batch, with nothing outside the
+    written slots' bytes touched."""
+    torch = torch_dev
+    ecx.tune("host_chunk_kib", 16)
+    try:
+        for k, m, v, er, B in [(4, 2, 0, [1], 3 * 4096 + 100), (10, 4, 2, [3], 2 * 4096 + 24)]:
+            step = ecx.ClayCodeErasureDecodingStep(er, k, m, virtualUnits=v)
+            a = step.map().info()["n_out"] // len(er)
+            n = k + m
+            assert step.map().host_plan(n * a * B, B, a * B, B, 1, B)["slices"] > 1
+            src = torch.empty((1, n * a, B), dtype=torch.uint8, device="cuda")
+            ecx.fill_random(src, src.numel(), 77 + B)
+            dev_out = torch.empty((1, a, B), dtype=torch.uint8, device="cuda")
+            step.performCodingBatch(src, n * a * B, B, dev_out, a * B, B, 1, B)
+            torch.cuda.synchronize()
+            host_out = np.full((1, a, B), 0x3C, np.uint8)
+            step.performCodingBatchHost(src.cpu().numpy(), n * a * B, B, host_out, a * B, B, 1, B)
+            assert (host_out == dev_out.cpu().numpy()).all(), (k, m, er, B)
+        rs = ecx.ReedSolomon.create(12, 4)
+        L, P = 5 * 4096 + 7, 5 * 4096 + 64
+        present = [False, True, True, False] + [True] * 12
+        dmap = rs.decode_map(present)
+        assert dmap.host_plan(16 * P, P, 16 * P, P, 1, L)["slices"] > 1
+        rng = np.random.default_rng(12)
+        host = rng.integers(0, 256, (1, 16, P), dtype=np.uint8)
+        dev = torch.from_numpy(host.copy()).cuda()
+        dmap.apply_batch(dev, 16 * P, P, dev, 16 * P, P, 1, L)
+        torch.cuda.synchronize()
+        dmap.apply_batch_host(host, 16 * P, P, host, 16 * P, P, 1, L)
+        assert (host == dev.cpu().numpy()).all()
+    finally:
+        ecx.tune("host_chunk_kib", 65536)
+
+
 def test_host_check_batch_random_layouts(ecx):
     """isParityCorrectBatchHost(Devices) over 24 random layouts -- RS(k, m) with k + m <= 24,
     shard lengths 1 .. 20,000 B, byte windows at random offsets, padded pitches, 1 .. 9 stripes,

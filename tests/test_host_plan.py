@@ -30,7 +30,7 @@ def test_headline_layout_keeps_64_mib_chunks(ecx, default_chunks):
     slots apart are one 3D copy; 20 x 32 KiB of input per stripe -> 102 stripes per 64 MiB chunk."""
     p = clay_plan(ecx, 4, 2, 0, [1], 32768, 2048)
     assert p == {"chunk": 102, "chunks": 21, "buffers": 3, "h2d_copies": 3, "h2d_rows": 3, "d2h_copies": 1,
-                 "d2h_rows": 1, "h2d_3d": 1, "d2h_3d": 0}
+                 "d2h_rows": 1, "h2d_3d": 1, "d2h_3d": 0, "slices": 1}
 
 
 def test_two_node_repair_folds_to_one_copy_per_chunk(ecx, default_chunks):
@@ -81,3 +81,15 @@ def test_small_chunks_and_empty_batches(ecx):
         ecx.tune("host_chunk_kib", 65536)
     assert set(clay_plan(ecx, 4, 2, 0, [1], 2048, 0).values()) == {0}
     assert set(clay_plan(ecx, 4, 2, 0, [1], 0, 5).values()) == {0}
+
+
+def test_one_huge_stripe_is_pipelined_in_column_slices(ecx, default_chunks):
+    """Config 4 with 1 MiB sub-chunks: one 3.5 GiB stripe per call, 832 MiB of input -- one chunk of
+    stripes, so the batch is cut into 13 column slices of 80 KiB (~64 MiB of input each, 4 KiB
+    multiples, the last 64 KiB) that run through the ring; per slice each progression of runs is one
+    copy.  A batch of a few ordinary stripes is not sliced."""
+    p = clay_plan(ecx, 10, 4, 2, [3], 1 << 20, 1)
+    assert p["slices"] == 13 and p["buffers"] == 3 and p["chunks"] == 1
+    assert p["h2d_copies"] == 3 and p["d2h_copies"] == 1
+    q = clay_plan(ecx, 10, 4, 2, [3], 4096, 12)  # 12 x 3.4 MB: one chunk, less than 4 chunks of input
+    assert q["slices"] == 1
