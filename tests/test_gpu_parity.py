@@ -2767,6 +2767,51 @@ def test_host_batch_column_slices_match_device_batch(ecx, torch_dev):
         ecx.tune("host_chunk_kib", 65536)
 
 
+def test_host_batch_random_layouts_match_device_batch(ecx, torch_dev):
+    """apply_batch_host over 60 random layouts against apply_batch on the device, same bytes: random
+    maps (1-24 inputs, 1-6 outputs, slot sets with gaps, repeats of a period or none), slot pitches
+    equal to or above the byte count, stripe strides with slack, ragged byte counts, 1-9 stripes,
+    and host_chunk_kib 16 / 64 / 65536 -- so every copy plan of host_pipe.cpp runs: merged runs,
+    folded 2D periods, 3D progressions, lone runs, many chunks and column slices.  Outputs go to a
+    separate buffer pre-filled with a marker that must survive outside the written slots."""
+    torch = torch_dev
+    rng = np.random.default_rng(20261019)
+    try:
+        for case in range(60):
+            n_slots = int(rng.integers(2, 40))
+            n_in = int(rng.integers(1, min(24, n_slots) + 1))
+            if rng.random() < 0.4:  # a periodic slot set: every `step`-th group of `g` slots
+                g = int(rng.integers(1, 4))
+                step = g + int(rng.integers(1, 4))
+                ins = [b + j for b in range(0, n_slots, step) for j in range(g) if b + j < n_slots][:n_in]
+            else:
+                ins = sorted(rng.choice(n_slots, n_in, replace=False).tolist())
+            n_in = len(ins)
+            n_out_slots = int(rng.integers(1, 12))
+            n_out = int(rng.integers(1, min(6, n_out_slots) + 1))
+            outs = sorted(rng.choice(n_out_slots, n_out, replace=False).tolist())
+            M = rng.integers(0, 256, (n_out, n_in), dtype=np.uint8)
+            gm = ecx.GfMap.from_matrix(M, ins, outs)
+            L = int(rng.choice([1, 100, 4096, 5000, 12288, 20000]))
+            pitch = L + int(rng.choice([0, 0, 16, 4096]))
+            S = 1 if rng.random() < 0.3 else int(rng.integers(2, 10))  # one stripe: column slices
+            in_ss = n_slots * pitch + int(rng.choice([0, 0, 64]))
+            out_pitch = L + int(rng.choice([0, 32]))
+            out_ss = n_out_slots * out_pitch + int(rng.choice([0, 128]))
+            ecx.tune("host_chunk_kib", int(rng.choice([16, 64, 65536])))
+            host_in = rng.integers(0, 256, S * in_ss, dtype=np.uint8)
+            host_out = np.full(S * out_ss, 0xA5, np.uint8)
+            dev_in = torch.from_numpy(host_in.copy()).cuda()
+            dev_out = torch.full((S * out_ss,), 0xA5, dtype=torch.uint8, device="cuda")
+            gm.apply_batch(dev_in, in_ss, pitch, dev_out, out_ss, out_pitch, S, L)
+            torch.cuda.synchronize()
+            gm.apply_batch_host(host_in, in_ss, pitch, host_out, out_ss, out_pitch, S, L)
+            want = dev_out.cpu().numpy()
+            assert (host_out == want).all(), (case, ins, outs, L, pitch, S, in_ss, out_pitch, out_ss)
+    finally:
+        ecx.tune("host_chunk_kib", 65536)
+
+
 def test_host_check_batch_random_layouts(ecx):
     """isParityCorrectBatchHost(Devices) over 24 random layouts -- RS(k, m) with k + m <= 24,
     shard lengths 1 .. 20,000 B, byte windows at random offsets, padded pitches, 1 .. 9 stripes,
