@@ -320,7 +320,9 @@ int ecx_clay_perform_coding_batch_host(ecx_clay *clay, const uint8_t *in, int64_
  * buffer ring per GPU).  Device j of `devices` (ndev entries, HIP ordinals; repeats allowed)
  * takes the contiguous stripe range [j*S/ndev, (j+1)*S/ndev) (the remainder spread over the
  * first ranges, as shard_stripes), on a worker thread of its own; the call returns when every
- * worker has finished.  An out-of-range device id or ndev <= 0 is refused
+ * worker has finished.  With fewer stripes than entries (one or two huge stripes) the entries
+ * split the bytes of every slot instead, in 4 KiB units, so each still moves a share over its
+ * own link.  An out-of-range device id or ndev <= 0 is refused
  * (ECX_E_ILLEGAL_ARGUMENT) before anything is copied; on a failure every device is drained and
  * the first failing device's status is returned.  The calling thread's current device is
  * unchanged. */
@@ -337,7 +339,8 @@ int ecx_clay_perform_coding_batch_host_devices(ecx_clay *clay, const uint8_t *in
  * H2D and through the read-only check kernel, and only the verdict bytes come back --
  * verdict[s] (a host byte array of nstripes) = 1 when stripe s's parity is correct over bytes
  * [offset, offset + byte_count), else 0.  Synchronous; the _devices form splits the stripes
- * over a device list exactly as ecx_map_apply_batch_host_devices does. */
+ * over a device list as ecx_map_apply_batch_host_devices does (always by stripes: a verdict
+ * covers a whole stripe). */
 int ecx_rs_is_parity_correct_batch_host(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride,
                                         int64_t shard_stride, int64_t nstripes, int64_t offset,
                                         int64_t byte_count, uint8_t *verdict);

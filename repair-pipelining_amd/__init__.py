@@ -566,7 +566,8 @@ class GfMap:
                                  out_slot_stride, nstripes, byte_count, devices):
         """apply_batch_host split over several GPUs (ecx_map_apply_batch_host_devices): device j
         of ``devices`` takes the contiguous stripe range shard_stripes(nstripes, len(devices), j)
-        on a worker thread of its own; synchronous."""
+        on a worker thread of its own -- or, with fewer stripes than entries, a contiguous range of
+        every slot's bytes (4 KiB units); synchronous."""
         self._check(inp, in_stripe_stride, in_slot_stride, out, out_stripe_stride, out_slot_stride, nstripes,
                     byte_count)
         devs = list(devices)
@@ -958,8 +959,9 @@ class ClayCodeErasureDecodingStep:
     def performCodingBatchHostDevices(self, inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride,
                                       out_sub_stride, nstripes, bufSize, devices) -> None:
         """performCodingBatchHost split over several GPUs of this process
-        (ecx_clay_perform_coding_batch_host_devices): contiguous stripe ranges, one worker
-        thread and pipe per device entry."""
+        (ecx_clay_perform_coding_batch_host_devices): contiguous stripe ranges (byte ranges of
+        every sub-chunk when there are fewer stripes than entries), one worker thread and pipe per
+        device entry."""
         self._check_batch(inp, in_stripe_stride, in_sub_stride, out, out_stripe_stride, out_sub_stride, nstripes,
                           bufSize)
         devs = list(devices)

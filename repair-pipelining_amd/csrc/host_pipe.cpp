@@ -526,6 +526,17 @@ void run_host_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in_strip
                             uint8_t *out, int64_t out_stripe_stride, int64_t out_slot_stride, int64_t nstripes,
                             int64_t nbytes, const int *devices, int ndev) {
     if (nbytes <= 0 || cm.map().n_out == 0) nstripes = 0;  // validate the list, touch nothing
+    // Fewer stripes than device entries (one or two huge stripes): split the bytes of every slot
+    // instead, in 4 KiB units -- the map is bytewise -- so every entry's link still carries a share.
+    constexpr int64_t kColUnit = 4096;
+    if (nstripes > 0 && nstripes < ndev && nbytes >= 2 * kColUnit) {
+        on_devices(devices, ndev, (nbytes + kColUnit - 1) / kColUnit, [&](int64_t u0, int64_t nu) {
+            const int64_t c0 = u0 * kColUnit, w = std::min(nu * kColUnit, nbytes - c0);
+            run_host_batch(cm, in + c0, in_stripe_stride, in_slot_stride, out + c0, out_stripe_stride, out_slot_stride,
+                           nstripes, w);
+        });
+        return;
+    }
     on_devices(devices, ndev, nstripes, [&](int64_t lo, int64_t n) {
         run_host_batch(cm, in + lo * in_stripe_stride, in_stripe_stride, in_slot_stride, out + lo * out_stripe_stride,
                        out_stripe_stride, out_slot_stride, n, nbytes);

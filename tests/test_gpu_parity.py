@@ -2767,6 +2767,34 @@ def test_host_batch_column_slices_match_device_batch(ecx, torch_dev):
         ecx.tune("host_chunk_kib", 65536)
 
 
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_host_batch_devices_split_columns_of_few_stripes(ecx, torch_dev, devices):
+    """Fewer stripes than device entries: ecx_*_batch_host_devices splits the bytes of every slot
+    (4 KiB units) over the entries instead of the stripes -- one Clay(4,2) stripe with a ragged byte
+    count, and two in-place RS(12,4) stripes on a padded pitch -- and writes what the device batch
+    writes, nothing else."""
+    torch = torch_dev
+    B = 5 * 4096 + 100
+    step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
+    src = torch.empty((1, 48, B), dtype=torch.uint8, device="cuda")
+    ecx.fill_random(src, src.numel(), 5150)
+    dev_out = torch.empty((1, 8, B), dtype=torch.uint8, device="cuda")
+    step.performCodingBatch(src, 48 * B, B, dev_out, 8 * B, B, 1, B)
+    torch.cuda.synchronize()
+    host_out = np.full((1, 8, B), 0x3C, np.uint8)
+    step.performCodingBatchHostDevices(src.cpu().numpy(), 48 * B, B, host_out, 8 * B, B, 1, B, devices)
+    assert (host_out == dev_out.cpu().numpy()).all()
+    rs = ecx.ReedSolomon.create(12, 4)
+    L, P, S = 3 * 4096 + 5, 3 * 4096 + 48, 2
+    dmap = rs.decode_map([False] + [True] * 14 + [False])
+    host = np.random.default_rng(3).integers(0, 256, (S, 16, P), dtype=np.uint8)
+    dev = torch.from_numpy(host.copy()).cuda()
+    dmap.apply_batch(dev, 16 * P, P, dev, 16 * P, P, S, L)
+    torch.cuda.synchronize()
+    dmap.apply_batch_host_devices(host, 16 * P, P, host, 16 * P, P, S, L, devices + [0])
+    assert (host == dev.cpu().numpy()).all()
+
+
 def test_host_batch_random_layouts_match_device_batch(ecx, torch_dev):
     """apply_batch_host over 60 random layouts against apply_batch on the device, same bytes: random
     maps (1-24 inputs, 1-6 outputs, slot sets with gaps, repeats of a period or none), slot pitches
