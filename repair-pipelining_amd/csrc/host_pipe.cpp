@@ -13,8 +13,11 @@
 //
 // Only the map's used input slots cross PCIe; the Clay(4,2) e=1 repair, for
 // example, moves 20 of the 48 sub-chunks of a stripe.  Consecutive used slots
-// that are also consecutive in host memory are merged into one strided (2D)
-// copy per chunk.
+// that are also consecutive in host memory form a run; a chunk's copies are
+// planned from the runs (make_plan): periodic runs folded into one 2D copy,
+// other progressions of equal runs in one 3D copy each, a one-chunk batch of
+// huge stripes cut into column slices, and over a device list, few stripes
+// split by byte ranges (ecx_map_host_plan reports the plan).
 #include <algorithm>
 #include <cstring>
 #include <thread>
@@ -23,7 +26,6 @@
 
 namespace ecx {
 namespace {
-
 
 struct Run {
     int slot0;     // first host slot
