@@ -200,9 +200,9 @@ int ecx_rs_encode_parity_blocked_batch_host(ecx_rs *rs, uint8_t *base, int64_t n
                                             int64_t block_bytes);
 int ecx_rs_decode_missing_blocked_batch_host(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base,
                                              int64_t nstripes, int64_t byte_count, int64_t block_bytes);
-/* The same split over several GPUs of this process (as ecx_map_apply_batch_host_devices): contiguous
- * stripe ranges, one worker thread and pipe per device entry; a range's full blocks and its tails
- * are each contiguous in the batch. */
+/* The same over several GPUs of this process: each of the two passes is split over the device
+ * entries as ecx_map_apply_batch_host_devices splits a batch -- the full blocks as nstripes * full
+ * small stripes, the tails by stripes (by byte ranges when there are fewer than entries). */
 int ecx_rs_encode_parity_blocked_batch_host_devices(ecx_rs *rs, uint8_t *base, int64_t nstripes, int64_t byte_count,
                                                     int64_t block_bytes, const int *devices, int ndev);
 int ecx_rs_decode_missing_blocked_batch_host_devices(ecx_rs *rs, const uint8_t *shard_present, uint8_t *base,

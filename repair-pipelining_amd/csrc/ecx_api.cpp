@@ -608,26 +608,16 @@ void launch_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int
 }
 
 // The same two passes from host memory: two pipelined host batches (host_pipe.cpp), the second
-// after the first has drained (each is synchronous).  With a device list (ndev > 0), contiguous
-// stripe ranges per entry: a range's full blocks and its tails are each contiguous in the batch.
+// after the first has drained (each is synchronous).  With a device list (ndev > 0) each pass is
+// split over the entries like any host batch: the full blocks as nstripes * full small stripes,
+// the tails by stripes (by byte ranges where there are fewer stripes than entries).
 void host_blocked(CompiledMap &cm, uint8_t *base, int n, int64_t nstripes, int64_t byte_count, int64_t block,
                   const int *devices = nullptr, int ndev = 0) {
-    if (ndev == 0 && !devices) {
-        blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
-            run_host_batch(cm, base + off, ss, len, base + off, ss, len, units, len);
-        });
-        return;
-    }
-    int64_t body = 0;  // the whole batch's full blocks: its extent is checked before any worker starts
-    blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t, int64_t, int64_t) { body = std::max(body, off); });
-    const int64_t full = block > 0 ? byte_count / block : 0, tail = block > 0 ? byte_count % block : 0;
-    for_device_ranges(devices, ndev, byte_count > 0 ? nstripes : 0, [&](int64_t lo, int64_t cnt) {
-        blocked_passes(n, cnt, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
-            (void)off;  // the range's own offsets; its place in the batch: the full-block pass has
-                        // slots of `block` bytes, the tail pass slots of `tail` < block bytes
-            uint8_t *p = len == block ? base + lo * full * n * block : base + body + lo * n * tail;
-            run_host_batch(cm, p, ss, len, p, ss, len, units, len);
-        });
+    const bool multi = ndev != 0 || devices;
+    if (multi) for_device_ranges(devices, ndev, 0, [](int64_t, int64_t) {});  // the list, even for an empty batch
+    blocked_passes(n, nstripes, byte_count, block, [&](int64_t off, int64_t ss, int64_t len, int64_t units) {
+        if (multi) run_host_batch_devices(cm, base + off, ss, len, base + off, ss, len, units, len, devices, ndev);
+        else run_host_batch(cm, base + off, ss, len, base + off, ss, len, units, len);
     });
 }
 }  // namespace
