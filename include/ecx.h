@@ -339,8 +339,8 @@ int ecx_clay_perform_coding_batch_host_devices(ecx_clay *clay, const uint8_t *in
  * H2D and through the read-only check kernel, and only the verdict bytes come back --
  * verdict[s] (a host byte array of nstripes) = 1 when stripe s's parity is correct over bytes
  * [offset, offset + byte_count), else 0.  Synchronous; the _devices form splits the stripes
- * over a device list as ecx_map_apply_batch_host_devices does (always by stripes: a verdict
- * covers a whole stripe). */
+ * over a device list as ecx_map_apply_batch_host_devices does; with fewer stripes than entries
+ * each entry checks a byte range of every shard, and a stripe passes when every range does. */
 int ecx_rs_is_parity_correct_batch_host(ecx_rs *rs, const uint8_t *base, int64_t stripe_stride,
                                         int64_t shard_stride, int64_t nstripes, int64_t offset,
                                         int64_t byte_count, uint8_t *verdict);

@@ -549,6 +549,28 @@ void run_host_check_batch_devices(CompiledMap &cm, const uint8_t *in, int64_t in
                                   int64_t in_slot_stride, int64_t nstripes, int64_t nbytes, uint8_t *verdict,
                                   const int *devices, int ndev) {
     if (nstripes > 0 && !verdict) throw Error(ECX_E_NULL, "verdict buffer is null");
+    // Fewer stripes than entries: each entry checks a byte range of every slot into its own
+    // verdicts, and a stripe passes when it passes in every range.
+    constexpr int64_t kColUnit = 4096;
+    if (nstripes > 0 && nstripes < ndev && nbytes >= 2 * kColUnit && cm.map().n_out > 0) {
+        const int64_t units = (nbytes + kColUnit - 1) / kColUnit;
+        std::vector<std::vector<uint8_t>> part((size_t)ndev);
+        on_devices(devices, ndev, units, [&](int64_t u0, int64_t nu) {
+            int j = 0;  // this range's entry: the one whose range starts at u0
+            for (int64_t b = 0, e = 0; j < ndev; ++j) {
+                stripe_range(units, ndev, j, &b, &e);
+                if (b == u0 && e > b) break;
+            }
+            std::vector<uint8_t> &v = part[(size_t)j];
+            v.assign((size_t)nstripes, 0);
+            const int64_t c0 = u0 * kColUnit, w = std::min(nu * kColUnit, nbytes - c0);
+            run_host_check_batch(cm, in + c0, in_stripe_stride, in_slot_stride, nstripes, w, v.data());
+        });
+        std::memset(verdict, 1, (size_t)nstripes);
+        for (const std::vector<uint8_t> &v : part)
+            for (size_t s2 = 0; s2 < v.size(); ++s2) verdict[s2] = (uint8_t)(verdict[s2] && v[s2]);
+        return;
+    }
     on_devices(devices, ndev, nstripes, [&](int64_t lo, int64_t n) {
         run_host_check_batch(cm, in + lo * in_stripe_stride, in_stripe_stride, in_slot_stride, n, nbytes,
                              verdict + lo);

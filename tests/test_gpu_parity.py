@@ -2772,7 +2772,8 @@ def test_host_batch_devices_split_columns_of_few_stripes(ecx, torch_dev, devices
     """Fewer stripes than device entries: ecx_*_batch_host_devices splits the bytes of every slot
     (4 KiB units) over the entries instead of the stripes -- one Clay(4,2) stripe with a ragged byte
     count, and two in-place RS(12,4) stripes on a padded pitch -- and writes what the device batch
-    writes, nothing else."""
+    writes, nothing else; the check ANDs the entries' verdicts, so a corrupted byte in any range
+    fails its stripe."""
     torch = torch_dev
     B = 5 * 4096 + 100
     step = ecx.ClayCodeErasureDecodingStep([1], 4, 2)
@@ -2793,6 +2794,13 @@ def test_host_batch_devices_split_columns_of_few_stripes(ecx, torch_dev, devices
     torch.cuda.synchronize()
     dmap.apply_batch_host_devices(host, 16 * P, P, host, 16 * P, P, S, L, devices + [0])
     assert (host == dev.cpu().numpy()).all()
+    # the check: one corrupted byte in the last 4 KiB of stripe 1 fails it whichever entry checks it
+    shards = host.copy()
+    rs.encode_map().apply_batch_host(shards, 16 * P, P, shards, 16 * P, P, S, L)
+    shards[1, 7, L - 3] ^= 0x5A
+    verdict = np.full(S, 9, np.uint8)
+    rs.isParityCorrectBatchHostDevices(shards, 16 * P, P, S, 0, L, verdict, devices + [0])
+    assert verdict.tolist() == [1, 0]
 
 
 def test_host_batch_random_layouts_match_device_batch(ecx, torch_dev):
