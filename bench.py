@@ -494,6 +494,9 @@ def e2e_rate(ecx, torch, wl, seconds: float, world: int = 1):
            "stripes_per_call": n, "calls": calls, "seconds": round(el, 3), "verified": ok,
            "host_bytes": n * (sb + ob), "host_cap": cap, "peak_rss_bytes": _peak_rss_bytes(),
            "path": "pinned host -> H2D -> kernel -> D2H, pipelined (ecx host batch, host_pipe.cpp)"}
+    plan = wl.host_plan(n)
+    if plan is not None:
+        out["plan"] = plan  # stripes per chunk, copies per chunk (3D, folded rows), column slices
     if wl.metric_unit != "GiB/s":
         out["value"] = round(units * (wl.metric_bytes or wl.unit_bytes) / el / wl.metric_scale, 1)
         out["unit"] = wl.metric_unit
@@ -579,6 +582,10 @@ class Workload:
     def host_call(self, hin, hout, n):
         raise NotImplementedError
 
+    def host_plan(self, n):
+        """How host_call's batch is chunked and copied (ecx_map_host_plan), or None."""
+        return None
+
     def host_expect(self, hin, hout, n) -> bool:
         """The host outputs of the first n stripes equal the device run's (compared in
         E2E_COPY_CHUNK steps: no full-size host copy of the device side)."""
@@ -641,6 +648,10 @@ class Clay42(Workload):
     def host_call(self, hin, hout, n):
         e = len(self.erased_list)
         self.step.performCodingBatchHost(hin, STRIPE_BYTES, B, hout, e * ALPHA * B, B, n, B)
+
+    def host_plan(self, n):
+        e = len(self.erased_list)
+        return self.step.map().host_plan(STRIPE_BYTES, B, e * ALPHA * B, B, n, B)
 
     def verify(self):
         return bool(self.torch.equal(self.out, self.pool.view(self.P, ALPHA, N_NODES, B)[:, :, self.erased, :]))
@@ -750,6 +761,10 @@ class Clay104(Workload):
     def host_call(self, hin, hout, n_):
         n, a, b = self.n, self.alpha, self.b
         self.step.performCodingBatchHost(hin, n * a * b, b, hout, a * b, b, n_, b)
+
+    def host_plan(self, n_):
+        n, a, b = self.n, self.alpha, self.b
+        return self.step.map().host_plan(n * a * b, b, a * b, b, n_, b)
 
     def verify(self):
         orig = self.pool.view(self.P, self.alpha, self.n, self.b)[:, :, self.erased, :]
@@ -899,6 +914,12 @@ class RS124(_RsLayout, Workload):
         p = self.pitch
         self.dmap.apply_batch_host(hin, 16 * p, p, hin, 16 * p, p, n, self.L)
 
+    def host_plan(self, n):
+        if self.layout == "blocked":
+            return None  # two passes (full blocks, tails)
+        p = self.pitch
+        return self.dmap.host_plan(16 * p, p, 16 * p, p, n, self.L)
+
     def sub_bytes(self):
         return self.L
 
@@ -978,6 +999,12 @@ class RS173(_RsLayout, Workload):
             return
         p = self.pitch
         self.rs.encode_map().apply_batch_host(hin, 20 * p, p, hin, 20 * p, p, n, self.L)
+
+    def host_plan(self, n):
+        if self.layout == "blocked":
+            return None  # two passes (full blocks, tails)
+        p = self.pitch
+        return self.rs.encode_map().host_plan(20 * p, p, 20 * p, p, n, self.L)
 
     def verify(self):
         """The parity the GPU wrote equals the oracle's on two stripes, and re-encoding
@@ -1143,6 +1170,10 @@ class LRCEncode(Workload):
         b = self.b
         self.emap.apply_batch_host(hin, 16 * b, b, hin, 16 * b, b, n, b)
 
+    def host_plan(self, n):
+        b = self.b
+        return self.emap.host_plan(16 * b, b, 16 * b, b, n, b)
+
     def verify(self):
         """Re-encoding leaves every stripe unchanged, and two stripes' parities equal the oracle's."""
         before = self.pool[:, 3::4].clone()
@@ -1216,6 +1247,10 @@ class LRC(Workload):
     def host_call(self, hin, hout, n):
         b = self.b
         self.rmap.apply_batch_host(hin, 16 * b, b, hout, b, b, n, b)
+
+    def host_plan(self, n):
+        b = self.b
+        return self.rmap.host_plan(16 * b, b, b, b, n, b)
 
     def verify(self):
         return bool(self.torch.equal(self.out[:, 0], self.pool[:, 2]))

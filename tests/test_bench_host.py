@@ -271,6 +271,7 @@ def test_e2e_leg_fills_in_chunks_within_the_budget(monkeypatch):
     wl = _bare(bench.RS173, pool=pool, L=64, P=40)
     calls = []
     wl.host_call = lambda ha, ho, n: calls.append(n)  # in place, so the host copy is already "encoded"
+    wl.host_plan = lambda n: None  # no map behind this stand-in
     full = pool.numel()
 
     class Ecx:
@@ -342,3 +343,27 @@ def test_e2e_blocked_layout_host_batch_order(monkeypatch):
     monkeypatch.setattr(bench, "E2E_HOST_BYTES", k * n * L)
     r = bench.e2e_rate(Ecx, torch, wl, 0.01, world=1)
     assert r["verified"] and r["stripes_per_call"] == k
+
+
+def test_e2e_leg_reports_the_host_plan():
+    """The e2e leg's `plan` (ecx_map_host_plan, host-only) for the bench's own layouts: the headline
+    keeps 64 MiB chunks with its runs of 5 planes in one 3D copy, Clay(10,4) node 3 takes 3 copies a
+    chunk, the two-node repair one folded copy, RS(17,3) natural one merged run, and the blocked
+    layouts (two passes) report none."""
+    import rpamd
+    ecx = rpamd.load()
+    ecx.tune("host_chunk_kib", 65536)
+    c42 = _bare(bench.Clay42, step=ecx.ClayCodeErasureDecodingStep([1], 4, 2), erased=1)
+    p = c42.host_plan(2048)
+    assert (p["chunk"], p["h2d_copies"], p["h2d_3d"], p["slices"]) == (102, 3, 1, 1)
+    c2 = _bare(bench.Clay42x2, step=ecx.ClayCodeErasureDecodingStep([0, 3], 4, 2))
+    assert (c2.host_plan(2048)["h2d_copies"], c2.host_plan(2048)["h2d_rows"]) == (1, 16)
+    c104 = _bare(bench.Clay104, step=ecx.ClayCodeErasureDecodingStep([3], 10, 4, virtualUnits=2), n=14, alpha=256,
+                 b=4096)
+    assert (c104.host_plan(219)["h2d_copies"], c104.host_plan(219)["chunk"]) == (3, 19)
+    big = _bare(bench.Clay104, step=c104.step, n=14, alpha=256, b=1 << 20)
+    assert big.host_plan(1)["slices"] == 13
+    rs = ecx.ReedSolomon.create(17, 3)
+    r173 = _bare(bench.RS173, rs=rs, layout="natural", pitch=200000, L=200000)
+    assert r173.host_plan(805)["h2d_copies"] == 1
+    assert _bare(bench.RS173, rs=rs, layout="blocked", pitch=32768, L=200000).host_plan(805) is None
